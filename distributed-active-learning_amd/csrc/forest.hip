@@ -1,0 +1,205 @@
+// Random-forest hard votes fused with the uncertainty / density-weighted score.
+//
+// Reference:
+//   per-tree predict   final_thesis/uncertainty_sampling.py:88-93,
+//                      density_weighting.py:136-141 (T Spark jobs of
+//                      DecisionTreeModel(tree).predict; MLlib 2.1 Node.predict:
+//                      continuous split x[f] <= threshold -> left)
+//   vote sum           uncertainty_sampling.py:96-97 (groupByKey().mapValues(sum))
+//   LC score           uncertainty_sampling.py:98   abs(0.5 - (1 - v/T))
+//   DW entropy         density_weighting.py:148     -(1-v/T) log2(1-v/T)
+//   density product    density_weighting.py:166-167 e * d
+// The per-row positional re-key of uncertainty_sampling.py:100-104 is not
+// needed: row i's score stays in slot i (the aligned semantics of
+// lal_direct_mllib_implementation/classes/active_learner.py:160-183).
+//
+// MI355X design: HBM-bound streaming kernel.  A block stages R pool rows into
+// LDS with coalesced loads (row stride d+1 floats: the per-lane feature
+// gathers of the traversal hit distinct banks), the forest (complete-heap SoA,
+// 8 B per inner node) is LDS-resident when it fits, and TPR = 256/R threads
+// share a row, each walking every TPR-th tree with 4 independent traversals in
+// flight (ILP over trees).  Votes are integers; the score comes from an fp64
+// look-up table indexed by v, so US scores are exact fp64 and identical to the
+// reference's Python float arithmetic.
+#include "common.hpp"
+
+namespace dal {
+namespace {
+
+constexpr int kForestThreads = 256;
+constexpr int kTreeIlp = 4;
+
+struct ForestArgs {
+  const float* x;
+  int64_t n;
+  int d;
+  int64_t ldx;
+  const int2* inner;
+  const uint8_t* leaf;
+  int n_trees;
+  int depth;
+  const double* lut;
+  const long long* density;
+  double derr;
+  const uint8_t* flags;
+  double beta;
+  int order;
+  int32_t* votes;
+  double* scores;
+  uint64_t* keys;
+  uint64_t* keys_hi;
+};
+
+__device__ __forceinline__ double density_pow(double d, double beta) {
+  return beta == 1.0 ? d : pow(d, beta);
+}
+
+// |d^beta - d'^beta| bound for |d - d'| <= derr.
+__device__ __forceinline__ double density_pow_err(double d, double derr, double beta) {
+  if (beta == 1.0) return derr;
+  const double p = pow(fabs(d), beta);
+  const double hi = pow(fabs(d) + derr, beta);
+  const double lo = pow(fmax(fabs(d) - derr, 0.0), beta);
+  return fmax(fabs(hi - p), fabs(p - lo)) * (1.0 + 1e-12) + fabs(p) * 1e-14;
+}
+
+template <bool X_LDS, bool F_LDS>
+__global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs A, int R, int tpr,
+                                                                      int x_floats) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* xs = reinterpret_cast<float*>(smem);
+  const int n_inner = (1 << A.depth) - 1;
+  const int n_leaf = 1 << A.depth;
+  const int2* inner = A.inner;
+  const uint8_t* leaf = A.leaf;
+  const int tid = threadIdx.x;
+  if (F_LDS) {
+    int2* fs = reinterpret_cast<int2*>(smem + static_cast<size_t>(x_floats) * 4);
+    uint8_t* ls = reinterpret_cast<uint8_t*>(fs + A.n_trees * n_inner);
+    for (int e = tid; e < A.n_trees * n_inner; e += kForestThreads) fs[e] = A.inner[e];
+    for (int e = tid; e < A.n_trees * n_leaf; e += kForestThreads) ls[e] = A.leaf[e];
+    inner = fs;
+    leaf = ls;
+  }
+  const int xstride = A.d + 1;
+  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * R;
+  if (X_LDS) {
+    const int64_t rows_here = min(static_cast<int64_t>(R), A.n - row0);
+    for (int e = tid; e < rows_here * A.d; e += kForestThreads) {
+      const int r = e / A.d, c = e - r * A.d;
+      xs[r * xstride + c] = A.x[(row0 + r) * A.ldx + c];
+    }
+  }
+  __syncthreads();
+
+  const int r = tid / tpr, sub = tid - r * tpr;
+  const int64_t row = row0 + r;
+  const bool live = r < R && row < A.n;
+  const float* xrow = X_LDS ? xs + r * xstride : A.x + (live ? row : 0) * A.ldx;
+
+  int v = 0;
+  if (live) {
+    int t = sub;
+    for (; t + (kTreeIlp - 1) * tpr < A.n_trees; t += kTreeIlp * tpr) {
+      int h[kTreeIlp];
+#pragma unroll
+      for (int j = 0; j < kTreeIlp; ++j) h[j] = 0;
+      for (int lvl = 0; lvl < A.depth; ++lvl) {
+#pragma unroll
+        for (int j = 0; j < kTreeIlp; ++j) {
+          const int2 nd = inner[(t + j * tpr) * n_inner + h[j]];
+          const float xv = xrow[nd.x];
+          h[j] = 2 * h[j] + (xv <= __int_as_float(nd.y) ? 1 : 2);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kTreeIlp; ++j) v += leaf[(t + j * tpr) * n_leaf + (h[j] - n_inner)];
+    }
+    for (; t < A.n_trees; t += tpr) {
+      int h = 0;
+      for (int lvl = 0; lvl < A.depth; ++lvl) {
+        const int2 nd = inner[t * n_inner + h];
+        h = 2 * h + (xrow[nd.x] <= __int_as_float(nd.y) ? 1 : 2);
+      }
+      v += leaf[t * n_leaf + (h - n_inner)];
+    }
+  }
+  // row's TPR threads are consecutive lanes
+  for (int o = 1; o < tpr; o <<= 1) v += __shfl_xor(v, o);
+  if (!live || sub != 0) return;
+
+  const uint8_t fl = A.flags ? A.flags[row] : DAL_ROW_CANDIDATE;
+  const double e = A.lut[v];
+  double s, err = 0.0;
+  if (A.density) {
+    double d = from_fixed(A.density[row]);
+    if (fl & DAL_ROW_EXCLUDED) d = __builtin_nan("");
+    s = e * density_pow(d, A.beta);
+    if (e == e && e != 0.0 && d == d) {
+      err = fabs(e) * density_pow_err(d, A.derr, A.beta);
+      // keep the interval ends distinct from s after rounding
+      err = fmax(err, fabs(s) * 4.5e-16);
+    }
+  } else {
+    s = e;
+  }
+  A.votes[row] = v;
+  A.scores[row] = s;
+  const bool cand = fl & DAL_ROW_CANDIDATE;
+  A.keys[row] = cand ? score_key(pessimistic(s, err, A.order), A.order) : DAL_KEY_NONE;
+  if (A.keys_hi) A.keys_hi[row] = cand ? score_key(optimistic(s, err, A.order), A.order) : DAL_KEY_NONE;
+}
+
+}  // namespace
+}  // namespace dal
+
+using namespace dal;
+
+extern "C" int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
+                                const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
+                                const int64_t* density, double density_err, const uint8_t* row_flags,
+                                double beta, int order, int32_t* votes, double* scores, uint64_t* keys,
+                                uint64_t* keys_hi, dal_stream_t stream) {
+  if (!x || !inner || !leaf || !lut || !votes || !scores || !keys) return DAL_ERR_ARG;
+  if (order != DAL_ASCENDING && order != DAL_DESCENDING) return DAL_ERR_ARG;
+  if (n < 0 || d < 1 || ldx < d || n_trees < 1) return DAL_ERR_SHAPE;
+  if (depth < 1 || depth > DAL_MAX_TREE_DEPTH) return DAL_ERR_UNSUPPORTED;
+  if (n == 0) return DAL_OK;
+  ForestArgs A{x, n, static_cast<int>(d), ldx, reinterpret_cast<const int2*>(inner), leaf, n_trees,
+               depth, lut, reinterpret_cast<const long long*>(density), density_err, row_flags, beta,
+               order, votes, scores, keys, keys_hi};
+  // rows per block: stage up to 64 KiB of pool rows in LDS
+  int R = 256;
+  bool x_lds = true;
+  while (R > 16 && static_cast<int64_t>(R) * (d + 1) * 4 > 65536) R >>= 1;
+  if (static_cast<int64_t>(R) * (d + 1) * 4 > 65536) {
+    x_lds = false;
+    R = 256;
+  }
+  const int tpr = kForestThreads / R;
+  const int x_floats = x_lds ? R * static_cast<int>(d + 1) : 0;
+  const int64_t n_inner = (int64_t{1} << depth) - 1, n_leaf = int64_t{1} << depth;
+  const int64_t f_bytes = n_trees * (n_inner * 8 + n_leaf);
+  const bool f_lds = f_bytes <= 65536;
+  const int xf = static_cast<int>(round_up(x_floats, 4));  // forest region 16-B aligned
+  size_t smem = static_cast<size_t>(xf) * 4 + (f_lds ? static_cast<size_t>(f_bytes) : 0);
+  if (smem == 0) smem = 16;
+  const dim3 grid(static_cast<unsigned>(ceil_div(n, R)));
+  hipStream_t st = as_stream(stream);
+#define DAL_FOREST_LAUNCH(XL, FL)                                                                   \
+  do {                                                                                              \
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(forest_score_kernel<XL, FL>),             \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(smem)) !=  \
+        hipSuccess)                                                                                 \
+      return DAL_ERR_HIP;                                                                           \
+    hipLaunchKernelGGL((forest_score_kernel<XL, FL>), grid, dim3(kForestThreads), smem, st, A, R,  \
+                       tpr, xf);                                                                    \
+  } while (0)
+  if (x_lds && f_lds) DAL_FOREST_LAUNCH(true, true);
+  else if (x_lds) DAL_FOREST_LAUNCH(true, false);
+  else if (f_lds) DAL_FOREST_LAUNCH(false, true);
+  else DAL_FOREST_LAUNCH(false, false);
+#undef DAL_FOREST_LAUNCH
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}

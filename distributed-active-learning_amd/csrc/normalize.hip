@@ -1,0 +1,155 @@
+// Row L2 normalisation and the canonical fp64 column sum.
+//
+// Reference: final_thesis/density_weighting.py:66 (``_/np.linalg.norm(_)``),
+// cosine_similarity.py:28, similarity.py:28; exclusion of L0 as column j:
+// density_weighting.py:95-100.
+//
+// HBM-bound O(N*D) passes.  The fp64 arithmetic here is the canonical
+// definition the selected set is bit-exact to, so the library is built with
+// -ffp-contract=off: every multiply and add rounds separately, in the order
+// the oracle uses (sequential over features / rows).
+#include "common.hpp"
+
+namespace dal {
+namespace {
+
+constexpr int kNormRows = 64;    // rows per block (one per lane of wave 0)
+constexpr int kNormCols = 64;    // feature columns staged per step
+constexpr int kNormThreads = 256;
+
+// One block normalises 64 rows.  Pass 1 stages 64x64 tiles through LDS with
+// coalesced loads so that lane r can sum row r sequentially over features
+// (canonical order); pass 2 writes the fp32 unit rows (coalesced) and the
+// zero padding.
+__global__ __launch_bounds__(kNormThreads) void normalize_rows_kernel(
+    const float* __restrict__ x, int64_t n, int d, int64_t ldx, const uint8_t* __restrict__ flags,
+    int64_t n_pad, int d_pad, float* __restrict__ u, double* __restrict__ norm64,
+    int32_t* __restrict__ status) {
+  __shared__ float tile[kNormRows][kNormCols + 1];
+  __shared__ double rnorm[kNormRows];
+  const int tid = threadIdx.x;
+  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kNormRows;
+  double n2 = 0.0;
+  for (int c0 = 0; c0 < d; c0 += kNormCols) {
+    // coalesced load: 256 threads = 4 rows x 64 columns per step
+    for (int e = tid; e < kNormRows * kNormCols; e += kNormThreads) {
+      const int r = e / kNormCols, c = e % kNormCols;
+      const int64_t row = row0 + r;
+      float v = 0.0f;
+      if (row < n && c0 + c < d) v = x[row * ldx + c0 + c];
+      tile[r][c] = v;
+    }
+    __syncthreads();
+    if (tid < kNormRows) {
+      const int cmax = min(kNormCols, d - c0);
+      for (int c = 0; c < cmax; ++c) {
+        const double v = static_cast<double>(tile[tid][c]);
+        n2 = n2 + v * v;  // -ffp-contract=off: mul then add
+      }
+    }
+    __syncthreads();
+  }
+  if (tid < kNormRows) {
+    const int64_t row = row0 + tid;
+    double nr = __builtin_sqrt(n2);
+    if (row < n) {
+      if (!(n2 > 0.0)) atomicOr(status, DAL_FLAG_ZERO_NORM);
+      if (norm64) norm64[row] = nr;
+    }
+    rnorm[tid] = nr;
+  }
+  __syncthreads();
+  for (int r = tid / kWave; r < kNormRows; r += kNormThreads / kWave) {
+    const int64_t row = row0 + r;
+    if (row >= n_pad) break;
+    const bool live = row < n && !(flags && (flags[row] & DAL_ROW_EXCLUDED));
+    const double nr = rnorm[r];
+    float* urow = u + row * d_pad;
+    for (int c = tid % kWave; c < d_pad; c += kWave) {
+      float v = 0.0f;
+      if (live && c < d && nr > 0.0) v = static_cast<float>(static_cast<double>(x[row * ldx + c]) / nr);
+      urow[c] = v;
+    }
+  }
+}
+
+// partials[c][f] = sum_{r in chunk c, not excluded} x_rf / norm64[r]
+// (sequential over the chunk's rows).  Lanes run over features: coalesced.
+__global__ __launch_bounds__(64) void canon_colsum_partials_kernel(
+    const float* __restrict__ x, int64_t n, int d, int64_t ldx, const double* __restrict__ norm64,
+    const uint8_t* __restrict__ flags, double* __restrict__ partials) {
+  const int64_t c = blockIdx.x;
+  const int f = blockIdx.y * 64 + threadIdx.x;
+  if (f >= d) return;
+  double acc = 0.0;
+  const int64_t r0 = c * DAL_CANON_CHUNK;
+  const int64_t r1 = min(n, r0 + DAL_CANON_CHUNK);
+  for (int64_t r = r0; r < r1; ++r) {
+    if (flags && (flags[r] & DAL_ROW_EXCLUDED)) continue;
+    acc = acc + static_cast<double>(x[r * ldx + f]) / norm64[r];
+  }
+  partials[c * d + f] = acc;
+}
+
+__global__ __launch_bounds__(64) void canon_colsum_reduce_kernel(const double* __restrict__ partials,
+                                                                 int64_t n_chunks, int d,
+                                                                 double* __restrict__ s) {
+  const int f = blockIdx.x * 64 + threadIdx.x;
+  if (f >= d) return;
+  double acc = 0.0;
+  for (int64_t c = 0; c < n_chunks; ++c) acc = acc + partials[c * d + f];
+  s[f] = acc;
+}
+
+}  // namespace
+}  // namespace dal
+
+using namespace dal;
+
+extern "C" int64_t dal_pad_rows(int64_t n) { return round_up(n < 1 ? 1 : n, DAL_ROW_GRANULE); }
+
+extern "C" int64_t dal_pad_features(int64_t d) {
+  if (d <= 32) return 32;
+  if (d <= 64) return 64;
+  if (d <= 128) return 128;
+  return round_up(d, 256);
+}
+
+extern "C" int dal_normalize_rows(const float* x, int64_t n, int64_t d, int64_t ldx,
+                                  const uint8_t* row_flags, int64_t n_pad, int64_t d_pad, float* u,
+                                  double* norm64, int32_t* dev_status, dal_stream_t stream) {
+  if (!x || !u || !dev_status) return DAL_ERR_ARG;
+  if (n < 0 || d < 1 || ldx < d || n_pad < n || d_pad < d || d > (1 << 20)) return DAL_ERR_SHAPE;
+  if (n_pad == 0) return DAL_OK;
+  const int64_t blocks = ceil_div(n_pad, kNormRows);
+  hipLaunchKernelGGL(normalize_rows_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kNormThreads), 0,
+                     as_stream(stream), x, n, static_cast<int>(d), ldx, row_flags, n_pad,
+                     static_cast<int>(d_pad), u, norm64, dev_status);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}
+
+extern "C" int dal_canon_colsum_partials(const float* x, int64_t n, int64_t d, int64_t ldx,
+                                         const double* norm64, const uint8_t* row_flags,
+                                         double* partials, dal_stream_t stream) {
+  if (!x || !norm64 || !partials) return DAL_ERR_ARG;
+  if (n < 1 || d < 1 || ldx < d) return DAL_ERR_SHAPE;
+  const int64_t chunks = ceil_div(n, DAL_CANON_CHUNK);
+  hipLaunchKernelGGL(canon_colsum_partials_kernel,
+                     dim3(static_cast<unsigned>(chunks), static_cast<unsigned>(ceil_div(d, 64))),
+                     dim3(64), 0, as_stream(stream), x, n, static_cast<int>(d), ldx, norm64,
+                     row_flags, partials);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}
+
+extern "C" int dal_canon_colsum_reduce(const double* partials, int64_t n_chunks, int64_t d,
+                                       double* colsum, dal_stream_t stream) {
+  if (!partials || !colsum) return DAL_ERR_ARG;
+  if (n_chunks < 1 || d < 1) return DAL_ERR_SHAPE;
+  hipLaunchKernelGGL(canon_colsum_reduce_kernel, dim3(static_cast<unsigned>(ceil_div(d, 64))),
+                     dim3(64), 0, as_stream(stream), partials, n_chunks, static_cast<int>(d),
+                     colsum);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}

@@ -1,0 +1,502 @@
+// Top-k selection: sortBy(score).take(k) with a deterministic tie rule, and
+// the density-weighted selection with its exact fp64 re-rank.
+//
+// Reference: final_thesis/uncertainty_sampling.py:106,109 (ascending
+// sortBy + take(window_size)); density_weighting.py:168,172 (descending);
+// lal_direct_mllib_implementation/classes/active_learner.py:203 (k = 1).
+// Spark breaks ties by partition order (nondeterministic); the canonical rule
+// here is (key, then lower global row index), with NaN last and -0 == +0
+// (score_key in common.hpp).
+//
+// Pipeline (all device-side, no host round trip):
+//   8 x radix_hist   exact k-th smallest key, 8-bit digits MSB first; every
+//                    block re-derives the running (prefix, remaining-k) state
+//                    from the previous pass's 256-bin histogram.
+//   count/scan/write ordered compaction: every key < K*, plus the first
+//                    (in row order) keys == K* -- stable, so ties go to the
+//                    lower index.
+//   sort             one 1024-thread block, bitonic on (key, index) in LDS.
+// HBM-bound: each pass reads 8 B/row.
+#include "common.hpp"
+
+namespace dal {
+namespace {
+
+constexpr int kRadixThreads = 256;
+constexpr int kCompactRows = 1024;  // rows per compaction block (4 per thread)
+constexpr int kSortThreads = 1024;
+
+struct TopkHdr {
+  uint32_t hist[8][256];
+  unsigned long long prefix[9];
+  unsigned long long krem[9];
+  unsigned long long kstar, kfinal, total_lt, total_eq;
+  unsigned int cand_count, overflow, pad0, pad1;
+};
+
+struct TopkLayout {
+  size_t hdr, blk, off, ckey, cidx, cpay, total;
+  int64_t nb, cap;
+};
+
+TopkLayout topk_layout(int64_t n, int64_t cap) {
+  TopkLayout L;
+  L.nb = ceil_div(n < 1 ? 1 : n, kCompactRows);
+  L.cap = cap;
+  size_t o = 0;
+  L.hdr = o;
+  o += round_up(sizeof(TopkHdr), 256);
+  L.blk = o;
+  o += round_up(L.nb * 2 * sizeof(uint32_t), 256);
+  L.off = o;
+  o += round_up(L.nb * 2 * sizeof(uint32_t), 256);
+  L.ckey = o;
+  o += round_up(cap * 8, 256);
+  L.cidx = o;
+  o += round_up(cap * 8, 256);
+  L.cpay = o;
+  o += round_up(cap * 8, 256);
+  L.total = o;
+  return L;
+}
+
+// ---------------------------------------------------------------- radix ----
+// Resolve the digit of pass p-1 from its histogram: the first bucket whose
+// inclusive count reaches the remaining k.  256 threads, one bucket each.
+__device__ void resolve_digit(const TopkHdr* h, int p, unsigned long long& prefix,
+                              unsigned long long& krem, uint32_t* sh) {
+  const int tid = threadIdx.x;
+  const unsigned long long kr = h->krem[p];
+  uint32_t c = h->hist[p][tid];
+  sh[tid] = c;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const uint32_t y = tid >= o ? sh[tid - o] : 0;
+    __syncthreads();
+    sh[tid] += y;
+    __syncthreads();
+  }
+  __shared__ unsigned long long s_pre, s_krem;
+  const uint32_t incl = sh[tid], excl = incl - c;
+  if (incl >= kr && excl < kr) {
+    s_pre = h->prefix[p] | (static_cast<unsigned long long>(tid) << (56 - 8 * p));
+    s_krem = kr - excl;
+  }
+  __syncthreads();
+  prefix = s_pre;
+  krem = s_krem;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kRadixThreads) void radix_hist_kernel(const uint64_t* __restrict__ keys,
+                                                                   int64_t n, int64_t k, int pass,
+                                                                   TopkHdr* __restrict__ h) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t scan[256];
+  const int tid = threadIdx.x;
+  unsigned long long prefix = 0, krem = static_cast<unsigned long long>(k);
+  if (pass > 0) resolve_digit(h, pass - 1, prefix, krem, scan);
+  if (blockIdx.x == 0 && tid == 0) {
+    h->prefix[pass] = prefix;
+    h->krem[pass] = krem;
+  }
+  hist[tid] = 0;
+  __syncthreads();
+  const int shift = 56 - 8 * pass;
+  const unsigned long long hmask = pass == 0 ? 0ull : (~0ull << (64 - 8 * pass));
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kRadixThreads;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kRadixThreads + tid; i < n; i += stride) {
+    const unsigned long long key = keys[i];
+    if ((key & hmask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
+  }
+  __syncthreads();
+  if (hist[tid]) atomicAdd(&h->hist[pass][tid], hist[tid]);
+}
+
+// ----------------------------------------------------------- compaction ---
+// Predicates per row: lt (take unconditionally) / eq (take the first eq_take
+// in row order).  EXACT: on the key itself.  INTERVAL: on the optimistic end
+// of the row's density-score interval (dal_dw_select).
+struct IntervalArgs {
+  const uint64_t* keys_hi;  // optimistic key of each row's score interval
+};
+
+template <bool INTERVAL>
+__device__ __forceinline__ void predicate(const uint64_t* keys, const IntervalArgs& I, int64_t i,
+                                          unsigned long long K, bool& lt, bool& eq) {
+  const unsigned long long lo = keys[i];
+  if (!INTERVAL) {
+    lt = lo < K;
+    eq = lo == K;
+    return;
+  }
+  // K = k-th smallest pessimistic key.  A row can reach the canonical top-k
+  // only if its optimistic key is <= K; rows whose interval is a point
+  // (exact score) and equal to K are ties resolved by index.
+  const unsigned long long hi = I.keys_hi[i];
+  const bool exact = hi == lo;
+  lt = hi < K || (hi == K && !exact);
+  eq = hi == K && exact;
+}
+
+__device__ __forceinline__ void final_threshold(TopkHdr* h, unsigned long long& K,
+                                                unsigned long long& krem, uint32_t* scan) {
+  resolve_digit(h, 7, K, krem, scan);
+}
+
+template <bool INTERVAL>
+__global__ __launch_bounds__(kRadixThreads) void compact_count_kernel(const uint64_t* __restrict__ keys,
+                                                                      IntervalArgs I, int64_t n,
+                                                                      TopkHdr* __restrict__ h,
+                                                                      uint32_t* __restrict__ blk) {
+  __shared__ uint32_t scan[256];
+  __shared__ uint32_t red[2][4];
+  unsigned long long K, krem;
+  final_threshold(h, K, krem, scan);
+  const int tid = threadIdx.x;
+  if (blockIdx.x == 0 && tid == 0) {
+    h->kstar = K;
+    h->kfinal = krem;
+  }
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kCompactRows;
+  uint32_t lt_c = 0, eq_c = 0;
+  for (int j = 0; j < 4; ++j) {
+    const int64_t i = r0 + tid * 4 + j;
+    if (i >= n) break;
+    bool lt, eq;
+    predicate<INTERVAL>(keys, I, i, K, lt, eq);
+    lt_c += lt;
+    eq_c += eq;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    lt_c += __shfl_xor(lt_c, o);
+    eq_c += __shfl_xor(eq_c, o);
+  }
+  if ((tid & 63) == 0) {
+    red[0][tid >> 6] = lt_c;
+    red[1][tid >> 6] = eq_c;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    blk[2 * blockIdx.x] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    blk[2 * blockIdx.x + 1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  }
+}
+
+// exclusive scan of the per-block (lt, eq) counts; one 1024-thread block.
+__global__ __launch_bounds__(1024) void compact_scan_kernel(const uint32_t* __restrict__ blk,
+                                                            uint32_t* __restrict__ off, int64_t nb,
+                                                            TopkHdr* __restrict__ h) {
+  __shared__ uint32_t s[2][1024];
+  const int tid = threadIdx.x;
+  uint32_t carry_lt = 0, carry_eq = 0;
+  for (int64_t base = 0; base < nb; base += 1024) {
+    const int64_t b = base + tid;
+    const uint32_t vl = b < nb ? blk[2 * b] : 0, ve = b < nb ? blk[2 * b + 1] : 0;
+    s[0][tid] = vl;
+    s[1][tid] = ve;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const uint32_t yl = tid >= o ? s[0][tid - o] : 0, ye = tid >= o ? s[1][tid - o] : 0;
+      __syncthreads();
+      s[0][tid] += yl;
+      s[1][tid] += ye;
+      __syncthreads();
+    }
+    if (b < nb) {
+      off[2 * b] = carry_lt + s[0][tid] - vl;
+      off[2 * b + 1] = carry_eq + s[1][tid] - ve;
+    }
+    carry_lt += s[0][1023];
+    carry_eq += s[1][1023];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    h->total_lt = carry_lt;
+    h->total_eq = carry_eq;
+  }
+}
+
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint32_t x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[w] = x;
+  __syncthreads();
+  uint32_t before = 0;
+  total = 0;
+  for (int i = 0; i < kRadixThreads / 64; ++i) {
+    if (i < w) before += sh[i];
+    total += sh[i];
+  }
+  __syncthreads();
+  return x - v + before;
+}
+
+template <bool INTERVAL>
+__global__ __launch_bounds__(kRadixThreads) void compact_write_kernel(
+    const uint64_t* __restrict__ keys, IntervalArgs I, int64_t n, int64_t idx_base, int64_t k,
+    TopkHdr* __restrict__ h, const uint32_t* __restrict__ off, uint64_t* __restrict__ ckey,
+    int64_t* __restrict__ cidx, int64_t cap, int32_t* __restrict__ status) {
+  __shared__ uint32_t sh[2][4];
+  const int tid = threadIdx.x;
+  const unsigned long long K = h->kstar;
+  const uint64_t eq_take = INTERVAL ? static_cast<uint64_t>(k) : h->kfinal;
+  const uint64_t total_lt = h->total_lt;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kCompactRows;
+  bool lt[4], eq[4];
+  uint32_t lc = 0, ec = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t i = r0 + tid * 4 + j;
+    lt[j] = eq[j] = false;
+    if (i < n) predicate<INTERVAL>(keys, I, i, K, lt[j], eq[j]);
+    lc += lt[j];
+    ec += eq[j];
+  }
+  uint32_t tl, te;
+  uint32_t pl = block_excl_scan(lc, sh[0], tl) + off[2 * blockIdx.x];
+  uint32_t pe = block_excl_scan(ec, sh[1], te) + off[2 * blockIdx.x + 1];
+  bool ovf = false;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t i = r0 + tid * 4 + j;
+    int64_t pos = -1;
+    if (lt[j]) pos = pl++;
+    else if (eq[j]) {
+      if (pe < eq_take) pos = static_cast<int64_t>(total_lt + pe);
+      ++pe;
+    }
+    if (pos >= 0) {
+      if (pos < cap) {
+        ckey[pos] = INTERVAL ? 0ull : keys[i];
+        cidx[pos] = idx_base + i;
+      } else {
+        ovf = true;
+      }
+    }
+  }
+  if (ovf) {
+    atomicOr(&h->overflow, 1u);
+    if (status) atomicOr(status, DAL_FLAG_CAND_OVERFLOW);
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    const uint64_t take_eq = h->total_eq < eq_take ? h->total_eq : eq_take;
+    const uint64_t cnt = total_lt + take_eq;
+    h->cand_count = static_cast<unsigned>(cnt < static_cast<uint64_t>(cap) ? cnt : cap);
+  }
+}
+
+// ------------------------------------------------------------- re-rank ----
+// Canonical fp64 density-weighted score of each candidate (bit-identical to
+// oracle.density_canonical: x/norm, then sequential mul+add over features;
+// the library is compiled with -ffp-contract=off).
+__global__ __launch_bounds__(256) void rerank_kernel(const TopkHdr* __restrict__ h, int64_t idx_base,
+                                                     const float* __restrict__ x, int d, int64_t ldx,
+                                                     const double* __restrict__ norm64,
+                                                     const double* __restrict__ colsum,
+                                                     const double* __restrict__ lut,
+                                                     const int32_t* __restrict__ votes,
+                                                     const uint8_t* __restrict__ flags, double beta,
+                                                     uint64_t* __restrict__ ckey,
+                                                     const int64_t* __restrict__ cidx,
+                                                     double* __restrict__ cpay) {
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (c >= h->cand_count) return;
+  const int64_t i = cidx[c] - idx_base;
+  const double nr = norm64[i];
+  const float* xr = x + i * ldx;
+  double acc = 0.0;
+  for (int f = 0; f < d; ++f) {
+    const double u = static_cast<double>(xr[f]) / nr;
+    acc = acc + u * colsum[f];
+  }
+  if (flags && (flags[i] & DAL_ROW_EXCLUDED)) acc = __builtin_nan("");
+  const double e = lut[votes[i]];
+  const double s = e * (beta == 1.0 ? acc : pow(acc, beta));
+  cpay[c] = s;
+  ckey[c] = score_key(s, DAL_DESCENDING);
+}
+
+// ---------------------------------------------------------------- sort ----
+template <bool PAY>
+__global__ __launch_bounds__(kSortThreads) void sort_kernel(const uint64_t* __restrict__ keys,
+                                                            const int64_t* __restrict__ idx,
+                                                            const double* __restrict__ pay,
+                                                            const TopkHdr* __restrict__ h,
+                                                            int64_t n_static, int64_t k,
+                                                            uint64_t* __restrict__ out_keys,
+                                                            int64_t* __restrict__ out_idx,
+                                                            double* __restrict__ out_pay) {
+  constexpr int CAP = PAY ? DAL_SORT_CAP_PAYLOAD : DAL_SORT_CAP;
+  __shared__ unsigned long long sk[CAP];
+  __shared__ long long si[CAP];
+  __shared__ double sp[PAY ? CAP : 1];
+  const int tid = threadIdx.x;
+  int64_t m = h ? static_cast<int64_t>(h->cand_count) : n_static;
+  if (m > CAP) m = CAP;
+  int mp = 2;
+  while (mp < m) mp <<= 1;
+  for (int i = tid; i < mp; i += kSortThreads) {
+    if (i < m) {
+      sk[i] = keys[i];
+      si[i] = idx[i];
+      if (PAY) sp[i] = pay[i];
+    } else {
+      sk[i] = ~0ull;
+      si[i] = 0x7FFFFFFFFFFFFFFFll;
+      if (PAY) sp[i] = 0.0;
+    }
+  }
+  __syncthreads();
+  for (int size = 2; size <= mp; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = tid; t < (mp >> 1); t += kSortThreads) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const unsigned long long ka = sk[lo], kb = sk[hi];
+        const long long ia = si[lo], ib = si[hi];
+        const bool a_gt_b = ka > kb || (ka == kb && ia > ib);
+        if (a_gt_b == up) {
+          sk[lo] = kb;
+          sk[hi] = ka;
+          si[lo] = ib;
+          si[hi] = ia;
+          if (PAY) {
+            const double t0 = sp[lo];
+            sp[lo] = sp[hi];
+            sp[hi] = t0;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const int64_t kk = k < m ? k : m;
+  for (int i = tid; i < kk; i += kSortThreads) {
+    if (out_keys) out_keys[i] = sk[i];
+    out_idx[i] = si[i];
+    if (PAY && out_pay) out_pay[i] = sp[i];
+  }
+}
+
+int run_radix(const uint64_t* keys, int64_t n, int64_t k, TopkHdr* h, hipStream_t st) {
+  if (hipMemsetAsync(h, 0, sizeof(TopkHdr), st) != hipSuccess) return DAL_ERR_HIP;
+  int64_t blocks = ceil_div(n, kRadixThreads * 8);
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  for (int p = 0; p < 8; ++p) {
+    hipLaunchKernelGGL(radix_hist_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kRadixThreads), 0,
+                       st, keys, n, k, p, h);
+  }
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}
+
+template <bool INTERVAL>
+int run_compact(const uint64_t* keys, const IntervalArgs& I, int64_t n, int64_t idx_base, int64_t k,
+                void* ws, const TopkLayout& L, int32_t* status, hipStream_t st) {
+  char* base = static_cast<char*>(ws);
+  TopkHdr* h = reinterpret_cast<TopkHdr*>(base + L.hdr);
+  uint32_t* blk = reinterpret_cast<uint32_t*>(base + L.blk);
+  uint32_t* off = reinterpret_cast<uint32_t*>(base + L.off);
+  const dim3 g(static_cast<unsigned>(L.nb));
+  hipLaunchKernelGGL(compact_count_kernel<INTERVAL>, g, dim3(kRadixThreads), 0, st, keys, I, n, h, blk);
+  hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, st, blk, off, L.nb, h);
+  hipLaunchKernelGGL(compact_write_kernel<INTERVAL>, g, dim3(kRadixThreads), 0, st, keys, I, n,
+                     idx_base, k, h, off, reinterpret_cast<uint64_t*>(base + L.ckey),
+                     reinterpret_cast<int64_t*>(base + L.cidx), L.cap, status);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}
+
+}  // namespace
+}  // namespace dal
+
+using namespace dal;
+
+extern "C" size_t dal_topk_workspace_bytes(int64_t n, int64_t k) {
+  return topk_layout(n, k < 1 ? 1 : k).total;
+}
+
+extern "C" int dal_topk(const uint64_t* keys, int64_t n, int64_t k, int64_t idx_base, void* ws,
+                        size_t ws_bytes, int64_t* out_idx, uint64_t* out_keys, dal_stream_t stream) {
+  if (!keys || !ws || !out_idx) return DAL_ERR_ARG;
+  if (n < 1 || k < 1 || k > n) return DAL_ERR_SHAPE;
+  if (k > DAL_SORT_CAP) return DAL_ERR_CAPACITY;
+  const TopkLayout L = topk_layout(n, k);
+  if (ws_bytes < L.total || (reinterpret_cast<uintptr_t>(ws) & 255)) return DAL_ERR_SHAPE;
+  hipStream_t st = as_stream(stream);
+  TopkHdr* h = reinterpret_cast<TopkHdr*>(static_cast<char*>(ws) + L.hdr);
+  int rc = run_radix(keys, n, k, h, st);
+  if (rc) return rc;
+  rc = run_compact<false>(keys, IntervalArgs{nullptr}, n, idx_base, k, ws, L, nullptr, st);
+  if (rc) return rc;
+  char* base = static_cast<char*>(ws);
+  hipLaunchKernelGGL(sort_kernel<false>, dim3(1), dim3(kSortThreads), 0, st,
+                     reinterpret_cast<const uint64_t*>(base + L.ckey),
+                     reinterpret_cast<const int64_t*>(base + L.cidx), nullptr, h, int64_t{0}, k,
+                     out_keys, out_idx, nullptr);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}
+
+extern "C" size_t dal_dw_select_workspace_bytes(int64_t n, int64_t k) {
+  (void)k;
+  return topk_layout(n, DAL_SORT_CAP_PAYLOAD).total;
+}
+
+extern "C" int dal_dw_select(const uint64_t* keys_lo, const uint64_t* keys_hi, const int32_t* votes,
+                             const uint8_t* row_flags, int64_t n, int64_t k, int64_t idx_base,
+                             const double* lut, double beta, const float* x, int64_t d, int64_t ldx,
+                             const double* norm64, const double* colsum, void* ws, size_t ws_bytes,
+                             int64_t* out_idx, double* out_scores, uint64_t* out_keys,
+                             int32_t* dev_status, dal_stream_t stream) {
+  if (!keys_lo || !keys_hi || !votes || !lut || !x || !norm64 || !colsum || !ws || !out_idx ||
+      !out_scores || !dev_status)
+    return DAL_ERR_ARG;
+  if (n < 1 || k < 1 || k > n || d < 1 || ldx < d) return DAL_ERR_SHAPE;
+  if (k > DAL_SORT_CAP_PAYLOAD) return DAL_ERR_CAPACITY;
+  const TopkLayout L = topk_layout(n, DAL_SORT_CAP_PAYLOAD);
+  if (ws_bytes < L.total || (reinterpret_cast<uintptr_t>(ws) & 255)) return DAL_ERR_SHAPE;
+  hipStream_t st = as_stream(stream);
+  char* base = static_cast<char*>(ws);
+  TopkHdr* h = reinterpret_cast<TopkHdr*>(base + L.hdr);
+  int rc = run_radix(keys_lo, n, k, h, st);
+  if (rc) return rc;
+  rc = run_compact<true>(keys_lo, IntervalArgs{keys_hi}, n, idx_base, k, ws, L, dev_status, st);
+  if (rc) return rc;
+  uint64_t* ckey = reinterpret_cast<uint64_t*>(base + L.ckey);
+  int64_t* cidx = reinterpret_cast<int64_t*>(base + L.cidx);
+  double* cpay = reinterpret_cast<double*>(base + L.cpay);
+  hipLaunchKernelGGL(rerank_kernel, dim3(DAL_SORT_CAP_PAYLOAD / 256), dim3(256), 0, st, h, idx_base, x,
+                     static_cast<int>(d), ldx, norm64, colsum, lut, votes, row_flags, beta, ckey, cidx,
+                     cpay);
+  hipLaunchKernelGGL(sort_kernel<true>, dim3(1), dim3(kSortThreads), 0, st, ckey, cidx, cpay, h,
+                     int64_t{0}, k, out_keys, out_idx, out_scores);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}
+
+extern "C" int dal_sort_pairs(const uint64_t* keys, const int64_t* idx, const double* payload, int64_t n,
+                              int64_t k, uint64_t* out_keys, int64_t* out_idx, double* out_payload,
+                              dal_stream_t stream) {
+  if (!keys || !idx || !out_idx) return DAL_ERR_ARG;
+  if (n < 1 || k < 1) return DAL_ERR_SHAPE;
+  hipStream_t st = as_stream(stream);
+  if (payload) {
+    if (n > DAL_SORT_CAP_PAYLOAD) return DAL_ERR_CAPACITY;
+    hipLaunchKernelGGL(sort_kernel<true>, dim3(1), dim3(kSortThreads), 0, st, keys, idx, payload,
+                       nullptr, n, k, out_keys, out_idx, out_payload);
+  } else {
+    if (n > DAL_SORT_CAP) return DAL_ERR_CAPACITY;
+    hipLaunchKernelGGL(sort_kernel<false>, dim3(1), dim3(kSortThreads), 0, st, keys, idx, nullptr,
+                       nullptr, n, k, out_keys, out_idx, nullptr);
+  }
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}

@@ -1,0 +1,47 @@
+"""Density-weighted uncertainty query step -- drop-in for final_thesis/density_weighting.py.
+
+Reference pipeline:
+  proximity matrix  density_weighting.py:58-75  rows L2-normalised (:66), S = U.U^T
+                    via BlockMatrix.multiply (:73), N^2 entries pulled to Python (:74-75)
+  L0 exclusion      :89-100   entries with i or j in the initial window are dropped once
+  per iteration     :136-145  T per-tree predicts + vote sum
+                    :148      e = -(1-v/T) log2(1-v/T)
+                    :157-161  d_i = sum of the row's remaining S entries (includes j = i)
+                    :166-172  score = e * d, descending sortBy, take(window_size)
+Here: a fused fp32-MFMA Gram row-sum (S never exists; the density is cached
+per pool because the reference's is constant across iterations), a fused
+forest + score kernel, and a device top-k whose boundary candidates are
+re-ranked in canonical fp64 so the selected set is bit-exact.
+``beta`` (declared at :33, unused by the reference) weights d^beta.
+"""
+from __future__ import annotations
+
+from .engine import PoolState, Selection, as_pool_state, density_step
+from .forest import Forest
+
+
+def information_density(pool, excluded_idx=None, device=None):
+    """d_i = sum_{j not in E} cos(x_i, x_j) for every row (fp64, NaN for i in E).
+
+    excluded_idx  E; the reference uses L0 = range(window_size).
+    """
+    state = as_pool_state(pool, excluded=excluded_idx, device=device)
+    d = state.density()
+    state.check_status()
+    return d
+
+
+def select(pool, unlabeled_idx, forest: Forest, k: int, beta: float = 1.0, excluded_idx=None,
+           density=None, device=None) -> Selection:
+    """Score every unlabeled row by entropy x density^beta and select the top k.
+
+    excluded_idx  rows dropped from the density (default: none; the reference
+                  passes its initial labeled window, range(window_size))
+    density       optional int64 fixed-point density from a previous call
+                  (PoolState.density_fixed()); by default the pool's cached one
+    """
+    state = as_pool_state(pool, excluded=excluded_idx, device=device)
+    return density_step(state, unlabeled_idx, forest, k, beta=beta, density_fixed=density)
+
+
+__all__ = ["information_density", "select", "PoolState", "Selection"]

@@ -1,0 +1,349 @@
+"""Device pipeline of one query-selection step (single GPU / one shard).
+
+Every arithmetic step is a libdal HIP kernel (include/dal.h); torch is used
+only for device memory, the current HIP stream and trivial index plumbing.
+There is no CPU fallback: without libdal.so or a GPU these functions raise.
+
+Reference loop body being replaced (one ``while True`` iteration):
+  uncertainty_sampling.py:85-112   per-tree predict, vote sum, LC score, sortBy, take(k)
+  density_weighting.py:58-100      proximity matrix (built once per pool)
+  density_weighting.py:133-176     entropy x density, descending sortBy, take(k)
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import (DAL_ASCENDING, DAL_DESCENDING, DAL_FLAG_CAND_OVERFLOW, DAL_FLAG_ZERO_NORM,
+                   DAL_ROW_CANDIDATE, DAL_ROW_EXCLUDED, DAL_CANON_CHUNK, DAL_FIXED_SCALE, call)
+from .forest import Forest
+from .luts import ASCENDING, lut as make_lut
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def _stream(device=None) -> int:
+    torch = _torch()
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _ptr(t) -> int:
+    return t.data_ptr()
+
+
+def _require_cuda(device):
+    torch = _torch()
+    if not torch.cuda.is_available():
+        raise _lib.DalError("dal requires a ROCm GPU (torch.cuda.is_available() is False)")
+    return torch.device(device if device is not None else "cuda")
+
+
+@dataclass
+class Selection:
+    """Result of one selection step (all tensors on the pool's device).
+
+    scores          fp64 [U]: score of every unlabeled row, in ``unlabeled`` order
+    indices         int64 [k]: selected global row indices, best first
+    selected_scores fp64 [k]: their scores (canonical fp64 for density weighting)
+    votes           int32 [U]: forest votes for class 1 of every unlabeled row
+    """
+
+    scores: object
+    indices: object
+    selected_scores: object
+    votes: object = None
+
+    def as_pairs(self):
+        """``add_to_labeled_set`` of the reference: a list of (index, score)."""
+        return list(zip(self.indices.cpu().tolist(), self.selected_scores.cpu().tolist()))
+
+
+class PoolState:
+    """A device-resident pool and its per-pool caches.
+
+    The reference builds the proximity matrix once per pool and drops the
+    initial labeled window L0 from it once (density_weighting.py:58-100), so the
+    density is constant across AL iterations; it is computed lazily here and
+    cached (the "warm" path), keyed by the excluded set.
+
+    For a row shard (multi-GPU) ``row_base`` is the global index of row 0 and
+    ``n_total`` the global pool size.
+    """
+
+    def __init__(self, pool, excluded=None, device=None, row_base: int = 0, n_total=None,
+                 n_pad=None):
+        torch = _torch()
+        dev = _require_cuda(device)
+        lib = _lib.load()
+        if isinstance(pool, torch.Tensor):
+            x = pool.to(device=dev, dtype=torch.float32)
+        else:
+            x = torch.from_numpy(np.ascontiguousarray(np.asarray(pool, dtype=np.float32))).to(dev)
+        if x.dim() != 2:
+            raise ValueError("pool must be a 2-D [rows, features] array")
+        self.x = x.contiguous()
+        self.device = dev
+        self.n, self.d = int(x.shape[0]), int(x.shape[1])
+        self.row_base = int(row_base)
+        self.n_total = int(n_total) if n_total is not None else self.n
+        self.n_pad = int(lib.dal_pad_rows(self.n)) if n_pad is None else int(n_pad)
+        if self.n_pad < self.n or self.n_pad % 512:
+            raise ValueError("n_pad must be a multiple of 512 and >= the row count")
+        self.d_pad = int(lib.dal_pad_features(self.d))
+        self.flags = torch.zeros(self.n, dtype=torch.uint8, device=dev)
+        self.excluded = np.zeros(0, dtype=np.int64)
+        self.set_excluded(excluded)
+        self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._u = None
+        self._norm64 = None
+        self._density = None
+        self._colsum_partials = None
+        self._colsum = None
+        self.gram_events = None  # list -> (start, end) HIP events around each Gram call
+
+    def clear_caches(self):
+        """Drop normalised rows, density and column sums (forces a cold step)."""
+        self._u = self._norm64 = self._density = self._colsum = self._colsum_partials = None
+
+    # ------------------------------------------------------------- caches
+    def set_excluded(self, excluded):
+        """E (global indices): dropped from the density as i and as j
+        (density_weighting.py:95-100)."""
+        torch = _torch()
+        ex = np.unique(np.asarray([] if excluded is None else excluded, dtype=np.int64))
+        if np.array_equal(ex, self.excluded) and hasattr(self, "_u"):
+            return
+        self.excluded = ex
+        self.flags.zero_()
+        local = ex[(ex >= self.row_base) & (ex < self.row_base + self.n)] - self.row_base
+        if local.size:
+            self.flags[torch.from_numpy(local).to(self.device)] = DAL_ROW_EXCLUDED
+        self._u = self._norm64 = self._density = self._colsum = self._colsum_partials = None
+
+    def n_excluded_global(self) -> int:
+        return int(self.excluded.size)
+
+    def normalized(self):
+        """(u [n_pad, d_pad] fp32 with E rows zeroed, norm64 [n] fp64)."""
+        if self._u is None:
+            torch = _torch()
+            if self.n == 0:
+                self._u = torch.zeros((self.n_pad, self.d_pad), dtype=torch.float32, device=self.device)
+                self._norm64 = torch.zeros(0, dtype=torch.float64, device=self.device)
+                return self._u, self._norm64
+            self._u = torch.empty((self.n_pad, self.d_pad), dtype=torch.float32, device=self.device)
+            self._norm64 = torch.empty(self.n, dtype=torch.float64, device=self.device)
+            call("dal_normalize_rows", _ptr(self.x), self.n, self.d, self.d, _ptr(self.flags),
+                 self.n_pad, self.d_pad, _ptr(self._u), _ptr(self._norm64), _ptr(self.status),
+                 _stream(self.device))
+        return self._u, self._norm64
+
+    def colsum_partials(self):
+        """Canonical fp64 column-sum partials of this shard ([chunks, d])."""
+        if self._colsum_partials is None:
+            torch = _torch()
+            _, norm64 = self.normalized()
+            chunks = (self.n + DAL_CANON_CHUNK - 1) // DAL_CANON_CHUNK
+            self._colsum_partials = torch.empty((chunks, self.d), dtype=torch.float64, device=self.device)
+            call("dal_canon_colsum_partials", _ptr(self.x), self.n, self.d, self.d, _ptr(norm64),
+                 _ptr(self.flags), _ptr(self._colsum_partials), _stream(self.device))
+        return self._colsum_partials
+
+    def colsum(self, partials=None):
+        """s = sum_{j not in E} u_j in the canonical fp64 order."""
+        if partials is not None:
+            torch = _torch()
+            s = torch.empty(self.d, dtype=torch.float64, device=self.device)
+            call("dal_canon_colsum_reduce", _ptr(partials), int(partials.shape[0]), self.d, _ptr(s),
+                 _stream(self.device))
+            return s
+        if self._colsum is None:
+            self._colsum = self.colsum(self.colsum_partials())
+        return self._colsum
+
+    def density_fixed(self, u_cols=None, n_cols_pad=None):
+        """int64 fixed-point Gram row-sums (value * 2^32) of this shard's rows
+        against every column of ``u_cols`` (default: this pool)."""
+        if self._density is None or u_cols is not None:
+            torch = _torch()
+            u, _ = self.normalized()
+            acc = torch.zeros(self.n_pad, dtype=torch.int64, device=self.device)
+            cols = u if u_cols is None else u_cols
+            ncp = self.n_pad if n_cols_pad is None else int(n_cols_pad)
+            ev = None
+            if self.gram_events is not None:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
+            call("dal_gram_rowsum", _ptr(u), self.n_pad, _ptr(cols), ncp, self.d_pad, self.d_pad,
+                 _ptr(acc), 0, _stream(self.device))
+            if ev is not None:
+                ev[1].record()
+                self.gram_events.append(ev)
+            if u_cols is not None:
+                return acc
+            self._density = acc
+        return self._density
+
+    def set_density_fixed(self, acc):
+        self._density = acc
+
+    def density(self):
+        """fp64 density d[n] (NaN for rows in E): Gram row-sum / 2^32."""
+        torch = _torch()
+        d = self.density_fixed()[: self.n].to(torch.float64) * (1.0 / DAL_FIXED_SCALE)
+        ex = (self.flags & DAL_ROW_EXCLUDED).bool()
+        return torch.where(ex, torch.full_like(d, float("nan")), d)
+
+    # ------------------------------------------------------------ helpers
+    def row_flags(self, unlabeled_idx):
+        """EXCLUDED bits | CANDIDATE for the (global) unlabeled indices of this shard."""
+        torch = _torch()
+        unl = _as_index(unlabeled_idx, self.device)
+        loc = unl - self.row_base
+        loc = loc[(loc >= 0) & (loc < self.n)]
+        flags = self.flags.clone()
+        flags[loc] |= DAL_ROW_CANDIDATE
+        return flags, unl, loc
+
+    def check_status(self):
+        st = int(self.status.item())
+        if st & DAL_FLAG_ZERO_NORM:
+            raise ValueError("pool contains a zero-norm row: cosine similarity is undefined "
+                             "(the reference would propagate NaN into every density)")
+        if st & DAL_FLAG_CAND_OVERFLOW:
+            raise _lib.DalError("density re-rank candidate set exceeded DAL_SORT_CAP_PAYLOAD")
+
+
+def _as_index(idx, device):
+    torch = _torch()
+    if isinstance(idx, torch.Tensor):
+        return idx.to(device=device, dtype=torch.int64)
+    return torch.from_numpy(np.asarray(idx, dtype=np.int64).reshape(-1)).to(device)
+
+
+def as_pool_state(pool, excluded=None, device=None) -> PoolState:
+    if isinstance(pool, PoolState):
+        if excluded is not None:
+            pool.set_excluded(excluded)
+        return pool
+    return PoolState(pool, excluded=excluded, device=device)
+
+
+def device_lut(strategy: str, n_trees: int, device):
+    torch = _torch()
+    return torch.from_numpy(make_lut(strategy, n_trees)).to(device)
+
+
+def forest_score(state: PoolState, forest: Forest, lut_dev, flags, order: int, density=None,
+                 density_err: float = 0.0, beta: float = 1.0, want_hi: bool = False):
+    """Launch dal_forest_score over the shard; returns (votes, scores, keys, keys_hi)."""
+    torch = _torch()
+    inner, leaf = forest.device(state.device)
+    n = state.n
+    votes = torch.empty(n, dtype=torch.int32, device=state.device)
+    scores = torch.empty(n, dtype=torch.float64, device=state.device)
+    keys = torch.empty(n, dtype=torch.int64, device=state.device)
+    keys_hi = torch.empty(n, dtype=torch.int64, device=state.device) if want_hi else None
+    call("dal_forest_score", _ptr(state.x), n, state.d, state.d, _ptr(inner), _ptr(leaf),
+         forest.n_trees, forest.depth, _ptr(lut_dev), 0 if density is None else _ptr(density),
+         float(density_err), _ptr(flags), float(beta), int(order), _ptr(votes), _ptr(scores),
+         _ptr(keys), 0 if keys_hi is None else _ptr(keys_hi), _stream(state.device))
+    return votes, scores, keys, keys_hi
+
+
+def topk_keys(keys, k: int, idx_base: int = 0):
+    """k smallest keys (ties -> lower index): (indices int64 [k], keys [k])."""
+    torch = _torch()
+    lib = _lib.load()
+    n = int(keys.shape[0])
+    ws = torch.empty(int(lib.dal_topk_workspace_bytes(n, k)) + 256, dtype=torch.uint8,
+                     device=keys.device)
+    wsp = (_ptr(ws) + 255) // 256 * 256
+    out_idx = torch.empty(k, dtype=torch.int64, device=keys.device)
+    out_keys = torch.empty(k, dtype=torch.int64, device=keys.device)
+    call("dal_topk", _ptr(keys), n, k, int(idx_base), wsp, int(lib.dal_topk_workspace_bytes(n, k)),
+         _ptr(out_idx), _ptr(out_keys), _stream(keys.device))
+    return out_idx, out_keys
+
+
+def density_error(state: PoolState) -> float:
+    """Bound on |d_gemm - d_canonical| (rigorous; dal_density_error_bound)."""
+    n_cols = state.n_total - state.n_excluded_global()
+    return float(_lib.load().dal_density_error_bound(max(n_cols, 1)))
+
+
+def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k: int,
+                    beta: float, colsum):
+    """dal_dw_select on this shard: exact canonical top-k of the shard."""
+    torch = _torch()
+    lib = _lib.load()
+    n = state.n
+    _, norm64 = state.normalized()
+    wsb = int(lib.dal_dw_select_workspace_bytes(n, k))
+    ws = torch.empty(wsb + 256, dtype=torch.uint8, device=state.device)
+    wsp = (_ptr(ws) + 255) // 256 * 256
+    out_idx = torch.empty(k, dtype=torch.int64, device=state.device)
+    out_scores = torch.empty(k, dtype=torch.float64, device=state.device)
+    out_keys = torch.empty(k, dtype=torch.int64, device=state.device)
+    call("dal_dw_select", _ptr(keys_lo), _ptr(keys_hi), _ptr(votes), _ptr(flags), n, k,
+         state.row_base, _ptr(lut_dev), float(beta), _ptr(state.x), state.d, state.d, _ptr(norm64),
+         _ptr(colsum), wsp, wsb, _ptr(out_idx), _ptr(out_scores), _ptr(out_keys),
+         _ptr(state.status), _stream(state.device))
+    return out_idx, out_scores, out_keys
+
+
+def sort_pairs(keys, idx, k: int, payload=None):
+    """Sort (key, idx) pairs (with an optional fp64 payload) and keep k."""
+    torch = _torch()
+    n = int(keys.shape[0])
+    k = min(k, n)
+    out_keys = torch.empty(k, dtype=torch.int64, device=keys.device)
+    out_idx = torch.empty(k, dtype=torch.int64, device=keys.device)
+    out_pay = torch.empty(k, dtype=torch.float64, device=keys.device) if payload is not None else None
+    call("dal_sort_pairs", _ptr(keys), _ptr(idx), 0 if payload is None else _ptr(payload), n, k,
+         _ptr(out_keys), _ptr(out_idx), 0 if out_pay is None else _ptr(out_pay), _stream(keys.device))
+    return out_keys, out_idx, out_pay
+
+
+# ---------------------------------------------------------------- steps --
+def uncertainty_step(state: PoolState, unlabeled_idx, forest: Forest, k: int,
+                     strategy: str = "least_confidence") -> Selection:
+    """One iteration of uncertainty_sampling.py:85-112 on the GPU."""
+    flags, unl, loc = state.row_flags(unlabeled_idx)
+    n_cand = int(loc.shape[0])
+    if n_cand == 0:
+        raise ValueError("unlabeled set is empty (the reference loop breaks here)")
+    kk = min(int(k), n_cand)
+    order = DAL_ASCENDING if ASCENDING[strategy] else DAL_DESCENDING
+    lut_dev = device_lut(strategy, forest.n_trees, state.device)
+    votes, scores, keys, _ = forest_score(state, forest, lut_dev, flags, order)
+    idx, _ = topk_keys(keys, kk, state.row_base)
+    sel_scores = scores[idx - state.row_base]
+    state.check_status()
+    return Selection(scores=scores[loc], indices=idx, selected_scores=sel_scores, votes=votes[loc])
+
+
+def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: float = 1.0,
+                 density_fixed=None) -> Selection:
+    """One iteration of density_weighting.py:133-176 on the GPU:
+    score = ent[v] * d^beta, descending; exact canonical selection."""
+    flags, unl, loc = state.row_flags(unlabeled_idx)
+    n_cand = int(loc.shape[0])
+    if n_cand == 0:
+        raise ValueError("unlabeled set is empty (the reference loop breaks here)")
+    kk = min(int(k), n_cand)
+    dens = state.density_fixed() if density_fixed is None else density_fixed
+    lut_dev = device_lut("entropy", forest.n_trees, state.device)
+    votes, scores, keys_lo, keys_hi = forest_score(
+        state, forest, lut_dev, flags, DAL_DESCENDING, density=dens,
+        density_err=density_error(state), beta=beta, want_hi=True)
+    idx, sel_scores, _ = dw_select_local(state, flags, votes, keys_lo, keys_hi, lut_dev, kk, beta,
+                                         state.colsum())
+    state.check_status()
+    return Selection(scores=scores[loc], indices=idx, selected_scores=sel_scores, votes=votes[loc])

@@ -1,0 +1,197 @@
+"""Row-sharded multi-GPU query selection (one process per GPU, RCCL over xGMI).
+
+Reference parallelism: Spark data parallelism over RDD row partitions, with
+the cross-partition steps done as shuffles:
+BlockMatrix.multiply's block cogroup (density_weighting.py:73), groupByKey
+(:144, :159) and sortBy + take to the driver (:168, :172).
+
+Here the pool is row-sharded in contiguous shards of ``shard`` rows (a
+multiple of DAL_ROW_GRANULE, identical on every rank; the last rank holds the
+remainder).  Two exchanges, both all-gathers over ``torch.distributed``
+(backend "nccl" = RCCL on ROCm):
+
+  1. the normalised shards u_r (fp32, [shard, d_pad]) and the canonical fp64
+     column-sum partials -> every rank holds U (the density needs every
+     column) -- replaces the BlockMatrix shuffle;
+  2. each rank's exact local top-k (key, index, score) -> an identical
+     deterministic merge on every rank -- replaces sortBy + take.
+
+Determinism: global row r sits at column r of the gathered U on every P, the
+density is accumulated in exact int64 fixed point, and the canonical column
+sum is reduced over the same 256-row chunks in the same order, so every
+density bit, every score and the selected set are identical for P = 1..8.
+
+The phases are methods so that tests can drive P shards in one process
+(GPU, ``emulate``) or replace the local HIP steps with the oracle (CPU, gloo).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import DAL_ASCENDING, DAL_CANON_CHUNK, DAL_DESCENDING, DAL_KEY_NONE, DAL_ROW_GRANULE
+
+
+def shard_rows(n_total: int, world: int) -> int:
+    """Rows per shard: ceil(N / P) rounded up to the row granule (512)."""
+    per = -(-n_total // world)
+    return -(-per // DAL_ROW_GRANULE) * DAL_ROW_GRANULE
+
+
+def shard_range(n_total: int, world: int, rank: int):
+    s = shard_rows(n_total, world)
+    lo = min(rank * s, n_total)
+    hi = min(lo + s, n_total)
+    return lo, hi, s
+
+
+@dataclass
+class LocalTopk:
+    """A rank's exact local top-k, padded to k with DAL_KEY_NONE."""
+
+    keys: object  # int64 [k] (uint64 bit patterns)
+    idx: object  # int64 [k] global row indices
+    scores: object  # fp64 [k]
+
+
+def merge_topk(keys_all, idx_all, scores_all, k: int, sort_fn):
+    """Deterministic merge of P gathered local top-k lists (rank-major).
+
+    Each list is sorted by (key, index) and shards are in global index order,
+    so sorting by (key, position) orders ties by global index; ``sort_fn``
+    returns the positions of the k best."""
+    torch = __import__("torch")
+    n = int(keys_all.shape[0])
+    pos = torch.arange(n, dtype=torch.int64, device=keys_all.device)
+    best = sort_fn(keys_all, pos, k)
+    valid = keys_all[best] != _as_i64(DAL_KEY_NONE)
+    best = best[valid]
+    return idx_all[best], scores_all[best]
+
+
+def _as_i64(u: int) -> int:
+    return u - (1 << 64) if u >= (1 << 63) else u
+
+
+class ShardedSelector:
+    """One rank's shard of the pool and its share of a selection step."""
+
+    def __init__(self, x_local, n_total: int, rank: int, world: int, excluded=None, device=None):
+        from .engine import PoolState
+
+        self.n_total, self.rank, self.world = int(n_total), int(rank), int(world)
+        self.lo, self.hi, self.shard = shard_range(self.n_total, self.world, self.rank)
+        if int(x_local.shape[0]) != self.hi - self.lo:
+            raise ValueError(f"rank {rank}: expected {self.hi - self.lo} rows, got {x_local.shape[0]}")
+        self.state = PoolState(x_local, excluded=excluded, device=device, row_base=self.lo,
+                               n_total=self.n_total, n_pad=self.shard)
+        self._density = None
+
+    # ---- phase A: local normalisation + canonical partials ------------
+    def prep(self):
+        """(u_local [shard, d_pad] fp32, partials [shard/256, d] fp64)."""
+        torch = __import__("torch")
+        st = self.state
+        u, _ = st.normalized()
+        parts = torch.zeros((self.shard // DAL_CANON_CHUNK, st.d), dtype=torch.float64,
+                            device=st.device)
+        if st.n:
+            p = st.colsum_partials()
+            parts[: p.shape[0]] = p
+        return u, parts
+
+    # ---- phase B: density against all columns + local exact top-k ------
+    def local_density(self, u_full):
+        if self._density is None:
+            self._density = self.state.density_fixed(u_cols=u_full, n_cols_pad=int(u_full.shape[0]))
+            self.state.set_density_fixed(self._density)
+        return self._density
+
+    def local_select(self, u_full, partials_full, unlabeled_idx, forest, k: int, mode: str = "dw",
+                     strategy: str = "least_confidence", beta: float = 1.0) -> LocalTopk:
+        from .engine import (density_error, device_lut, dw_select_local, forest_score, topk_keys)
+        from .luts import ASCENDING
+
+        torch = __import__("torch")
+        st = self.state
+        keys = torch.full((k,), _as_i64(DAL_KEY_NONE), dtype=torch.int64, device=st.device)
+        idx = torch.full((k,), -1, dtype=torch.int64, device=st.device)
+        scores = torch.full((k,), float("nan"), dtype=torch.float64, device=st.device)
+        if st.n == 0:
+            return LocalTopk(keys, idx, scores)
+        flags, _, loc = st.row_flags(unlabeled_idx)
+        n_cand = int(loc.shape[0])
+        if n_cand == 0:
+            return LocalTopk(keys, idx, scores)
+        kk = min(k, n_cand)
+        if mode == "dw":
+            dens = self.local_density(u_full)
+            colsum = st.colsum(partials_full)
+            lut_dev = device_lut("entropy", forest.n_trees, st.device)
+            votes, sc, klo, khi = forest_score(st, forest, lut_dev, flags, DAL_DESCENDING, density=dens,
+                                               density_err=density_error(st), beta=beta, want_hi=True)
+            i, s, kk_keys = dw_select_local(st, flags, votes, klo, khi, lut_dev, kk, beta, colsum)
+        else:
+            order = DAL_ASCENDING if ASCENDING[strategy] else DAL_DESCENDING
+            lut_dev = device_lut(strategy, forest.n_trees, st.device)
+            votes, sc, kys, _ = forest_score(st, forest, lut_dev, flags, order)
+            i, kk_keys = topk_keys(kys, kk, st.row_base)
+            s = sc[i - st.row_base]
+        keys[:kk], idx[:kk], scores[:kk] = kk_keys, i, s
+        st.check_status()
+        return LocalTopk(keys, idx, scores)
+
+
+def hip_sort_positions(keys, pos, k):
+    from .engine import sort_pairs
+
+    _, out_pos, _ = sort_pairs(keys, pos, k)
+    return out_pos
+
+
+class TorchComm:
+    """all-gather over torch.distributed (RCCL on ROCm GPUs, gloo on CPU)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+
+    def all_gather(self, t):
+        torch = __import__("torch")
+        out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        self.dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        return out
+
+
+def select(sel: ShardedSelector, comm, unlabeled_idx, forest, k: int, mode: str = "dw",
+           strategy: str = "least_confidence", beta: float = 1.0, sort_fn=hip_sort_positions):
+    """One selection step across all ranks; returns (indices [k], scores [k]),
+    identical on every rank."""
+    u_local, parts = sel.prep()
+    u_full = comm.all_gather(u_local) if mode == "dw" and sel._density is None else None
+    parts_full = comm.all_gather(parts) if mode == "dw" else None
+    top = sel.local_select(u_full, parts_full, unlabeled_idx, forest, k, mode, strategy, beta)
+    keys_all = comm.all_gather(top.keys)
+    idx_all = comm.all_gather(top.idx)
+    sc_all = comm.all_gather(top.scores)
+    return merge_topk(keys_all, idx_all, sc_all, k, sort_fn)
+
+
+def emulate(selectors, unlabeled_idx, forest, k: int, mode: str = "dw",
+            strategy: str = "least_confidence", beta: float = 1.0, sort_fn=hip_sort_positions):
+    """Run P shards in one process (tests): the all-gathers become concatenations."""
+    torch = __import__("torch")
+    preps = [s.prep() for s in selectors]
+    u_full = torch.cat([p[0] for p in preps]) if mode == "dw" else None
+    parts_full = torch.cat([p[1] for p in preps]) if mode == "dw" else None
+    tops = [s.local_select(u_full, parts_full, unlabeled_idx, forest, k, mode, strategy, beta)
+            for s in selectors]
+    keys_all = torch.cat([t.keys for t in tops])
+    idx_all = torch.cat([t.idx for t in tops])
+    sc_all = torch.cat([t.scores for t in tops])
+    return merge_topk(keys_all, idx_all, sc_all, k, sort_fn)

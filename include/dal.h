@@ -1,0 +1,183 @@
+/*
+ * dal.h -- C ABI of the MI355X-native active-learning query-selection path.
+ *
+ * Drop-in boundary for the hot path of dv66/Distributed-Active-Learning
+ * (final_thesis/uncertainty_sampling.py, density_weighting.py,
+ * cosine_similarity.py, similarity.py).  The reference calls Spark MLlib over
+ * Py4J for every operation below; each entry point names the reference call
+ * site it replaces.  A maintainer binds these with ctypes;
+ * the in-tree binding is distributed-active-learning_amd/dal/_lib.py.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Every pointer is DEVICE memory owned by
+ *    the caller (the library never allocates); ``stream`` is a hipStream_t
+ *    (NULL = default stream) and every call is asynchronous and
+ *    stream-ordered.  No global mutable state: calls are re-entrant.
+ *  - Return value: DAL_OK (0) or a negative dal_status (argument / shape /
+ *    launch errors, detected on the host before or at launch).
+ *    Data-dependent conditions found by a kernel (zero-norm row, candidate
+ *    overflow) are OR-ed into the caller's device word ``dev_status``
+ *    (DAL_FLAG_*), which the caller reads after synchronising.
+ *  - Pool rows are fp32, row-major with leading dimension ``ldx`` (floats).
+ *  - Normalised pool buffer ``u``: [n_pad][d_pad] fp32, rows padded with zero
+ *    rows to dal_pad_rows(n), features padded with zeros to
+ *    dal_pad_features(d).  Zero rows/features contribute exactly 0.
+ *  - Density accumulator: int64 fixed point, value = acc * 2^-32
+ *    (DAL_FIXED_SCALE).  Integer adds are associative, so the density is
+ *    bit-identical for any launch geometry and any number of GPUs.
+ *  - Sort keys: uint64, smaller = better (dal_score_key() order); NaN scores
+ *    map to DAL_KEY_NAN (last), rows that are not candidates to DAL_KEY_NONE.
+ *    Ties are broken by the lower global row index.
+ */
+#ifndef DAL_H
+#define DAL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* dal_stream_t; /* hipStream_t */
+
+enum dal_status {
+  DAL_OK = 0,
+  DAL_ERR_ARG = -1,         /* null pointer / bad enum */
+  DAL_ERR_SHAPE = -2,       /* size, padding or alignment contract violated */
+  DAL_ERR_UNSUPPORTED = -3, /* e.g. tree deeper than DAL_MAX_TREE_DEPTH */
+  DAL_ERR_HIP = -4,         /* HIP launch / attribute failure */
+  DAL_ERR_CAPACITY = -5     /* k or candidate count above the kernel capacity */
+};
+
+/* bits OR-ed into *dev_status by kernels */
+#define DAL_FLAG_ZERO_NORM 1      /* a pool row has ||x|| == 0 (cosine undefined) */
+#define DAL_FLAG_CAND_OVERFLOW 2  /* re-rank candidate set exceeded capacity */
+
+/* per-row flags (uint8 per pool row) */
+#define DAL_ROW_CANDIDATE 1 /* row is in the unlabeled set and may be selected */
+#define DAL_ROW_EXCLUDED 2  /* row is in E: dropped from density as i and as j */
+
+#define DAL_ASCENDING 0
+#define DAL_DESCENDING 1
+
+#define DAL_KEY_NAN 0xFFFFFFFFFFFFFFFEull
+#define DAL_KEY_NONE 0xFFFFFFFFFFFFFFFFull
+#define DAL_FIXED_SCALE 4294967296.0 /* 2^32 */
+#define DAL_ROW_GRANULE 512
+#define DAL_CANON_CHUNK 256
+#define DAL_MAX_TREE_DEPTH 16
+#define DAL_SORT_CAP 8192          /* max pairs the single-block sort handles */
+#define DAL_SORT_CAP_PAYLOAD 4096  /* ... when it also carries an fp64 payload */
+
+const char* dal_status_string(int status);
+int dal_abi_version(void);
+int64_t dal_pad_rows(int64_t n);
+int64_t dal_pad_features(int64_t d);
+/* Rigorous bound |d_gemm - d_canonical| <= dal_density_error_bound(n_cols)
+ * for the fp32-MFMA density ("Density error bound"). */
+double dal_density_error_bound(int64_t n_cols);
+
+/* ---- (a1) row L2 normalisation --------------------------------------
+ * Replaces density_weighting.py:66 / cosine_similarity.py:28 /
+ * similarity.py:28  ``data.map(lambda _: _/np.linalg.norm(_))``.
+ * norm64[i] = sqrt(sum_d x_id^2) in fp64 (sequential over d, no FMA);
+ * u[i][d] = (float)(x_id / norm64[i]); rows with DAL_ROW_EXCLUDED and rows
+ * n..n_pad-1 are written as zeros (E is dropped as j: density_weighting.py:95-100).
+ * row_flags may be NULL.  A zero row sets DAL_FLAG_ZERO_NORM. */
+int dal_normalize_rows(const float* x, int64_t n, int64_t d, int64_t ldx,
+                       const uint8_t* row_flags, int64_t n_pad, int64_t d_pad,
+                       float* u, double* norm64, int32_t* dev_status, dal_stream_t stream);
+
+/* ---- canonical fp64 column sum (re-rank side of the density) -----------
+ * partials[c][f] = sum over rows c*256 .. c*256+255 (< n, not EXCLUDED) of
+ * x_rf / norm64[r], sequential in row order; rows of a shard start at a
+ * multiple of 256.  dal_canon_colsum_reduce sums partials sequentially over c. */
+int dal_canon_colsum_partials(const float* x, int64_t n, int64_t d, int64_t ldx,
+                              const double* norm64, const uint8_t* row_flags,
+                              double* partials, dal_stream_t stream);
+int dal_canon_colsum_reduce(const double* partials, int64_t n_chunks, int64_t d,
+                            double* colsum, dal_stream_t stream);
+
+/* ---- (a2-a4) fused cosine Gram row-sum -------------------------------
+ * Replaces density_weighting.py:67-75 (IndexedRowMatrix -> BlockMatrix
+ * U.multiply(UT) -> toCoordinateMatrix().entries), :95-100 (L0 exclusion) and
+ * :157-161 (groupByKey sum):  acc[i] += sum_j <u_rows[i], u_cols[j]> * 2^32.
+ * Tiled fp32 MFMA (v_mfma_f32_32x32x2_f32) with the row-sum fused into the
+ * accumulators; S is never materialised.  acc must be zeroed by the caller
+ * (the call accumulates, so it can be issued once per column shard).
+ * n_rows_pad % 256 == 0, n_cols_pad % 512 == 0, d_pad from dal_pad_features,
+ * ld >= d_pad (floats).  grid_blocks <= 0 selects one block per CU. */
+int dal_gram_rowsum(const float* u_rows, int64_t n_rows_pad, const float* u_cols,
+                    int64_t n_cols_pad, int64_t d_pad, int64_t ld, int64_t* acc,
+                    int grid_blocks, dal_stream_t stream);
+
+/* ---- (a5-a10) forest votes + uncertainty / density-weighted score ------
+ * Replaces uncertainty_sampling.py:88-98 / density_weighting.py:136-167:
+ * T x DecisionTreeModel.predict, groupByKey vote sum, the LUT score and the
+ * e*d product.  Forest in complete-heap SoA layout (dal/forest.py):
+ *   inner[t][h] = {feature (int32), threshold bits (fp32, rounded toward -inf
+ *   from fp64 so that x32 <= t32  <=>  x <= t64)}, h < 2^depth - 1,
+ *   leaf[t][l] in {0,1}, l < 2^depth.  x[f] <= thr -> child 2h+1, else 2h+2.
+ * lut: fp64[T+1].  density (nullable) -> uncertainty mode: score = lut[v];
+ * else score = lut[v] * d^beta with d = density*2^-32 (NaN for EXCLUDED rows).
+ * keys[i] = dal score key for ``order`` (DAL_KEY_NONE when not CANDIDATE).
+ * In density mode the GEMM density is approximate, so each score is an
+ * interval [score - err_i, score + err_i], err_i = |lut[v]| * density_err
+ * (beta = 1; the d^beta image of the interval otherwise): keys[i] is the
+ * PESSIMISTIC end's key and keys_hi[i] (nullable) the OPTIMISTIC end's key;
+ * exact scores (lut[v] == 0 or NaN) have keys[i] == keys_hi[i]. */
+int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ldx,
+                     const int32_t* inner, const uint8_t* leaf, int32_t n_trees, int32_t depth,
+                     const double* lut, const int64_t* density, double density_err,
+                     const uint8_t* row_flags, double beta, int order,
+                     int32_t* votes, double* scores, uint64_t* keys, uint64_t* keys_hi,
+                     dal_stream_t stream);
+
+/* ---- (a11) top-k: sortBy(score).take(k) --------------------------------
+ * Replaces uncertainty_sampling.py:106,109 / density_weighting.py:168,172.
+ * The k smallest keys, ties -> lower index; out_idx = idx_base + row, sorted
+ * by (key, index).  1 <= k <= min(n, DAL_SORT_CAP).  Exact radix select
+ * (8 x 8-bit digit histograms) + ordered compaction + one-block bitonic sort. */
+size_t dal_topk_workspace_bytes(int64_t n, int64_t k);
+int dal_topk(const uint64_t* keys, int64_t n, int64_t k, int64_t idx_base, void* ws,
+             size_t ws_bytes, int64_t* out_idx, uint64_t* out_keys, dal_stream_t stream);
+
+/* ---- density-weighted selection with exact fp64 re-rank ----------------
+ * Given the interval keys written by dal_forest_score (density mode,
+ * DAL_DESCENDING): K = k-th smallest pessimistic key; every row whose
+ * optimistic key is < K (or == K with a non-point interval) plus the first k
+ * point-interval rows == K (row order) are candidates -- a superset of the
+ * canonical top-k.  Each candidate's canonical fp64 score
+ *   lut[v] * (sum_f (x_if / norm64[i]) * colsum[f])^beta   (sequential, no FMA)
+ * is recomputed and the k best by (score desc, NaN last, index asc) are
+ * returned: bit-exact with the fp64 oracle.  out_scores are the canonical
+ * fp64 scores, out_keys (nullable) their keys.  More than
+ * DAL_SORT_CAP_PAYLOAD candidates sets DAL_FLAG_CAND_OVERFLOW. */
+size_t dal_dw_select_workspace_bytes(int64_t n, int64_t k);
+int dal_dw_select(const uint64_t* keys_lo, const uint64_t* keys_hi, const int32_t* votes,
+                  const uint8_t* row_flags, int64_t n, int64_t k, int64_t idx_base,
+                  const double* lut, double beta, const float* x, int64_t d, int64_t ldx,
+                  const double* norm64, const double* colsum, void* ws, size_t ws_bytes,
+                  int64_t* out_idx, double* out_scores, uint64_t* out_keys,
+                  int32_t* dev_status, dal_stream_t stream);
+
+/* ---- multi-GPU merge ----------------------------------------------------
+ * Sort n (key, idx) pairs (e.g. the all-gathered per-GPU top-k lists) by
+ * (key, idx) and keep the first k.  n <= DAL_SORT_CAP.  ``payload`` (nullable)
+ * is permuted alongside (then n <= DAL_SORT_CAP_PAYLOAD). */
+int dal_sort_pairs(const uint64_t* keys, const int64_t* idx, const double* payload, int64_t n,
+                   int64_t k, uint64_t* out_keys, int64_t* out_idx, double* out_payload,
+                   dal_stream_t stream);
+
+/* ---- standalone similarity kernels --------------------------------------
+ * cosine_similarity.py:42-45: every entry of U.U^T (fp32 MFMA), written to
+ * out[n_pad][n_pad] (fp32).  similarity.py:38 (columnSimilarities, i<j) is
+ * the strict upper triangle of the same matrix. */
+int dal_gram_entries(const float* u, int64_t n_pad, int64_t d_pad, int64_t ld, float* out,
+                     dal_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DAL_H */

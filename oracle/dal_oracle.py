@@ -1,0 +1,417 @@
+"""CPU oracle for the query-selection hot path -- TEST INFRASTRUCTURE ONLY.
+
+This module is the checker, never the product.  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+it.  The product path (``distributed-active-learning_amd/dal``) never imports
+anything under ``oracle/`` and fails loudly when its HIP library is missing.
+
+It restates, in NumPy float64, the arithmetic of the reference's hot path
+(dv66/Distributed-Active-Learning, PySpark 2.1 + MLlib 2.1):
+
+* per-tree hard votes        final_thesis/uncertainty_sampling.py:88-97
+                             final_thesis/density_weighting.py:136-145
+                             lal_direct_mllib_implementation/classes/active_learner.py:172-189
+* least confidence           final_thesis/uncertainty_sampling.py:98
+                             lal_direct_mllib_implementation/classes/active_learner.py:197
+* one-sided "entropy"        final_thesis/density_weighting.py:148
+* row L2 normalisation       final_thesis/density_weighting.py:66, cosine_similarity.py:28,
+                             similarity.py:28
+* Gram U.U^T (BlockMatrix)   final_thesis/density_weighting.py:67-75, cosine_similarity.py:29-45
+* L0 exclusion               final_thesis/density_weighting.py:95-100
+* density row-sum            final_thesis/density_weighting.py:157-161
+* score = e * d              final_thesis/density_weighting.py:166-167
+* sortBy + take(k)           final_thesis/uncertainty_sampling.py:106,109 (ascending)
+                             final_thesis/density_weighting.py:168,172 (descending)
+* columnSimilarities (i<j)   final_thesis/similarity.py:34-38
+
+Parity status (see DESIGN.md "Oracle"): the reference cannot run here (no
+pyspark, no JVM; the arithmetic lives in the un-vendored Spark 2.1.0 MLlib jar).
+The look-up tables are PINNED by the known-answer values printed in the
+reference's own run log (final_thesis/results/striatum_distDW_window_10_samples_5000.txt).
+Votes are cross-checked against scikit-learn's per-tree ``predict`` (same
+``x <= t`` rule), and the Gram row-sum against the separable form; everything
+else is a restatement from the reference source -- "parity unpinned" at the
+Spark boundary beyond the LUT known-answer test.
+
+Canonical semantics (frozen):
+  votes   v_i = sum_t tree_t(x_i) in {0..T}, MLlib Node.predict: x[f] <= thr -> left
+  LUTs    lc[v]  = abs(0.5 - (1 - (v/T)))        ascending
+          mg[v]  = abs((v/T) - (1 - (v/T)))      ascending (build extension)
+          ent[v] = -(1-(v/T)) * log2(1-(v/T))    descending; v=0 -> -0.0, v=T -> NaN
+  density d_i = sum_{j not in E} <u_i, u_j>,  u = x / ||x||   (d_i = NaN for i in E)
+  score   US = lut[v];  DW = ent[v] * d^beta
+  select  sort by (score in order, NaN last, -0.0 == +0.0, then global index asc); take k
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+# Row-chunk of the canonical fp64 column sum.  The product's re-rank kernel
+# uses the same chunking so that the fp64 sum order (and hence every bit of
+# the canonical density) is identical for any number of GPUs.
+CANON_CHUNK = 256
+
+STRATEGIES = ("least_confidence", "margin", "entropy")
+ASCENDING = {"least_confidence": True, "margin": True, "entropy": False}
+
+
+# --------------------------------------------------------------------------
+# Look-up tables (fp64, evaluated with Python float ops in the reference order)
+# --------------------------------------------------------------------------
+def lut_least_confidence(T: int) -> np.ndarray:
+    """uncertainty_sampling.py:98 -- ``abs(0.5 - (1-(_[1]/n_estimators)))``."""
+    return np.array([abs(0.5 - (1 - (v / T))) for v in range(T + 1)], dtype=np.float64)
+
+
+def lut_margin(T: int) -> np.ndarray:
+    """Binary margin |p1 - p0| (north-star extension; not in the reference)."""
+    return np.array([abs((v / T) - (1 - (v / T))) for v in range(T + 1)], dtype=np.float64)
+
+
+def _log2_ref(p: float) -> float:
+    # The reference log prints 0.13680278410054497 for v=1 (T=10); only
+    # log(x)/log(2) reproduces that last bit (numpy 2.2's log2 gives ...494).
+    return math.log(p) / math.log(2)
+
+
+def lut_entropy(T: int) -> np.ndarray:
+    """density_weighting.py:148 -- ``-(1-(v/T)) * np.log2(1-(v/T))``.
+
+    v=0 -> -1 * 0.0 = -0.0;  v=T -> -(0.0) * log2(0) = NaN (0 * -inf).
+    """
+    out = []
+    for v in range(T + 1):
+        p0 = 1 - (v / T)
+        if p0 > 0.0:
+            out.append(-(p0) * _log2_ref(p0))
+        else:
+            out.append(float("nan"))
+    return np.array(out, dtype=np.float64)
+
+
+def lut(strategy: str, T: int) -> np.ndarray:
+    if strategy == "least_confidence":
+        return lut_least_confidence(T)
+    if strategy == "margin":
+        return lut_margin(T)
+    if strategy == "entropy":
+        return lut_entropy(T)
+    raise ValueError(f"unknown strategy {strategy!r}")
+
+
+# --------------------------------------------------------------------------
+# Forest (MLlib DecisionTreeModel semantics, flattened)
+# --------------------------------------------------------------------------
+@dataclass
+class OracleForest:
+    """Flattened binary-classification forest.
+
+    feature[n] < 0 marks a leaf whose class (0/1) is value[n]; internal node n
+    sends x to left[n] when ``x[feature[n]] <= threshold[n]`` (fp64 compare,
+    MLlib 2.1 ``Node.predict`` for continuous splits), else right[n].
+    Node indices are global (roots[t] is tree t's root).
+    """
+
+    feature: np.ndarray  # int32 [n_nodes]
+    threshold: np.ndarray  # float64 [n_nodes]
+    left: np.ndarray  # int32 [n_nodes]
+    right: np.ndarray  # int32 [n_nodes]
+    value: np.ndarray  # int32 [n_nodes] (leaf class)
+    roots: np.ndarray  # int32 [T]
+
+    @property
+    def n_trees(self) -> int:
+        return int(self.roots.shape[0])
+
+
+def tree_predictions(forest: OracleForest, X: np.ndarray) -> np.ndarray:
+    """Per-tree hard predictions, [T, N] int32.
+
+    uncertainty_sampling.py:89-93: ``DecisionTreeModel(tree).predict(...)``
+    for every tree of ``model._java_model.trees()``.
+    """
+    X64 = np.asarray(X, dtype=np.float64)
+    n = X64.shape[0]
+    rows = np.arange(n)
+    out = np.empty((forest.n_trees, n), dtype=np.int32)
+    for t, root in enumerate(forest.roots):
+        node = np.full(n, root, dtype=np.int64)
+        while True:
+            f = forest.feature[node]
+            internal = f >= 0
+            if not internal.any():
+                break
+            fi = np.where(internal, f, 0)
+            go_left = X64[rows, fi] <= forest.threshold[node]
+            nxt = np.where(go_left, forest.left[node], forest.right[node])
+            node = np.where(internal, nxt, node)
+        out[t] = forest.value[node]
+    return out
+
+
+def votes(forest: OracleForest, X: np.ndarray) -> np.ndarray:
+    """uncertainty_sampling.py:96 -- ``groupByKey().mapValues(sum)`` of the
+    per-tree 0/1 predictions: v_i in {0..T} (int32)."""
+    return tree_predictions(forest, X).sum(axis=0).astype(np.int32)
+
+
+# --------------------------------------------------------------------------
+# Cosine density
+# --------------------------------------------------------------------------
+def l2_normalize(X: np.ndarray) -> np.ndarray:
+    """density_weighting.py:66 -- ``_/np.linalg.norm(_)`` in fp64.
+
+    Canonical order: ||x||^2 summed sequentially over features (mul, then add;
+    no fused multiply-add), correctly-rounded sqrt and divide.  Zero rows are
+    rejected (the reference would propagate NaN through every density).
+    """
+    X64 = np.asarray(X, dtype=np.float64)
+    n2 = np.zeros(X64.shape[0], dtype=np.float64)
+    for d in range(X64.shape[1]):
+        col = X64[:, d]
+        n2 = n2 + col * col
+    if np.any(n2 == 0.0):
+        raise ValueError("zero-norm row in pool (cosine undefined)")
+    norm = np.sqrt(n2)
+    return X64 / norm[:, None]
+
+
+def exclusion_mask(n: int, excluded) -> np.ndarray:
+    m = np.zeros(n, dtype=bool)
+    if excluded is not None and len(excluded):
+        m[np.asarray(excluded, dtype=np.int64)] = True
+    return m
+
+
+def gram(X: np.ndarray) -> np.ndarray:
+    """cosine_similarity.py:42 -- ``U.multiply(UT)``: full N x N (diagonal included)."""
+    U = l2_normalize(X)
+    return U @ U.T
+
+
+def density_gram(X: np.ndarray, excluded=None) -> np.ndarray:
+    """Reference algorithm (small N): full fp64 Gram, drop every entry with
+    i in E or j in E (density_weighting.py:95-100), raw row-sum including j=i
+    (density_weighting.py:157-161).  Rows in E have no entries -> NaN."""
+    S = gram(X)
+    ex = exclusion_mask(X.shape[0], excluded)
+    S[:, ex] = 0.0
+    d = S.sum(axis=1)
+    d[ex] = np.nan
+    return d
+
+
+def column_sum_canonical(U: np.ndarray, excluded_mask: np.ndarray) -> np.ndarray:
+    """s = sum_{j not in E} u_j in the canonical order: sequential within
+    CANON_CHUNK-row chunks, then sequential over chunks."""
+    n, D = U.shape
+    n_chunks = (n + CANON_CHUNK - 1) // CANON_CHUNK
+    pad = n_chunks * CANON_CHUNK - n
+    Uz = np.where(excluded_mask[:, None], 0.0, U)
+    keep = ~excluded_mask
+    if pad:
+        Uz = np.concatenate([Uz, np.zeros((pad, D))])
+        keep = np.concatenate([keep, np.zeros(pad, dtype=bool)])
+    Uc = Uz.reshape(n_chunks, CANON_CHUNK, D)
+    kc = keep.reshape(n_chunks, CANON_CHUNK)
+    acc = np.zeros((n_chunks, D), dtype=np.float64)
+    for r in range(CANON_CHUNK):
+        # skipped (excluded / padding) rows are not added at all
+        acc = np.where(kc[:, r, None], acc + Uc[:, r, :], acc)
+    s = np.zeros(D, dtype=np.float64)
+    for c in range(n_chunks):
+        s = s + acc[c]
+    return s
+
+
+def density_canonical(X: np.ndarray, excluded=None, rows=None) -> np.ndarray:
+    """Canonical fp64 density via the exact identity
+    sum_j <u_i,u_j> = <u_i, sum_j u_j>, summed in the frozen order
+    (d_i = sequential over features of u_id * s_d).  Equals density_gram to
+    ~1e-15 relative; it is the definition the selected set is bit-exact to."""
+    U = l2_normalize(X)
+    ex = exclusion_mask(X.shape[0], excluded)
+    s = column_sum_canonical(U, ex)
+    sel = np.arange(X.shape[0]) if rows is None else np.asarray(rows, dtype=np.int64)
+    Ui = U[sel]
+    d = np.zeros(Ui.shape[0], dtype=np.float64)
+    for k in range(U.shape[1]):
+        d = d + Ui[:, k] * s[k]
+    d[ex[sel]] = np.nan
+    return d
+
+
+# --------------------------------------------------------------------------
+# Selection (canonical comparator)
+# --------------------------------------------------------------------------
+def order_key(scores: np.ndarray, ascending: bool) -> np.ndarray:
+    """Sortable float key: NaN last, -0.0 == +0.0 (adding +0.0 maps -0.0 to +0.0)."""
+    s = np.asarray(scores, dtype=np.float64) + 0.0
+    key = s if ascending else -s
+    return np.where(np.isnan(s), np.inf, key), np.isnan(s)
+
+
+def select_topk(scores: np.ndarray, index: np.ndarray, k: int, ascending: bool):
+    """sortBy(score).take(k) with the canonical deterministic tie rule:
+    (score in order, NaN last, -0.0 == +0.0, then global index ascending)."""
+    scores = np.asarray(scores, dtype=np.float64)
+    index = np.asarray(index, dtype=np.int64)
+    key, isnan = order_key(scores, ascending)
+    # lexsort: last key is primary
+    order = np.lexsort((index, key, isnan.astype(np.int8)))
+    take = order[: min(k, len(order))]
+    return index[take], scores[take]
+
+
+def uncertainty_select(X, unlabeled_idx, forest: OracleForest, k: int,
+                       strategy: str = "least_confidence"):
+    """One loop iteration of uncertainty_sampling.py:85-112 (aligned per-row
+    scores as in active_learner.py:160-203).  Returns (scores[U], sel_idx, sel_scores)."""
+    unl = np.asarray(unlabeled_idx, dtype=np.int64)
+    v = votes(forest, np.asarray(X)[unl])
+    table = lut(strategy, forest.n_trees)
+    sc = table[v]
+    sel_idx, sel_sc = select_topk(sc, unl, k, ASCENDING[strategy])
+    return sc, sel_idx, sel_sc
+
+
+def density_select(X, unlabeled_idx, forest: OracleForest, k: int, beta: float = 1.0,
+                   excluded=None, density=None):
+    """One loop iteration of density_weighting.py:133-176:
+    score = ent[v] * d^beta (descending).  ``excluded`` defaults to the
+    reference's L0 = range(window) -- here the caller passes it explicitly."""
+    unl = np.asarray(unlabeled_idx, dtype=np.int64)
+    Xn = np.asarray(X)
+    if density is None:
+        density = density_canonical(Xn, excluded)
+    d = np.asarray(density, dtype=np.float64)[unl]
+    v = votes(forest, Xn[unl])
+    e = lut_entropy(forest.n_trees)[v]
+    dp = d if beta == 1.0 else np.power(d, beta)
+    sc = e * dp
+    sel_idx, sel_sc = select_topk(sc, unl, k, ascending=False)
+    return sc, sel_idx, sel_sc
+
+
+# --------------------------------------------------------------------------
+# Standalone similarity kernels
+# --------------------------------------------------------------------------
+def cosine_entries(X: np.ndarray) -> np.ndarray:
+    """cosine_similarity.py:42-45: every entry of U.U^T (N x N, fp64)."""
+    return gram(X)
+
+
+def column_similarities(X: np.ndarray):
+    """similarity.py:34-38: ``RowMatrix(points-as-columns).columnSimilarities()``
+    -> exact cos(x_i, x_j) for i < j (no diagonal).  Returns (i, j, value)."""
+    S = gram(X)
+    i, j = np.triu_indices(S.shape[0], k=1)
+    return i, j, S[i, j]
+
+
+def max_cosine(X: np.ndarray, labeled_idx):
+    """Config 5 restatement of similarity.py: m_i = max_{l in L} cos(x_i, x_l)
+    and its arg-max (first l on ties).  fp64 on the given inputs."""
+    U = l2_normalize(X)
+    L = np.asarray(labeled_idx, dtype=np.int64)
+    S = U @ U[L].T
+    arg = np.argmax(S, axis=1)
+    return S[np.arange(S.shape[0]), arg], arg.astype(np.int32)
+
+
+def diversity_select(X, labeled_idx, k: int, candidates=None):
+    """Select the k rows least similar to the labeled set (ascending max-cos,
+    ties -> lower index).  ``candidates`` defaults to every row."""
+    m, _ = max_cosine(X, labeled_idx)
+    idx = np.arange(X.shape[0]) if candidates is None else np.asarray(candidates)
+    return select_topk(m[idx], idx, k, ascending=True)
+
+
+# --------------------------------------------------------------------------
+# Synthetic inputs of the BASELINE.json configs (shared with bench/tests)
+# --------------------------------------------------------------------------
+def synthetic_pool(n: int, d: int, seed: int = 0, dist: str = "uniform") -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    if dist == "uniform":
+        return rng.random((n, d), dtype=np.float32)
+    if dist == "normal":
+        return rng.standard_normal((n, d), dtype=np.float32)
+    raise ValueError(dist)
+
+
+def synthetic_forest(n_trees: int, depth: int, n_features: int, seed: int = 1,
+                     dist: str = "uniform") -> OracleForest:
+    """T complete depth-``depth`` trees in heap order: feature ~ U{0..D-1},
+    threshold ~ U(0,1) (or N(0,1)) rounded to fp32, leaf class ~ Bernoulli(0.5)."""
+    rng = np.random.default_rng(seed)
+    n_int = (1 << depth) - 1
+    n_leaf = 1 << depth
+    per = n_int + n_leaf
+    feat, thr, left, right, val, roots = [], [], [], [], [], []
+    for t in range(n_trees):
+        base = t * per
+        roots.append(base)
+        f = rng.integers(0, n_features, size=n_int)
+        if dist == "uniform":
+            th = rng.random(n_int).astype(np.float32).astype(np.float64)
+        else:
+            th = rng.standard_normal(n_int).astype(np.float32).astype(np.float64)
+        lv = rng.integers(0, 2, size=n_leaf)
+        for h in range(per):
+            if h < n_int:
+                feat.append(int(f[h]))
+                thr.append(float(th[h]))
+                left.append(base + 2 * h + 1)
+                right.append(base + 2 * h + 2)
+                val.append(0)
+            else:
+                feat.append(-1)
+                thr.append(0.0)
+                left.append(-1)
+                right.append(-1)
+                val.append(int(lv[h - n_int]))
+    return OracleForest(
+        feature=np.array(feat, dtype=np.int32),
+        threshold=np.array(thr, dtype=np.float64),
+        left=np.array(left, dtype=np.int32),
+        right=np.array(right, dtype=np.int32),
+        value=np.array(val, dtype=np.int32),
+        roots=np.array(roots, dtype=np.int32),
+    )
+
+
+def forest_from_sklearn(rf, positive_label=1) -> OracleForest:
+    """Flatten a fitted sklearn RandomForestClassifier into hard-vote trees
+    (vote = 1 when the tree's leaf class equals ``positive_label``)."""
+    classes = np.asarray(rf.classes_)
+    feat, thr, left, right, val, roots = [], [], [], [], [], []
+    base = 0
+    for est in rf.estimators_:
+        tr = est.tree_
+        roots.append(base)
+        for n in range(tr.node_count):
+            if tr.children_left[n] < 0:
+                feat.append(-1)
+                thr.append(0.0)
+                left.append(-1)
+                right.append(-1)
+                cls = classes[int(np.argmax(tr.value[n][0]))]
+                val.append(1 if cls == positive_label else 0)
+            else:
+                feat.append(int(tr.feature[n]))
+                thr.append(float(tr.threshold[n]))
+                left.append(base + int(tr.children_left[n]))
+                right.append(base + int(tr.children_right[n]))
+                val.append(0)
+        base += tr.node_count
+    return OracleForest(
+        feature=np.array(feat, dtype=np.int32),
+        threshold=np.array(thr, dtype=np.float64),
+        left=np.array(left, dtype=np.int32),
+        right=np.array(right, dtype=np.int32),
+        value=np.array(val, dtype=np.int32),
+        roots=np.array(roots, dtype=np.int32),
+    )

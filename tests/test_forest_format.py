@@ -1,0 +1,86 @@
+"""Forest SoA conversion (dal.forest) -- host logic, CPU only.
+
+The heap walk below is test infrastructure mirroring the kernel's traversal
+(x <= thr -> 2h+1 else 2h+2) so the layout can be checked without a GPU.
+"""
+import numpy as np
+import pytest
+from hypothesis import given, settings, strategies as st
+
+from conftest import golden_forest, load_golden
+from dal.forest import Forest, threshold_to_f32
+from oracle import dal_oracle as O
+
+
+def heap_votes(F: Forest, X):
+    X32 = np.asarray(X, dtype=np.float32)
+    n = X32.shape[0]
+    rows = np.arange(n)
+    n_inner = (1 << F.depth) - 1
+    v = np.zeros(n, dtype=np.int64)
+    thr = F.inner[:, :, 1].view(np.float32)
+    for t in range(F.n_trees):
+        h = np.zeros(n, dtype=np.int64)
+        for _ in range(F.depth):
+            f = F.inner[t, h, 0]
+            go_left = X32[rows, f] <= thr[t, h]
+            h = 2 * h + np.where(go_left, 1, 2)
+        v += F.leaf[t, h - n_inner]
+    return v
+
+
+@pytest.mark.parametrize("name,prefix", [("unlabeled_init.npz", "forest_"),
+                                         ("checkerboard2x2.npz", "it1_forest_"),
+                                         ("checkerboard2x2.npz", "it5_forest_"),
+                                         ("checkerboard4x4.npz", "it5_forest_"),
+                                         ("rotated_checkerboard2x2.npz", "it5_forest_"),
+                                         ("synthetic_1500x30_T100.npz", "forest_")])
+def test_heap_layout_votes_match_oracle(name, prefix):
+    g = load_golden(name)
+    of = golden_forest(g, prefix)
+    F = Forest.from_nodes(of.feature, of.threshold, of.left, of.right, of.value, of.roots)
+    assert F.depth <= 4 or prefix == "forest_"
+    X = g["X"]
+    assert np.array_equal(heap_votes(F, X), O.votes(of, X))
+
+
+def test_from_sklearn_matches_oracle_export():
+    from sklearn.ensemble import RandomForestClassifier
+
+    rng = np.random.default_rng(0)
+    X = rng.random((400, 6)).astype(np.float32)
+    y = (X[:, 0] + X[:, 1] > 1).astype(int)
+    rf = RandomForestClassifier(n_estimators=7, max_depth=6, random_state=3).fit(X, y)
+    F = Forest.from_sklearn(rf)
+    of = O.forest_from_sklearn(rf)
+    assert np.array_equal(heap_votes(F, X), O.votes(of, X))
+    hard = np.stack([e.predict(X) for e in rf.estimators_]).astype(int).sum(0)
+    assert np.array_equal(heap_votes(F, X), hard)
+
+
+def test_single_class_forest_votes():
+    from sklearn.ensemble import RandomForestClassifier
+
+    X = np.random.default_rng(1).random((20, 3)).astype(np.float32)
+    rf = RandomForestClassifier(n_estimators=4, max_depth=4, random_state=0).fit(X, np.ones(20, int))
+    F = Forest.from_sklearn(rf)
+    assert F.depth == 1  # single leaves padded to one always-left split
+    assert np.array_equal(heap_votes(F, X), np.full(20, 4))
+
+
+@settings(max_examples=300, deadline=None)
+@given(t=st.floats(allow_nan=False, width=64), x=st.floats(allow_nan=False, width=32))
+def test_threshold_rounding_preserves_compare(t, x):
+    t32 = threshold_to_f32(np.array([t]))[0]
+    assert (np.float32(x) <= t32) == (float(np.float32(x)) <= t)
+
+
+def test_depth_limit():
+    # a chain of 17 splits
+    n = 17
+    feat = list(range(n)) + [-1] * (n + 1)
+    left = [n + i for i in range(n)] + [-1] * (n + 1)
+    right = [i + 1 for i in range(n - 1)] + [2 * n] + [-1] * (n + 1)
+    with pytest.raises(ValueError):
+        Forest.from_nodes([f if f >= 0 else -1 for f in feat], np.zeros(2 * n + 1), left, right,
+                          np.zeros(2 * n + 1), [0])

@@ -1,0 +1,393 @@
+"""Parity of the HIP path (through the C ABI) with the CPU oracle and the
+committed golden fixtures.  Needs an MI355X: ``pytest -m gpu``.
+
+Bars (DESIGN.md "Parity"):
+  * votes, LUT scores, selected indices (+ their order), canonical selected
+    scores: bit-exact;
+  * GEMM density: within the rigorous bound dal_density_error_bound(N) and
+    1e-5 relative of the fp64 oracle;
+  * fp32 cosine entries: 2e-6 absolute.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_forest, load_golden
+from oracle import dal_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DENSITY_RTOL = 1e-5
+
+
+def _forest(of):
+    from dal.forest import Forest
+
+    return Forest.from_nodes(of.feature, of.threshold, of.left, of.right, of.value, of.roots)
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+# ------------------------------------------------------------ kernels -----
+def test_normalize_bit_exact(cuda):
+    import torch
+    from dal.engine import PoolState
+
+    X = O.synthetic_pool(3000, 61, seed=11)
+    st = PoolState(X, excluded=[3, 7], device=cuda)
+    u, norm = st.normalized()
+    X64 = X.astype(np.float64)
+    n2 = np.zeros(3000)
+    for d in range(61):
+        n2 = n2 + X64[:, d] * X64[:, d]
+    ref_norm = np.sqrt(n2)
+    assert np.array_equal(_np(norm), ref_norm)
+    ref_u = (X64 / ref_norm[:, None]).astype(np.float32)
+    ref_u[[3, 7]] = 0
+    got = _np(u)
+    assert got.shape == (3072, 64)
+    assert np.array_equal(got[:3000, :61], ref_u)
+    assert not got[:, 61:].any() and not got[3000:].any()
+    torch.cuda.synchronize()
+    st.check_status()
+
+
+def test_zero_norm_row_raises(cuda):
+    from dal import density_weighting as dw
+
+    X = O.synthetic_pool(600, 16, seed=1)
+    X[17] = 0
+    with pytest.raises(ValueError):
+        dw.information_density(X, device=cuda)
+
+
+@pytest.mark.parametrize("n,d", [(700, 30), (1000, 64), (513, 128), (300, 200)])
+def test_canonical_colsum_bit_exact(cuda, n, d):
+    from dal.engine import PoolState
+
+    X = O.synthetic_pool(n, d, seed=n)
+    E = [0, 1, 2, n - 1]
+    st = PoolState(X, excluded=E, device=cuda)
+    U = O.l2_normalize(X)
+    ref = O.column_sum_canonical(U, O.exclusion_mask(n, E))
+    assert np.array_equal(_np(st.colsum()), ref)
+
+
+@pytest.mark.parametrize("n,d,dist", [(4096, 256, "uniform"), (5000, 64, "uniform"),
+                                      (3000, 30, "normal"), (2100, 128, "uniform"),
+                                      (1200, 500, "uniform")])
+def test_gram_density_within_bound(cuda, n, d, dist):
+    from dal import _lib
+    from dal.engine import PoolState
+
+    X = O.synthetic_pool(n, d, seed=7, dist=dist)
+    E = list(range(10))
+    st = PoolState(X, excluded=E, device=cuda)
+    got = _np(st.density())
+    ref = O.density_canonical(X, E)
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    err = np.abs(got[ok] - ref[ok])
+    bound = _lib.load().dal_density_error_bound(n - len(E))
+    assert err.max() <= bound
+    # accuracy bar of the north star: 1e-5 relative (signed data: relative to sum |S_ij|)
+    scale = np.abs(O.l2_normalize(X) @ O.l2_normalize(X)[ok].T).sum(axis=1)[ok]
+    assert (err / scale).max() <= DENSITY_RTOL
+
+
+def test_gram_density_deterministic_across_grids(cuda):
+    """int64 fixed-point accumulation: identical bits for any grid/unit split."""
+    import torch
+    from dal import _lib
+    from dal.engine import PoolState, _ptr, _stream
+
+    X = O.synthetic_pool(6000, 64, seed=3)
+    st = PoolState(X, device=cuda)
+    u, _ = st.normalized()
+    outs = []
+    for grid in (0, 1, 7, 64, 300):
+        acc = torch.zeros(st.n_pad, dtype=torch.int64, device=cuda)
+        _lib.call("dal_gram_rowsum", _ptr(u), st.n_pad, _ptr(u), st.n_pad, st.d_pad, st.d_pad,
+                  _ptr(acc), grid, _stream(cuda))
+        outs.append(_np(acc))
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0])
+
+
+def test_gram_density_column_shards_add_up(cuda):
+    """Accumulating over column shards == one call (multi-GPU ring contract)."""
+    import torch
+    from dal import _lib
+    from dal.engine import PoolState, _ptr, _stream
+
+    X = O.synthetic_pool(4096, 64, seed=9)
+    st = PoolState(X, device=cuda)
+    u, _ = st.normalized()
+    full = torch.zeros(st.n_pad, dtype=torch.int64, device=cuda)
+    _lib.call("dal_gram_rowsum", _ptr(u), st.n_pad, _ptr(u), st.n_pad, 64, 64, _ptr(full), 0,
+              _stream(cuda))
+    part = torch.zeros_like(full)
+    for c0 in range(0, st.n_pad, 1024):
+        _lib.call("dal_gram_rowsum", _ptr(u), st.n_pad, _ptr(u[c0:]), 1024, 64, 64, _ptr(part), 0,
+                  _stream(cuda))
+    assert torch.equal(full, part)
+
+
+# ------------------------------------------------------------- forest -----
+FOREST_CASES = [("unlabeled_init.npz", "forest_", "votes"),
+                ("checkerboard2x2.npz", "it1_forest_", "it1_votes"),
+                ("checkerboard2x2.npz", "it5_forest_", "it5_votes"),
+                ("checkerboard4x4.npz", "it5_forest_", "it5_votes"),
+                ("rotated_checkerboard2x2.npz", "it5_forest_", "it5_votes"),
+                ("synthetic_512x64_T10.npz", "forest_", "votes"),
+                ("synthetic_4096x256_T10.npz", "forest_", "votes"),
+                ("synthetic_1500x30_T100.npz", "forest_", "votes")]
+
+
+@pytest.mark.parametrize("name,prefix,vkey", FOREST_CASES)
+def test_forest_votes_bit_exact(cuda, name, prefix, vkey):
+    from dal import uncertainty_sampling as us
+
+    g = load_golden(name)
+    F = _forest(golden_forest(g, prefix))
+    n = g["X"].shape[0]
+    sel = us.select(g["X"], np.arange(n), F, 1, device=cuda)
+    assert np.array_equal(_np(sel.votes), g[vkey])
+
+
+def test_forest_deep_sklearn_trees(cuda):
+    from sklearn.ensemble import RandomForestClassifier
+    from dal import uncertainty_sampling as us
+    from dal.forest import Forest
+
+    rng = np.random.default_rng(4)
+    X = rng.random((3000, 300)).astype(np.float32)  # D > 255: global-memory rows
+    y = (X[:, 0] + X[:, 5] * X[:, 9] > 0.8).astype(int)
+    rf = RandomForestClassifier(n_estimators=13, max_depth=9, random_state=0).fit(X[:500], y[:500])
+    F = Forest.from_sklearn(rf)
+    sel = us.select(X, np.arange(3000), F, 5, device=cuda)
+    assert np.array_equal(_np(sel.votes), O.votes(O.forest_from_sklearn(rf), X))
+
+
+# ---------------------------------------------------------- selection -----
+US_CASES = [("unlabeled_init.npz", "", (1, 2)),
+            ("checkerboard2x2.npz", "it1_", (1, 10)), ("checkerboard2x2.npz", "it5_", (1, 10)),
+            ("checkerboard4x4.npz", "it1_", (1, 10)), ("checkerboard4x4.npz", "it5_", (1, 10)),
+            ("rotated_checkerboard2x2.npz", "it5_", (1, 10)),
+            ("synthetic_512x64_T10.npz", "", (1, 10, 100)),
+            ("synthetic_4096x256_T10.npz", "", (1, 10, 100)),
+            ("synthetic_1500x30_T100.npz", "", (1, 10, 100))]
+
+
+@pytest.mark.parametrize("name,it,ks", US_CASES)
+@pytest.mark.parametrize("strategy", O.STRATEGIES)
+def test_uncertainty_select_golden(cuda, name, it, ks, strategy):
+    from dal import uncertainty_sampling as us
+
+    g = load_golden(name)
+    F = _forest(golden_forest(g, it + "forest_"))
+    unl = g[it + "unlabeled"]
+    for k in ks:
+        sel = us.select(g["X"], unl, F, k, strategy=strategy, device=cuda)
+        assert np.array_equal(_np(sel.indices), g[f"{it}us_{strategy}_k{k}_idx"]), k
+        exp = g[f"{it}us_{strategy}_k{k}_scores"]
+        got = _np(sel.selected_scores)
+        assert np.array_equal(got, exp, equal_nan=True)
+        assert np.array_equal(np.signbit(got), np.signbit(exp))
+    assert np.array_equal(_np(sel.scores), g[f"{it}us_{strategy}_scores"], equal_nan=True)
+
+
+DW_CASES = [("checkerboard2x2.npz", "it1_", (1, 10)), ("checkerboard2x2.npz", "it5_", (1, 10)),
+            ("checkerboard4x4.npz", "it5_", (1, 10)),
+            ("rotated_checkerboard2x2.npz", "it1_", (1, 10)),
+            ("rotated_checkerboard2x2.npz", "it5_", (1, 10)),
+            ("synthetic_512x64_T10.npz", "", (1, 10, 100)),
+            ("synthetic_4096x256_T10.npz", "", (1, 10, 100)),
+            ("synthetic_1500x30_T100.npz", "", (1, 10, 100))]
+
+
+@pytest.mark.parametrize("name,it,ks", DW_CASES)
+def test_density_select_golden(cuda, name, it, ks):
+    from dal import density_weighting as dw
+    from dal.engine import PoolState
+
+    g = load_golden(name)
+    F = _forest(golden_forest(g, it + "forest_"))
+    unl = g[it + "unlabeled"]
+    st = PoolState(g["X"], excluded=g["excluded"], device=cuda)
+    for k in ks:
+        sel = dw.select(st, unl, F, k)
+        assert np.array_equal(_np(sel.indices), g[f"{it}dw_k{k}_idx"]), k
+        exp = g[f"{it}dw_k{k}_scores"]
+        got = _np(sel.selected_scores)
+        assert np.array_equal(got, exp, equal_nan=True), k
+        assert np.array_equal(np.signbit(got), np.signbit(exp))
+    # every returned score is within the density bound of the oracle's
+    ref = g[f"{it}dw_scores"]
+    got = _np(sel.scores)
+    ok = ~np.isnan(ref)
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    assert np.allclose(got[ok], ref[ok], rtol=DENSITY_RTOL, atol=1e-9)
+
+
+def test_unlabeled_init_density_config1(cuda):
+    from dal import density_weighting as dw
+
+    g = load_golden("unlabeled_init.npz")
+    F = _forest(golden_forest(g))
+    for k in (1, 2):
+        sel = dw.select(g["X"], g["unlabeled"], F, k, excluded_idx=[])
+        assert np.array_equal(_np(sel.indices), g[f"dw_k{k}_idx"])
+        assert np.array_equal(_np(sel.selected_scores), g[f"dw_k{k}_scores"], equal_nan=True)
+
+
+# -------------------------------------------------------------- top-k -----
+def test_topk_edge_cases(cuda):
+    import torch
+    from dal.engine import topk_keys
+
+    rng = np.random.default_rng(0)
+    # all equal keys -> lowest indices
+    keys = torch.full((5000,), 7, dtype=torch.int64, device=cuda)
+    idx, _ = topk_keys(keys, 37)
+    assert _np(idx).tolist() == list(range(37))
+    # k == n, random with duplicates, index base
+    kv = rng.integers(0, 50, size=3000)
+    keys = torch.from_numpy(kv.astype(np.int64)).to(cuda)
+    idx, k_out = topk_keys(keys, 3000, idx_base=1000)
+    exp = np.lexsort((np.arange(3000), kv)) + 1000
+    assert np.array_equal(_np(idx), exp)
+    # full 64-bit range incl. "negative" int64 bit patterns (unsigned order)
+    kv = rng.integers(0, 2**63 - 1, size=20000, dtype=np.int64)
+    kv[::3] = -kv[::3]
+    keys = torch.from_numpy(kv).to(cuda)
+    idx, _ = topk_keys(keys, 1000)
+    u = kv.view(np.uint64)
+    exp = np.lexsort((np.arange(20000), u))[:1000]
+    assert np.array_equal(_np(idx), exp)
+    # k = 1
+    idx, _ = topk_keys(keys, 1)
+    assert _np(idx)[0] == exp[0]
+
+
+def test_sort_pairs_merge(cuda):
+    import torch
+    from dal.engine import sort_pairs
+
+    rng = np.random.default_rng(1)
+    kv = rng.integers(0, 100, size=7000).astype(np.int64)
+    iv = rng.permutation(7000).astype(np.int64)
+    pay = rng.random(7000)
+    ok, oi, _ = sort_pairs(torch.from_numpy(kv).to(cuda), torch.from_numpy(iv).to(cuda), 500)
+    order = np.lexsort((iv, kv))[:500]
+    assert np.array_equal(_np(oi), iv[order])
+    ok, oi, op = sort_pairs(torch.from_numpy(kv[:4000]).to(cuda), torch.from_numpy(iv[:4000]).to(cuda),
+                            100, payload=torch.from_numpy(pay[:4000]).to(cuda))
+    order = np.lexsort((iv[:4000], kv[:4000]))[:100]
+    assert np.array_equal(_np(oi), iv[order])
+    assert np.array_equal(_np(op), pay[order])
+
+
+def test_dw_all_ties_first_iteration(cuda):
+    """Reference log iteration 1: every score is -0.0 (votes 0) -> the k lowest
+    unlabeled indices, score -0.0 (striatum_distDW_window_10_samples_5000.txt:3)."""
+    from dal import density_weighting as dw
+    from dal.forest import Forest
+
+    X = O.synthetic_pool(5000, 20, seed=2)
+    inner = np.zeros((10, 1, 2), np.int32)
+    inner[:, :, 1] = np.array([np.inf], np.float32).view(np.int32)[0]
+    F = Forest(inner=inner, leaf=np.zeros((10, 2), np.uint8), depth=1)
+    unl = np.arange(10, 5000)
+    sel = dw.select(X, unl, F, 10, excluded_idx=np.arange(10))
+    assert _np(sel.indices).tolist() == list(range(10, 20))
+    s = _np(sel.selected_scores)
+    assert np.all(s == 0) and np.all(np.signbit(s))
+
+
+def test_dw_nan_scores_rank_last(cuda):
+    from dal import density_weighting as dw
+    from dal.forest import Forest
+
+    X = O.synthetic_pool(800, 8, seed=3)
+    inner = np.zeros((4, 1, 2), np.int32)
+    inner[:, 0, 0] = 0
+    inner[:, 0, 1] = np.array([0.5], np.float32).view(np.int32)[0]
+    leaf = np.array([[1, 1]] * 4, np.uint8)  # every tree votes 1 -> v = T -> NaN
+    leaf[0] = [0, 1]  # rows with x0 <= 0.5 get v = 3 (finite), others NaN
+    F = Forest(inner=inner, leaf=leaf, depth=1)
+    unl = np.arange(800)
+    sel = dw.select(X, unl, F, 800)
+    of = O.OracleForest  # oracle reference via the golden-free path
+    ref_sc, ref_idx, ref_ss = O.density_select(X, unl, _oracle_from(F), 800, 1.0, None)
+    assert np.array_equal(_np(sel.indices), ref_idx)
+    assert np.array_equal(_np(sel.selected_scores), ref_ss, equal_nan=True)
+
+
+def _oracle_from(F):
+    """Heap-layout Forest -> oracle node arrays (test helper)."""
+    feat, thr, left, right, val, roots = [], [], [], [], [], []
+    n_inner = (1 << F.depth) - 1
+    per = 2 * n_inner + 1
+    for t in range(F.n_trees):
+        base = t * per
+        roots.append(base)
+        for h in range(per):
+            if h < n_inner:
+                feat.append(int(F.inner[t, h, 0]))
+                thr.append(float(F.inner[t, h, 1:2].view(np.float32)[0]))
+                left.append(base + 2 * h + 1)
+                right.append(base + 2 * h + 2)
+                val.append(0)
+            else:
+                feat.append(-1)
+                thr.append(0.0)
+                left.append(-1)
+                right.append(-1)
+                val.append(int(F.leaf[t, h - n_inner]))
+    return O.OracleForest(np.array(feat, np.int32), np.array(thr), np.array(left, np.int32),
+                          np.array(right, np.int32), np.array(val, np.int32),
+                          np.array(roots, np.int32))
+
+
+# ------------------------------------------------------- similarity ------
+def test_cosine_entries_and_column_similarities(cuda):
+    from dal import cosine_similarity as cs
+    from dal import similarity as sim
+
+    g = load_golden("similarity_96x500.npz")
+    S = _np(cs.cosine_entries(g["X"], device=cuda))
+    assert np.abs(S - g["entries"]).max() <= 2e-6
+    i, j, v = sim.column_similarities(g["X"], device=cuda)
+    assert np.array_equal(_np(i), g["ci"]) and np.array_equal(_np(j), g["cj"])
+    assert np.abs(_np(v) - g["cv"]).max() <= 2e-6
+
+
+# ------------------------------------------- config-2 scale properties ----
+def test_config2_scale_selection_bit_exact(cuda):
+    """100k x 64, T=10, k=100 (BASELINE config 2) against the oracle."""
+    from dal import density_weighting as dw
+    from dal import uncertainty_sampling as us
+    from dal.engine import PoolState
+    from dal.forest import Forest
+
+    X = O.synthetic_pool(100_000, 64, seed=0)
+    of = O.synthetic_forest(10, 4, 64, seed=1)
+    F = Forest.synthetic(10, 4, 64, seed=1)
+    E = np.arange(10)
+    unl = np.arange(10, 100_000)
+    st = PoolState(X, excluded=E, device=cuda)
+    sel = dw.select(st, unl, F, 100)
+    ref_sc, ref_idx, ref_ss = O.density_select(X, unl, of, 100, 1.0, E)
+    assert np.array_equal(_np(sel.indices), ref_idx)
+    assert np.array_equal(_np(sel.selected_scores), ref_ss)
+    got = _np(sel.scores)
+    ok = ~np.isnan(ref_sc)
+    assert np.allclose(got[ok], ref_sc[ok], rtol=DENSITY_RTOL, atol=0)
+    sel2 = dw.select(st, unl, F, 100)  # warm path (cached density): identical
+    assert np.array_equal(_np(sel2.indices), ref_idx)
+    u = us.select(st, unl, F, 1000)
+    _, ref_i, ref_s = O.uncertainty_select(X, unl, of, 1000)
+    assert np.array_equal(_np(u.indices), ref_i)
+    assert np.array_equal(_np(u.selected_scores), ref_s)

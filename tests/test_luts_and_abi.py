@@ -1,0 +1,63 @@
+"""Product LUTs vs oracle; the C ABI library exports every declared symbol
+and validates arguments on the host.  CPU only (no kernel launches)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+from dal import _lib, luts
+from oracle import dal_oracle as O
+
+
+@pytest.mark.parametrize("T", [1, 2, 3, 10, 50, 100, 2000])
+@pytest.mark.parametrize("strategy", luts.STRATEGIES)
+def test_product_luts_equal_oracle(T, strategy):
+    assert np.array_equal(luts.lut(strategy, T), O.lut(strategy, T), equal_nan=True)
+    assert np.array_equal(np.signbit(luts.lut(strategy, T)), np.signbit(O.lut(strategy, T)))
+
+
+def header_functions():
+    src = open(os.path.join(REPO, "include", "dal.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dal_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    names = header_functions()
+    assert len(names) >= 14
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(_lib.SIGNATURES), set(names) ^ set(_lib.SIGNATURES)
+
+
+def test_host_helpers():
+    lib = _lib.load()
+    assert lib.dal_abi_version() == 1
+    assert lib.dal_pad_rows(1) == 512 and lib.dal_pad_rows(100000) == 100352
+    assert [lib.dal_pad_features(d) for d in (1, 30, 33, 64, 65, 128, 129, 256, 500, 784)] == \
+        [32, 32, 64, 64, 128, 128, 256, 256, 512, 1024]
+    assert lib.dal_status_string(-2).decode().startswith("shape")
+    b = lib.dal_density_error_bound(100000)
+    assert 1.0 < b < 10.0  # ~3.1e-5 * N
+    assert lib.dal_topk_workspace_bytes(1 << 21, 1000) > 0
+
+
+def test_host_argument_validation_without_gpu():
+    lib = _lib.load()
+    # null pointers -> DAL_ERR_ARG before any HIP call
+    assert lib.dal_normalize_rows(None, 10, 4, 4, None, 512, 32, None, None, None, None) == -1
+    assert lib.dal_gram_rowsum(None, 256, None, 512, 64, 64, None, 0, None) == -1
+    assert lib.dal_topk(None, 10, 1, 0, None, 0, None, None, None) == -1
+    # bad shapes -> DAL_ERR_SHAPE
+    p = ctypes.c_void_p(256)
+    assert lib.dal_gram_rowsum(p, 100, p, 512, 64, 64, p, 0, None) == -2
+    assert lib.dal_gram_rowsum(p, 256, p, 500, 64, 64, p, 0, None) == -2
+    assert lib.dal_gram_rowsum(p, 256, p, 512, 48, 64, p, 0, None) == -2
+    assert lib.dal_topk(p, 10, 11, 0, p, 1 << 20, p, p, None) == -2
+    assert lib.dal_topk(p, 100000, 9000, 0, p, 1 << 30, p, p, None) == -5
+    assert lib.dal_forest_score(p, 10, 4, 4, p, p, 3, 17, p, None, 0.0, None, 1.0, 0, p, p, p,
+                                None, None) == -3
