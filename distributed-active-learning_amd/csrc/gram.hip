@@ -15,9 +15,11 @@
 //    from a 2 x 64 KiB LDS ring filled by global_load_lds_dwordx4 (one 1-KiB
 //    wave-instruction per 64 x 16 B), XOR-swizzled on the SOURCE address so the
 //    ds_read_b128 B-fragment reads are bank-conflict free.
-//  * Every stage (512 fp32 fmas per accumulator element) the fp32 accumulators
-//    are folded into int64 fixed point (2^-32); integer adds are associative,
-//    so per-row totals are bit-identical for any grid, unit split, or GPU count.
+//  * Every stage (512 fp32 fmas per accumulator element) each fp32 accumulator
+//    is folded as an integer multiple of 2^-32 (v_rndne_f32 of v*2^32) into an
+//    fp64 register; integer-valued fp64 adds below 2^53 are exact, and units
+//    end in int64 atomics, so per-row totals are bit-identical for any grid,
+//    unit split, column split or GPU count (fold groups = fixed column stages).
 //  * Persistent grid (one 256-thread block per CU): the (row-block, column-
 //    chunk) work units are dealt in equal contiguous ranges, so every CU gets
 //    the same number of MFMAs; a row block's A fragments are reloaded only when
@@ -26,6 +28,12 @@
 //  * Feature order inside an MFMA step is permuted (lane half h takes features
 //    8c+4h+m for step (c,m)) so each lane's B operand for 4 MFMAs is one
 //    16-byte LDS read; A uses the same permutation, so sum_d is unchanged.
+//    B reads run one step (8 MFMAs) ahead through a 2-deep register ring.
+//  * Measured alternatives (scripts/gram_ab.py, same-process A/B, MI355X):
+//    interleaving the fold with the next stage's MFMAs (dual accumulator sets)
+//    -3%; interleaving the next stage's DMA issue with the MFMAs -1%; a
+//    barrier-free variant streaming B per wave from L2 without LDS -6..-18%.
+
 #include "common.hpp"
 
 namespace dal {
@@ -47,6 +55,15 @@ struct GramCfg {
   static constexpr int NKC = KS / 8;      // 8-feature chunks (4 MFMA k-steps each)
   static constexpr int SWZ = (SLOTS < 16 ? SLOTS : 16) - 1;
 };
+
+// Exact fold of an fp32 stage partial: v * 2^32 rounded to an integer in
+// fp32 (|v| <= 16, so the product is exact and the rounded value is an
+// integer < 2^37), accumulated in fp64.  Integer-valued fp64 sums below 2^53
+// are exact, so the per-row totals do not depend on the order or grouping of
+// the folds (grid, unit split, column split, GPU count).
+__device__ __forceinline__ double fold_fixed(float v) {
+  return static_cast<double>(__builtin_rintf(v * 4294967296.0f));
+}
 
 template <int KS>
 __global__ __launch_bounds__(kGramThreads, 1) void gram_rowsum_kernel(
@@ -74,27 +91,24 @@ __global__ __launch_bounds__(kGramThreads, 1) void gram_rowsum_kernel(
   // global_load_lds makes it wait vmcnt(0) before the next ds_read, which
   // would serialise the prefetch with the MFMAs); we wait for it ourselves
   // at the top of the next iteration.  M0 is written and restored inside the
-  // statement (hipcc reserves M0).
-  auto issue = [&](int buf, int64_t stage) {
-    const int64_t col0 = stage * C::SC;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int base = (wave * 16 + q) * 64;
-      const int p = base + lane;
-      const int row = p / C::SLOTS;
-      const int slot = (p % C::SLOTS) ^ (row & C::SWZ);
-      const float* src = ucols + (col0 + row) * ld + ks_off + slot * 4;
-      const unsigned dst = __builtin_amdgcn_readfirstlane(
-          static_cast<unsigned>(reinterpret_cast<uintptr_t>((AS3 float4*)(lds + buf * kStageF4 + base))));
-      unsigned keep;
-      asm volatile(
-          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-          "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-          : "=&s"(keep)
-          : "v"(src), "s"(dst)
-          : "memory");
-    }
+  // statement (hipcc reserves M0).  Scalar stage base + 32-bit lane offset.
+  auto issue_piece = [&](int buf, const float* sbase, int q) {
+    const int base = (wave * 16 + q) * 64;
+    const int p = base + lane;
+    const int row = p / C::SLOTS;
+    const int slot = (p % C::SLOTS) ^ (row & C::SWZ);
+    const unsigned voff = static_cast<unsigned>((row * ld + slot * 4) * 4);
+    const unsigned dst = __builtin_amdgcn_readfirstlane(
+        static_cast<unsigned>(reinterpret_cast<uintptr_t>((AS3 float4*)(lds + buf * kStageF4 + base))));
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(dst), "s"(sbase)
+        : "memory");
   };
+  auto stage_base = [&](int64_t stage) { return ucols + stage * C::SC * ld + ks_off; };
 
   // ---- resident A fragments: rows rb*256 + wave*64 + rt*32 + li ----
   float4 a[2][C::NKC];
@@ -112,12 +126,86 @@ __global__ __launch_bounds__(kGramThreads, 1) void gram_rowsum_kernel(
   };
 
   f32x16 acc0 = {}, acc1 = {};
-  long long facc[2][16];
+  double facc[2][16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) facc[0][r] = facc[1][r] = 0;
+  for (int r = 0; r < 16; ++r) facc[0][r] = facc[1][r] = 0.0;
+  const f32x16 zero = {};
+
+  // One stage: 512 MFMAs per wave over the 64-KiB LDS stage `sbuf`; the next
+  // stage's DMA is in flight underneath.
+  auto stage = [&](int sbuf, bool pf, const float* pf_base) {
+    if (pf) {  // next stage's 16 DMA pieces up front (measured: beats interleaving)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) issue_piece(sbuf ^ 1, pf_base, q);
+    }
+    const float4* B = lds + sbuf * kStageF4;
+    constexpr int NSTEP = C::NCT * C::NKC;  // 8 MFMAs per step
+    auto bload = [&](int j) {
+      const int ct = j / C::NKC, c = j % C::NKC;
+      const int rowj = ct * 32 + li;
+      return B[rowj * C::SLOTS + ((2 * c + lh) ^ (rowj & C::SWZ))];
+    };
+    float4 ring[2];
+    ring[0] = bload(0);
+#pragma unroll
+    for (int j = 0; j < NSTEP; ++j) {
+      if (j + 1 < NSTEP) ring[(j + 1) & 1] = bload(j + 1);
+      const float4 b = ring[j & 1];
+      const int c = j % C::NKC;
+      const bool first = (j == 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][c].x, b.x, first ? zero : acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][c].x, b.x, first ? zero : acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][c].y, b.y, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][c].y, b.y, acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][c].z, b.z, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][c].z, b.z, acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][c].w, b.w, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][c].w, b.w, acc1, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      facc[0][r] += fold_fixed(acc0[r]);
+      facc[1][r] += fold_fixed(acc1[r]);
+    }
+  };
+
+  auto finish_unit = [&]() {
+    // exact (integer-valued) fp64 butterfly over the 32 column lanes of each
+    // half; row = (r&3) + 8(r>>2) + 4h
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        double v = facc[rt][r];
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        v += __shfl_xor(v, 16);
+        facc[rt][r] = v;
+      }
+    }
+    // lane li of half h publishes value (rt = li>>4, r = li&15): 64 rows, one atomic
+    double mine = 0.0;
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (rt * 16 + r == li) mine = facc[rt][r];
+        facc[rt][r] = 0.0;
+      }
+    }
+    const int r = li & 15;
+    const int64_t row = rb * kGramRows + wave * 64 + (li >> 4) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+    atomicAdd(acc_out + row, static_cast<unsigned long long>(static_cast<long long>(mine)));
+  };
 
   load_a(rb);
-  issue(0, s);
+  {
+    const float* b0 = stage_base(s);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) issue_piece(0, b0, q);
+  }
   int buf = 0;
 
   while (true) {
@@ -132,67 +220,8 @@ __global__ __launch_bounds__(kGramThreads, 1) void gram_rowsum_kernel(
 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA for `buf` landed
     __syncthreads();  // ... for every wave; everyone finished reading buf^1
-    if (has_next) issue(buf ^ 1, n_s);
-
-    // ---- 512 MFMAs per wave on stage `buf` ----
-    const float4* B = lds + buf * kStageF4;
-#pragma unroll
-    for (int ct = 0; ct < C::NCT; ++ct) {
-      const int rowj = ct * 32 + li;
-      const float4* brow = B + rowj * C::SLOTS;
-      const int sw = rowj & C::SWZ;
-#pragma unroll
-      for (int c = 0; c < C::NKC; ++c) {
-        const float4 b = brow[(2 * c + lh) ^ sw];
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][c].x, b.x, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][c].x, b.x, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][c].y, b.y, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][c].y, b.y, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][c].z, b.z, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][c].z, b.z, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][c].w, b.w, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][c].w, b.w, acc1, 0, 0, 0);
-      }
-    }
-
-    // ---- fold the stage into exact int64 fixed point ----
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      facc[0][r] += to_fixed(acc0[r]);
-      facc[1][r] += to_fixed(acc1[r]);
-      acc0[r] = 0.0f;
-      acc1[r] = 0.0f;
-    }
-
-    if (last_of_unit) {
-      // sum the 32 column lanes of each half (row = (r&3) + 8(r>>2) + 4h)
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          long long v = facc[rt][r];
-          v += __shfl_xor(v, 1);
-          v += __shfl_xor(v, 2);
-          v += __shfl_xor(v, 4);
-          v += __shfl_xor(v, 8);
-          v += __shfl_xor(v, 16);
-          facc[rt][r] = v;
-        }
-      }
-      // lane li of half h publishes value (rt = li>>4, r = li&15): 64 rows, one atomic
-      long long mine = 0;
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          if (rt * 16 + r == li) mine = facc[rt][r];
-          facc[rt][r] = 0;
-        }
-      }
-      const int r = li & 15;
-      const int64_t row = rb * kGramRows + wave * 64 + (li >> 4) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-      atomicAdd(acc_out + row, static_cast<unsigned long long>(mine));
-    }
+    stage(buf, has_next, stage_base(n_s));
+    if (last_of_unit) finish_unit();
 
     if (!has_next) break;
     if (last_of_unit) {
@@ -250,8 +279,8 @@ int launch_gram(const float* u_rows, int64_t n_rows_pad, const float* u_cols, in
   const int64_t n_units = n_row_blocks * n_chunks;
   const int64_t G = n_units < G0 ? n_units : G0;
   hipLaunchKernelGGL(gram_rowsum_kernel<KS>, dim3(static_cast<unsigned>(G)), dim3(kGramThreads), 0,
-                     stream, u_rows, u_cols, ld, ks_off, n_stages, static_cast<int>(cs), n_chunks,
-                     n_units, reinterpret_cast<unsigned long long*>(acc));
+                     stream, u_rows, u_cols, ld, ks_off, n_stages, static_cast<int>(cs), n_chunks, n_units,
+                     reinterpret_cast<unsigned long long*>(acc));
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
 }
@@ -279,19 +308,19 @@ extern "C" int dal_gram_rowsum(const float* u_rows, int64_t n_rows_pad, const fl
   if ((reinterpret_cast<uintptr_t>(u_rows) | reinterpret_cast<uintptr_t>(u_cols)) & 15)
     return DAL_ERR_SHAPE;
   hipStream_t st = as_stream(stream);
-  switch (d_pad) {
-    case 32: return launch_gram<32>(u_rows, n_rows_pad, u_cols, n_cols_pad, ld, 0, acc, grid_blocks, st);
-    case 64: return launch_gram<64>(u_rows, n_rows_pad, u_cols, n_cols_pad, ld, 0, acc, grid_blocks, st);
-    default:
-      // K-slices of 128 features: A stays register-resident (128 VGPRs/lane);
-      // the slices add into the same exact int64 accumulators.
-      for (int64_t off = 0; off < d_pad; off += 128) {
-        const int rc = launch_gram<128>(u_rows, n_rows_pad, u_cols, n_cols_pad, ld,
-                                        static_cast<int>(off), acc, grid_blocks, st);
-        if (rc != DAL_OK) return rc;
-      }
-      return DAL_OK;
+  const int ks = d_pad == 32 ? 32 : (d_pad == 64 ? 64 : 128);
+  for (int64_t off = 0; off < d_pad; off += ks) {
+    int rc;
+    if (ks == 32)
+      rc = launch_gram<32>(u_rows, n_rows_pad, u_cols, n_cols_pad, ld, 0, acc, grid_blocks, st);
+    else if (ks == 64)
+      rc = launch_gram<64>(u_rows, n_rows_pad, u_cols, n_cols_pad, ld, 0, acc, grid_blocks, st);
+    else  // K-slices of 128 features: A stays register-resident (128 floats/lane)
+      rc = launch_gram<128>(u_rows, n_rows_pad, u_cols, n_cols_pad, ld, static_cast<int>(off), acc,
+                            grid_blocks, st);
+    if (rc != DAL_OK) return rc;
   }
+  return DAL_OK;
 }
 
 extern "C" int dal_gram_entries(const float* u, int64_t n_pad, int64_t d_pad, int64_t ld, float* out,

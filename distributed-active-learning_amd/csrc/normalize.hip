@@ -74,30 +74,57 @@ __global__ __launch_bounds__(kNormThreads) void normalize_rows_kernel(
 }
 
 // partials[c][f] = sum_{r in chunk c, not excluded} x_rf / norm64[r]
-// (sequential over the chunk's rows).  Lanes run over features: coalesced.
-__global__ __launch_bounds__(64) void canon_colsum_partials_kernel(
+// (sequential over the chunk's rows).  The four waves divide 64 rows each
+// (lanes = features, coalesced loads) into an fp64 LDS tile; wave 0 then adds
+// the 256 rows in order -- the canonical sequence, but with the divisions and
+// loads in parallel.
+constexpr int kColFeat = 64;
+__global__ __launch_bounds__(256) void canon_colsum_partials_kernel(
     const float* __restrict__ x, int64_t n, int d, int64_t ldx, const double* __restrict__ norm64,
     const uint8_t* __restrict__ flags, double* __restrict__ partials) {
+  __shared__ double u[DAL_CANON_CHUNK][kColFeat];
+  __shared__ unsigned char live[DAL_CANON_CHUNK];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t c = blockIdx.x;
-  const int f = blockIdx.y * 64 + threadIdx.x;
-  if (f >= d) return;
-  double acc = 0.0;
+  const int f = blockIdx.y * kColFeat + lane;
   const int64_t r0 = c * DAL_CANON_CHUNK;
-  const int64_t r1 = min(n, r0 + DAL_CANON_CHUNK);
-  for (int64_t r = r0; r < r1; ++r) {
-    if (flags && (flags[r] & DAL_ROW_EXCLUDED)) continue;
-    acc = acc + static_cast<double>(x[r * ldx + f]) / norm64[r];
+  for (int i = 0; i < 64; ++i) {
+    const int rl = wave * 64 + i;
+    const int64_t r = r0 + rl;
+    double v = 0.0;
+    if (r < n && f < d) v = static_cast<double>(x[r * ldx + f]) / norm64[r];
+    u[rl][lane] = v;
   }
+  if (tid < DAL_CANON_CHUNK) {
+    const int64_t r = r0 + tid;
+    live[tid] = (r < n) && !(flags && (flags[r] & DAL_ROW_EXCLUDED));
+  }
+  __syncthreads();
+  if (wave != 0 || f >= d) return;
+  double acc = 0.0;
+#pragma unroll 16
+  for (int rl = 0; rl < DAL_CANON_CHUNK; ++rl)
+    if (live[rl]) acc = acc + u[rl][lane];
   partials[c * d + f] = acc;
 }
 
+// s[f] = sum_c partials[c][f], sequential over c; loads batched 32 deep.
 __global__ __launch_bounds__(64) void canon_colsum_reduce_kernel(const double* __restrict__ partials,
                                                                  int64_t n_chunks, int d,
                                                                  double* __restrict__ s) {
   const int f = blockIdx.x * 64 + threadIdx.x;
   if (f >= d) return;
+  constexpr int kBatch = 32;
   double acc = 0.0;
-  for (int64_t c = 0; c < n_chunks; ++c) acc = acc + partials[c * d + f];
+  int64_t c = 0;
+  for (; c + kBatch <= n_chunks; c += kBatch) {
+    double v[kBatch];
+#pragma unroll
+    for (int i = 0; i < kBatch; ++i) v[i] = partials[(c + i) * d + f];
+#pragma unroll
+    for (int i = 0; i < kBatch; ++i) acc = acc + v[i];
+  }
+  for (; c < n_chunks; ++c) acc = acc + partials[c * d + f];
   s[f] = acc;
 }
 
@@ -136,8 +163,8 @@ extern "C" int dal_canon_colsum_partials(const float* x, int64_t n, int64_t d, i
   if (n < 1 || d < 1 || ldx < d) return DAL_ERR_SHAPE;
   const int64_t chunks = ceil_div(n, DAL_CANON_CHUNK);
   hipLaunchKernelGGL(canon_colsum_partials_kernel,
-                     dim3(static_cast<unsigned>(chunks), static_cast<unsigned>(ceil_div(d, 64))),
-                     dim3(64), 0, as_stream(stream), x, n, static_cast<int>(d), ldx, norm64,
+                     dim3(static_cast<unsigned>(chunks), static_cast<unsigned>(ceil_div(d, kColFeat))),
+                     dim3(256), 0, as_stream(stream), x, n, static_cast<int>(d), ldx, norm64,
                      row_flags, partials);
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;

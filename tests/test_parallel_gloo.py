@@ -1,0 +1,148 @@
+"""Multi-process orchestration of dal.parallel over gloo (CPU, world_size 2
+and 3).  The two exchanges (all-gather of normalised shards + canonical column
+sum partials, all-gather of local top-k) and the deterministic merge are the
+product code; the per-shard arithmetic (HIP on the GPU) is replaced here by the
+oracle, so the test covers sharding, collectives and merge order on CPU."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from dal import parallel
+from dal.luts import lut
+from oracle import dal_oracle as O
+
+N, D, K = 2600, 12, 40
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class OracleShard(parallel.ShardedSelector):
+    """ShardedSelector with the per-shard steps computed by the oracle (CPU)."""
+
+    def __init__(self, X, n_total, rank, world, excluded, of):
+        self.n_total, self.rank, self.world = n_total, rank, world
+        self.lo, self.hi, self.shard = parallel.shard_range(n_total, world, rank)
+        self.x = X[self.lo:self.hi]
+        self.excluded = np.asarray(excluded)
+        self.of = of
+        self._density = None
+
+    def prep(self):
+        ex = O.exclusion_mask(self.n_total, self.excluded)[self.lo:self.hi]
+        u = torch.zeros((self.shard, D), dtype=torch.float64)
+        parts = torch.zeros((self.shard // 256, D), dtype=torch.float64)
+        if self.hi > self.lo:
+            U = O.l2_normalize(self.x)
+            U[ex] = 0.0
+            u[: U.shape[0]] = torch.from_numpy(U)
+            for c in range((U.shape[0] + 255) // 256):
+                acc = np.zeros(D)
+                for r in range(c * 256, min(U.shape[0], c * 256 + 256)):
+                    if not ex[r]:
+                        acc = acc + U[r]
+                parts[c] = torch.from_numpy(acc)
+        return u, parts
+
+    def local_select(self, u_full, parts_full, unl, forest, k, mode="dw", strategy="least_confidence",
+                     beta=1.0):
+        keys = torch.full((k,), parallel._as_i64(0xFFFFFFFFFFFFFFFF), dtype=torch.int64)
+        idx = torch.full((k,), -1, dtype=torch.int64)
+        sc = torch.full((k,), float("nan"), dtype=torch.float64)
+        unl = np.asarray(unl)
+        mine = unl[(unl >= self.lo) & (unl < self.hi)]
+        if mine.size == 0:
+            return parallel.LocalTopk(keys, idx, sc)
+        s = np.zeros(D)
+        for c in range(parts_full.shape[0]):
+            s = s + parts_full[c].numpy()
+        U = O.l2_normalize(self.x[mine - self.lo])
+        dd = np.zeros(mine.size)
+        for f in range(D):
+            dd = dd + U[:, f] * s[f]
+        dd[np.isin(mine, self.excluded)] = np.nan
+        v = O.votes(self.of, self.x[mine - self.lo])
+        score = lut("entropy", self.of.n_trees)[v] * dd
+        si, ss = O.select_topk(score, mine, k, ascending=False)
+        kk = si.size
+        # key: rank of the canonical order, encoded monotonically (test-only)
+        order_key = np.arange(kk) + 1
+        keys[:kk] = torch.from_numpy(_float_key(ss))
+        idx[:kk] = torch.from_numpy(si)
+        sc[:kk] = torch.from_numpy(ss)
+        return parallel.LocalTopk(keys, idx, sc)
+
+
+def _float_key(s):
+    """Test-side mirror of score_key (descending, NaN last, -0 == +0)."""
+    s = np.where(s == 0, 0.0, s)
+    b = s.view(np.uint64)
+    u = np.where(b >> np.uint64(63), ~b, b | np.uint64(1 << 63))
+    k = ~u
+    k = np.where(np.isnan(s), np.uint64(0xFFFFFFFFFFFFFFFE), k)
+    return k.view(np.int64)
+
+
+def _cpu_sort_positions(keys, pos, k):
+    u = keys.numpy().view(np.uint64)
+    order = np.lexsort((pos.numpy(), u))[:k]
+    return torch.from_numpy(order.astype(np.int64))
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        X = O.synthetic_pool(N, D, seed=4)
+        of = O.synthetic_forest(10, 4, D, seed=1)
+        E = np.arange(10)
+        unl = np.arange(10, N)
+        sel = OracleShard(X, N, rank, world, E, of)
+        idx, sc = parallel.select(sel, parallel.TorchComm(), unl, None, K, mode="dw",
+                                  sort_fn=_cpu_sort_positions)
+        q.put((rank, idx.numpy(), sc.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_sharded_density_select_matches_oracle(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    X = O.synthetic_pool(N, D, seed=4)
+    of = O.synthetic_forest(10, 4, D, seed=1)
+    _, ref_idx, ref_sc = O.density_select(X, np.arange(10, N), of, K, 1.0, np.arange(10))
+    for rank, idx, sc in res:
+        assert np.array_equal(idx, ref_idx), rank
+        assert np.array_equal(sc, ref_sc), rank
+
+
+def test_shard_ranges_cover_pool():
+    for n in (1, 511, 512, 100_000, 2_000_000, 284_807):
+        for w in (1, 2, 3, 4, 8):
+            rows = []
+            for r in range(w):
+                lo, hi, s = parallel.shard_range(n, w, r)
+                assert s % 512 == 0 and hi - lo <= s
+                rows.append((lo, hi))
+            assert rows[0][0] == 0 and rows[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(rows, rows[1:]))
