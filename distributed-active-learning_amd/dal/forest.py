@@ -139,6 +139,109 @@ class Forest:
                               np.concatenate(rgt), np.concatenate(val), np.array(roots))
 
     @classmethod
+    def from_mllib_debug_string(cls, text: str) -> "Forest":
+        """Parse MLlib's ``RandomForestModel.toDebugString()`` (Spark 2.1
+        ``Node.subtreeToString``): ``Tree k:`` headers, ``If (feature f <= t)`` /
+        ``Else (feature f > t)`` for continuous splits, ``Predict: c`` at leaves.
+        Categorical splits are rejected (the reference uses
+        ``categoricalFeaturesInfo={}``, uncertainty_sampling.py:73)."""
+        import re
+
+        lines = [ln.strip() for ln in text.splitlines() if ln.strip()]
+        trees, cur = [], None
+        for ln in lines:
+            if re.match(r"^Tree \d+:$", ln):
+                cur = []
+                trees.append(cur)
+            elif cur is not None and (ln.startswith("If ") or ln.startswith("Else ")
+                                      or ln.startswith("Predict:")):
+                cur.append(ln)
+        if not trees:
+            raise ValueError("no 'Tree k:' sections found in the debug string")
+        feat, thr, lft, rgt, val, roots = [], [], [], [], [], []
+        if_re = re.compile(r"^If \(feature (\d+) <= ([^)]+)\)$")
+        else_re = re.compile(r"^Else \(feature (\d+) > ([^)]+)\)$")
+
+        def new_node():
+            feat.append(-1)
+            thr.append(0.0)
+            lft.append(-1)
+            rgt.append(-1)
+            val.append(0)
+            return len(feat) - 1
+
+        for body in trees:
+            pos = 0
+
+            def parse():
+                nonlocal pos
+                ln = body[pos]
+                pos += 1
+                nd = new_node()
+                if ln.startswith("Predict:"):
+                    val[nd] = 1 if float(ln.split(":", 1)[1]) == 1.0 else 0
+                    return nd
+                m = if_re.match(ln)
+                if not m:
+                    raise ValueError(f"unsupported split line {ln!r} (only continuous splits)")
+                feat[nd], thr[nd] = int(m.group(1)), float(m.group(2))
+                lft[nd] = parse()
+                m2 = else_re.match(body[pos])
+                if not m2 or int(m2.group(1)) != feat[nd]:
+                    raise ValueError(f"malformed Else line {body[pos]!r}")
+                pos += 1
+                rgt[nd] = parse()
+                return nd
+
+            roots.append(parse())
+        return cls.from_nodes(feat, thr, lft, rgt, val, roots)
+
+    @classmethod
+    def from_mllib_saved(cls, path: str) -> "Forest":
+        """Read an MLlib ``RandomForestModel.save(sc, path)`` directory: Parquet
+        ``NodeData`` rows (treeId, nodeId, predict{predict, prob}, impurity,
+        isLeaf, split{feature, threshold, featureType, categories}, leftNodeId,
+        rightNodeId, infoGain) under ``path/data``; continuous splits only."""
+        import glob
+        import os
+
+        import pyarrow.parquet as pq
+
+        data = os.path.join(path, "data") if os.path.isdir(os.path.join(path, "data")) else path
+        files = sorted(glob.glob(os.path.join(data, "*.parquet")))
+        if not files:
+            raise ValueError(f"no parquet files under {data}")
+        rows = []
+        for f in files:
+            rows.extend(pq.read_table(f).to_pylist())
+        by_tree = {}
+        for r in rows:
+            by_tree.setdefault(int(r["treeId"]), {})[int(r["nodeId"])] = r
+        feat, thr, lft, rgt, val, roots = [], [], [], [], [], []
+        for t in sorted(by_tree):
+            nodes = by_tree[t]
+            gid = {nid: len(feat) + i for i, nid in enumerate(sorted(nodes))}
+            for nid in sorted(nodes):
+                r = nodes[nid]
+                if r["isLeaf"]:
+                    feat.append(-1)
+                    thr.append(0.0)
+                    lft.append(-1)
+                    rgt.append(-1)
+                    val.append(1 if float(r["predict"]["predict"]) == 1.0 else 0)
+                else:
+                    sp = r["split"]
+                    if int(sp.get("featureType", 0)) != 0:
+                        raise ValueError("categorical splits are not supported")
+                    feat.append(int(sp["feature"]))
+                    thr.append(float(sp["threshold"]))
+                    lft.append(gid[int(r["leftNodeId"])])
+                    rgt.append(gid[int(r["rightNodeId"])])
+                    val.append(0)
+            roots.append(gid[min(nodes)])  # MLlib root node id = 1 (smallest)
+        return cls.from_nodes(feat, thr, lft, rgt, val, roots)
+
+    @classmethod
     def synthetic(cls, n_trees: int, depth: int, n_features: int, seed: int = 1,
                   dist: str = "uniform") -> "Forest":
         """BASELINE.json synthetic forest: T complete depth-``depth`` trees,

@@ -84,3 +84,74 @@ def test_depth_limit():
     with pytest.raises(ValueError):
         Forest.from_nodes([f if f >= 0 else -1 for f in feat], np.zeros(2 * n + 1), left, right,
                           np.zeros(2 * n + 1), [0])
+
+
+def mllib_debug_string(of, kind="classifier"):
+    """Render oracle node arrays in Spark 2.1's toDebugString format (test helper)."""
+    out = [f"TreeEnsembleModel {kind} with {of.n_trees} trees", ""]
+
+    def rec(nd, ind):
+        pre = " " * ind
+        if of.feature[nd] < 0:
+            out.append(f"{pre}Predict: {float(of.value[nd])}")
+            return
+        f, t = int(of.feature[nd]), repr(float(of.threshold[nd]))
+        out.append(f"{pre}If (feature {f} <= {t})")
+        rec(of.left[nd], ind + 1)
+        out.append(f"{pre}Else (feature {f} > {t})")
+        rec(of.right[nd], ind + 1)
+
+    for t, root in enumerate(of.roots):
+        out.append(f"  Tree {t}:")
+        rec(int(root), 4)
+    return "\n".join(out) + "\n"
+
+
+@pytest.mark.parametrize("name,prefix", [("checkerboard4x4.npz", "it5_forest_"),
+                                         ("synthetic_1500x30_T100.npz", "forest_")])
+def test_from_mllib_debug_string(name, prefix):
+    g = load_golden(name)
+    of = golden_forest(g, prefix)
+    F = Forest.from_mllib_debug_string(mllib_debug_string(of))
+    assert np.array_equal(heap_votes(F, g["X"]), O.votes(of, g["X"]))
+
+
+def test_from_mllib_debug_string_rejects_categorical():
+    txt = "  Tree 0:\n    If (feature 0 in {1.0,2.0})\n     Predict: 0.0\n" \
+          "    Else (feature 0 not in {1.0,2.0})\n     Predict: 1.0\n"
+    with pytest.raises(ValueError):
+        Forest.from_mllib_debug_string(txt)
+
+
+def test_from_mllib_saved_parquet(tmp_path):
+    """MLlib RandomForestModel.save layout: NodeData rows in Parquet, node ids
+    1 (root), 2i, 2i+1 as MLlib assigns them."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+
+    g = load_golden("synthetic_512x64_T10.npz")
+    of = golden_forest(g)
+    rows = []
+    for t, root in enumerate(of.roots):
+        def rec(nd, nid):
+            leaf = of.feature[nd] < 0
+            rows.append({
+                "treeId": t, "nodeId": nid,
+                "predict": {"predict": float(of.value[nd]) if leaf else 0.0, "prob": 1.0},
+                "impurity": 0.0, "isLeaf": bool(leaf),
+                "split": None if leaf else {"feature": int(of.feature[nd]),
+                                            "threshold": float(of.threshold[nd]),
+                                            "featureType": 0, "categories": []},
+                "leftNodeId": None if leaf else 2 * nid,
+                "rightNodeId": None if leaf else 2 * nid + 1,
+                "infoGain": None if leaf else 0.1})
+            if not leaf:
+                rec(int(of.left[nd]), 2 * nid)
+                rec(int(of.right[nd]), 2 * nid + 1)
+        rec(int(root), 1)
+    (tmp_path / "data").mkdir()
+    half = len(rows) // 2
+    pq.write_table(pa.Table.from_pylist(rows[:half]), tmp_path / "data" / "part-0.parquet")
+    pq.write_table(pa.Table.from_pylist(rows[half:]), tmp_path / "data" / "part-1.parquet")
+    F = Forest.from_mllib_saved(str(tmp_path))
+    assert np.array_equal(heap_votes(F, g["X"]), O.votes(of, g["X"]))
