@@ -236,12 +236,16 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, ui
   return x - v + before;
 }
 
+// EXACT:    every key < K, then the first (k - #lt) keys == K in row order.
+// INTERVAL: candidates = lt rows plus eq rows whose global eq rank is < k,
+//           written as ONE stream in row order (position = #candidates before
+//           the row), so ties among candidates later resolve by row index.
 template <bool INTERVAL>
 __global__ __launch_bounds__(kRadixThreads) void compact_write_kernel(
     const uint64_t* __restrict__ keys, IntervalArgs I, int64_t n, int64_t idx_base, int64_t k,
     TopkHdr* __restrict__ h, const uint32_t* __restrict__ off, uint64_t* __restrict__ ckey,
     int64_t* __restrict__ cidx, int64_t cap, int32_t* __restrict__ status) {
-  __shared__ uint32_t sh[2][4];
+  __shared__ uint32_t sh[3][4];
   const int tid = threadIdx.x;
   const unsigned long long K = h->kstar;
   const uint64_t eq_take = INTERVAL ? static_cast<uint64_t>(k) : h->kfinal;
@@ -258,25 +262,47 @@ __global__ __launch_bounds__(kRadixThreads) void compact_write_kernel(
     ec += eq[j];
   }
   uint32_t tl, te;
-  uint32_t pl = block_excl_scan(lc, sh[0], tl) + off[2 * blockIdx.x];
-  uint32_t pe = block_excl_scan(ec, sh[1], te) + off[2 * blockIdx.x + 1];
+  const uint32_t lt_off = off[2 * blockIdx.x], eq_off = off[2 * blockIdx.x + 1];
+  uint32_t pl = block_excl_scan(lc, sh[0], tl) + lt_off;
+  uint32_t pe = block_excl_scan(ec, sh[1], te) + eq_off;
   bool ovf = false;
+  if (!INTERVAL) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t i = r0 + tid * 4 + j;
-    int64_t pos = -1;
-    if (lt[j]) pos = pl++;
-    else if (eq[j]) {
-      if (pe < eq_take) pos = static_cast<int64_t>(total_lt + pe);
-      ++pe;
-    }
-    if (pos >= 0) {
-      if (pos < cap) {
-        ckey[pos] = INTERVAL ? 0ull : keys[i];
-        cidx[pos] = idx_base + i;
-      } else {
-        ovf = true;
+    for (int j = 0; j < 4; ++j) {
+      const int64_t i = r0 + tid * 4 + j;
+      int64_t pos = -1;
+      if (lt[j]) pos = pl++;
+      else if (eq[j]) {
+        if (pe < eq_take) pos = static_cast<int64_t>(total_lt + pe);
+        ++pe;
       }
+      if (pos >= 0) {
+        if (pos < cap) {
+          ckey[pos] = keys[i];
+          cidx[pos] = idx_base + i;
+        } else {
+          ovf = true;
+        }
+      }
+    }
+  } else {
+    bool cand[4];
+    uint32_t cc = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      cand[j] = lt[j] || (eq[j] && pe < eq_take);
+      if (eq[j]) ++pe;
+      cc += cand[j];
+    }
+    uint32_t tc;
+    const uint64_t before = lt_off + (eq_off < eq_take ? eq_off : eq_take);
+    uint64_t pc = block_excl_scan(cc, sh[2], tc) + before;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!cand[j]) continue;
+      const int64_t pos = static_cast<int64_t>(pc++);
+      if (pos < cap) cidx[pos] = idx_base + r0 + tid * 4 + j;
+      else ovf = true;
     }
   }
   if (ovf) {
@@ -303,9 +329,13 @@ __global__ __launch_bounds__(256) void rerank_kernel(const TopkHdr* __restrict__
                                                      const uint8_t* __restrict__ flags, double beta,
                                                      uint64_t* __restrict__ ckey,
                                                      const int64_t* __restrict__ cidx,
-                                                     double* __restrict__ cpay) {
+                                                     double* __restrict__ cpay, int64_t cap) {
   const int64_t c = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (c >= h->cand_count) return;
+  if (c >= cap) return;
+  if (c >= h->cand_count) {
+    ckey[c] = DAL_KEY_NONE;
+    return;
+  }
   const int64_t i = cidx[c] - idx_base;
   const double nr = norm64[i];
   const float* xr = x + i * ldx;
@@ -319,6 +349,73 @@ __global__ __launch_bounds__(256) void rerank_kernel(const TopkHdr* __restrict__
   const double s = e * (beta == 1.0 ? acc : pow(acc, beta));
   cpay[c] = s;
   ckey[c] = score_key(s, DAL_DESCENDING);
+}
+
+// Canonical fp64 max-cosine of each candidate: one wave per candidate, lanes
+// over labeled rows; cos = sequential sum over features of u_if * u_lf with
+// u_i = x_i / ||x_i|| (sequential norm, no FMA) and u_l precomputed the same
+// way; max keeps the first (lowest l) maximum.
+__device__ __forceinline__ float bf16f(uint16_t b) { return __uint_as_float(static_cast<unsigned>(b) << 16); }
+
+__global__ __launch_bounds__(256) void rerank_maxcos_kernel(const TopkHdr* __restrict__ h, int64_t idx_base,
+                                                            const uint16_t* __restrict__ pool, int d,
+                                                            int64_t ld, const double* __restrict__ ulab,
+                                                            int64_t m, uint64_t* __restrict__ ckey,
+                                                            const int64_t* __restrict__ cidx,
+                                                            double* __restrict__ cpay, int64_t cap) {
+  const int lane = threadIdx.x & 63;
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (c >= cap) return;
+  if (c >= h->cand_count) {
+    if (lane == 0) ckey[c] = DAL_KEY_NONE;
+    return;
+  }
+  const int64_t i = cidx[c] - idx_base;
+  const uint16_t* xr = pool + i * ld;
+  double n2 = 0.0;
+  for (int f = 0; f < d; ++f) {
+    const double v = bf16f(xr[f]);
+    n2 = n2 + v * v;
+  }
+  const double nr = __builtin_sqrt(n2);
+  double best = -__builtin_inf();
+  int64_t arg = 0x7FFFFFFFFFFFFFFFll;
+  for (int64_t l = lane; l < m; l += 64) {
+    const double* ul = ulab + l * d;
+    double acc = 0.0;
+    for (int f = 0; f < d; ++f) acc = acc + (static_cast<double>(bf16f(xr[f])) / nr) * ul[f];
+    if (acc > best) {
+      best = acc;
+      arg = l;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ob = __shfl_xor(best, o);
+    const long long oa = __shfl_xor(static_cast<long long>(arg), o);
+    if (ob > best || (ob == best && oa < arg)) {
+      best = ob;
+      arg = oa;
+    }
+  }
+  if (lane == 0) {
+    cpay[c] = best;
+    ckey[c] = score_key(best, DAL_ASCENDING);
+  }
+}
+
+__global__ __launch_bounds__(256) void gather_selected_kernel(const int64_t* __restrict__ pos,
+                                                              const uint64_t* __restrict__ pkeys, int64_t k,
+                                                              const int64_t* __restrict__ cidx,
+                                                              const double* __restrict__ cpay,
+                                                              int64_t* __restrict__ out_idx,
+                                                              double* __restrict__ out_scores,
+                                                              uint64_t* __restrict__ out_keys) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (t >= k) return;
+  const int64_t p = pos[t];
+  out_idx[t] = cidx[p];
+  out_scores[t] = cpay[p];
+  if (out_keys) out_keys[t] = pkeys[t];
 }
 
 // ---------------------------------------------------------------- sort ----
@@ -445,39 +542,114 @@ extern "C" int dal_topk(const uint64_t* keys, int64_t n, int64_t k, int64_t idx_
   return DAL_OK;
 }
 
-extern "C" size_t dal_dw_select_workspace_bytes(int64_t n, int64_t k) {
-  (void)k;
-  return topk_layout(n, DAL_SORT_CAP_PAYLOAD).total;
+// Two-level workspace: level 1 selects candidates from n rows (capacity cap),
+// level 2 is an exact top-k over the cap canonical candidate keys.
+static size_t rerank_ws_bytes(int64_t n, int64_t k, int64_t cap) {
+  return topk_layout(n, cap).total + topk_layout(cap, k).total + round_up(k * 8, 256);
+}
+
+template <class Rerank>
+static int select_with_rerank(const uint64_t* keys_lo, const uint64_t* keys_hi, int64_t n, int64_t k,
+                              int64_t idx_base, int64_t cap, void* ws, size_t ws_bytes, Rerank rerank,
+                              int64_t* out_idx, double* out_scores, uint64_t* out_keys, int32_t* dev_status,
+                              hipStream_t st) {
+  if (n < 1 || k < 1 || k > n || cap < k) return DAL_ERR_SHAPE;
+  if (k > DAL_SORT_CAP) return DAL_ERR_CAPACITY;
+  const TopkLayout L1 = topk_layout(n, cap), L2 = topk_layout(cap, k);
+  if (ws_bytes < rerank_ws_bytes(n, k, cap) || (reinterpret_cast<uintptr_t>(ws) & 255)) return DAL_ERR_SHAPE;
+  char* base = static_cast<char*>(ws);
+  char* base2 = base + L1.total;
+  int64_t* pos = reinterpret_cast<int64_t*>(base2 + L2.total);
+  TopkHdr* h1 = reinterpret_cast<TopkHdr*>(base + L1.hdr);
+  TopkHdr* h2 = reinterpret_cast<TopkHdr*>(base2 + L2.hdr);
+  uint64_t* ckey = reinterpret_cast<uint64_t*>(base + L1.ckey);
+  int64_t* cidx = reinterpret_cast<int64_t*>(base + L1.cidx);
+  double* cpay = reinterpret_cast<double*>(base + L1.cpay);
+  int rc = run_radix(keys_lo, n, k, h1, st);
+  if (rc) return rc;
+  rc = run_compact<true>(keys_lo, IntervalArgs{keys_hi}, n, idx_base, k, ws, L1, dev_status, st);
+  if (rc) return rc;
+  rerank(h1, ckey, cidx, cpay, cap);  // canonical keys for every slot (NONE past the count)
+  rc = run_radix(ckey, cap, k, h2, st);
+  if (rc) return rc;
+  rc = run_compact<false>(ckey, IntervalArgs{nullptr}, cap, 0, k, base2, L2, nullptr, st);
+  if (rc) return rc;
+  uint64_t* pkeys = reinterpret_cast<uint64_t*>(base2 + L2.ckey);
+  hipLaunchKernelGGL(sort_kernel<false>, dim3(1), dim3(kSortThreads), 0, st, pkeys,
+                     reinterpret_cast<const int64_t*>(base2 + L2.cidx), nullptr, h2, int64_t{0}, k, pkeys,
+                     pos, nullptr);
+  hipLaunchKernelGGL(gather_selected_kernel, dim3(static_cast<unsigned>(ceil_div(k, 256))), dim3(256), 0, st,
+                     pos, pkeys, k, cidx, cpay, out_idx, out_scores, out_keys);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}
+
+extern "C" size_t dal_dw_select_workspace_bytes(int64_t n, int64_t k, int64_t cap) {
+  return rerank_ws_bytes(n, k, cap);
 }
 
 extern "C" int dal_dw_select(const uint64_t* keys_lo, const uint64_t* keys_hi, const int32_t* votes,
                              const uint8_t* row_flags, int64_t n, int64_t k, int64_t idx_base,
                              const double* lut, double beta, const float* x, int64_t d, int64_t ldx,
-                             const double* norm64, const double* colsum, void* ws, size_t ws_bytes,
-                             int64_t* out_idx, double* out_scores, uint64_t* out_keys,
+                             const double* norm64, const double* colsum, int64_t cap, void* ws,
+                             size_t ws_bytes, int64_t* out_idx, double* out_scores, uint64_t* out_keys,
                              int32_t* dev_status, dal_stream_t stream) {
   if (!keys_lo || !keys_hi || !votes || !lut || !x || !norm64 || !colsum || !ws || !out_idx ||
       !out_scores || !dev_status)
     return DAL_ERR_ARG;
-  if (n < 1 || k < 1 || k > n || d < 1 || ldx < d) return DAL_ERR_SHAPE;
-  if (k > DAL_SORT_CAP_PAYLOAD) return DAL_ERR_CAPACITY;
-  const TopkLayout L = topk_layout(n, DAL_SORT_CAP_PAYLOAD);
-  if (ws_bytes < L.total || (reinterpret_cast<uintptr_t>(ws) & 255)) return DAL_ERR_SHAPE;
+  if (d < 1 || ldx < d) return DAL_ERR_SHAPE;
   hipStream_t st = as_stream(stream);
-  char* base = static_cast<char*>(ws);
-  TopkHdr* h = reinterpret_cast<TopkHdr*>(base + L.hdr);
-  int rc = run_radix(keys_lo, n, k, h, st);
-  if (rc) return rc;
-  rc = run_compact<true>(keys_lo, IntervalArgs{keys_hi}, n, idx_base, k, ws, L, dev_status, st);
-  if (rc) return rc;
-  uint64_t* ckey = reinterpret_cast<uint64_t*>(base + L.ckey);
-  int64_t* cidx = reinterpret_cast<int64_t*>(base + L.cidx);
-  double* cpay = reinterpret_cast<double*>(base + L.cpay);
-  hipLaunchKernelGGL(rerank_kernel, dim3(DAL_SORT_CAP_PAYLOAD / 256), dim3(256), 0, st, h, idx_base, x,
-                     static_cast<int>(d), ldx, norm64, colsum, lut, votes, row_flags, beta, ckey, cidx,
-                     cpay);
-  hipLaunchKernelGGL(sort_kernel<true>, dim3(1), dim3(kSortThreads), 0, st, ckey, cidx, cpay, h,
-                     int64_t{0}, k, out_keys, out_idx, out_scores);
+  auto rerank = [&](TopkHdr* h, uint64_t* ckey, int64_t* cidx, double* cpay, int64_t cp) {
+    hipLaunchKernelGGL(rerank_kernel, dim3(static_cast<unsigned>(ceil_div(cp, 256))), dim3(256), 0, st, h,
+                       idx_base, x, static_cast<int>(d), ldx, norm64, colsum, lut, votes, row_flags, beta,
+                       ckey, cidx, cpay, cp);
+  };
+  return select_with_rerank(keys_lo, keys_hi, n, k, idx_base, cap, ws, ws_bytes, rerank, out_idx, out_scores,
+                            out_keys, dev_status, st);
+}
+
+extern "C" size_t dal_maxcos_select_workspace_bytes(int64_t n, int64_t k, int64_t cap) {
+  return rerank_ws_bytes(n, k, cap);
+}
+
+extern "C" int dal_maxcos_select(const uint64_t* keys_lo, const uint64_t* keys_hi, int64_t n, int64_t k,
+                                 int64_t idx_base, const uint16_t* pool, int64_t d, int64_t ld,
+                                 const double* ulab, int64_t m, int64_t cap, void* ws, size_t ws_bytes,
+                                 int64_t* out_idx, double* out_scores, uint64_t* out_keys,
+                                 int32_t* dev_status, dal_stream_t stream) {
+  if (!keys_lo || !keys_hi || !pool || !ulab || !ws || !out_idx || !out_scores || !dev_status)
+    return DAL_ERR_ARG;
+  if (d < 1 || ld < d || m < 1) return DAL_ERR_SHAPE;
+  hipStream_t st = as_stream(stream);
+  auto rerank = [&](TopkHdr* h, uint64_t* ckey, int64_t* cidx, double* cpay, int64_t cp) {
+    hipLaunchKernelGGL(rerank_maxcos_kernel, dim3(static_cast<unsigned>(ceil_div(cp, 4))), dim3(256), 0, st,
+                       h, idx_base, pool, static_cast<int>(d), ld, ulab, m, ckey, cidx, cpay, cp);
+  };
+  return select_with_rerank(keys_lo, keys_hi, n, k, idx_base, cap, ws, ws_bytes, rerank, out_idx, out_scores,
+                            out_keys, dev_status, st);
+}
+
+// Interval keys of fp32 values: lo/hi = keys of the pessimistic/optimistic
+// ends of [v - err, v + err] for ``order``; DAL_KEY_NONE for non-candidates.
+__global__ __launch_bounds__(256) void interval_keys_f32_kernel(const float* __restrict__ v, int64_t n,
+                                                                double err, const uint8_t* __restrict__ flags,
+                                                                int order, uint64_t* __restrict__ lo,
+                                                                uint64_t* __restrict__ hi) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n) return;
+  const bool cand = flags ? (flags[i] & DAL_ROW_CANDIDATE) : true;
+  const double s = static_cast<double>(v[i]);
+  lo[i] = cand ? score_key(pessimistic(s, err, order), order) : DAL_KEY_NONE;
+  hi[i] = cand ? score_key(optimistic(s, err, order), order) : DAL_KEY_NONE;
+}
+
+extern "C" int dal_interval_keys_f32(const float* values, int64_t n, double err, const uint8_t* row_flags,
+                                     int order, uint64_t* keys_lo, uint64_t* keys_hi, dal_stream_t stream) {
+  if (!values || !keys_lo || !keys_hi) return DAL_ERR_ARG;
+  if (order != DAL_ASCENDING && order != DAL_DESCENDING) return DAL_ERR_ARG;
+  if (n < 1 || !(err > 0.0)) return DAL_ERR_SHAPE;
+  hipLaunchKernelGGL(interval_keys_f32_kernel, dim3(static_cast<unsigned>(ceil_div(n, 256))), dim3(256), 0,
+                     as_stream(stream), values, n, err, row_flags, order, keys_lo, keys_hi);
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
 }

@@ -50,10 +50,24 @@ SIGNATURES = {
     "dal_topk_workspace_bytes": (c_size_t, [c_int64, c_int64]),
     "dal_topk": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_size_t, c_void_p, c_void_p,
                          c_void_p]),
-    "dal_dw_select_workspace_bytes": (c_size_t, [c_int64, c_int64]),
+    "dal_dw_select_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
     "dal_dw_select": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64,
                               c_void_p, c_double, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
-                              c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+                              c_int64, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
+                              c_void_p]),
+    "dal_maxcos_label_rows_granule": (c_int64, [c_int64]),
+    "dal_maxcos_error_bound": (c_double, [c_int64]),
+    "dal_inv_norms_bf16": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p, c_void_p,
+                                   c_void_p]),
+    "dal_canon_unit_rows_bf16": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p]),
+    "dal_max_cosine": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
+                               c_void_p, c_void_p]),
+    "dal_interval_keys_f32": (c_int, [c_void_p, c_int64, c_double, c_void_p, c_int, c_void_p,
+                                      c_void_p, c_void_p]),
+    "dal_maxcos_select_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
+    "dal_maxcos_select": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64,
+                                  c_int64, c_void_p, c_int64, c_int64, c_void_p, c_size_t, c_void_p,
+                                  c_void_p, c_void_p, c_void_p, c_void_p]),
     "dal_sort_pairs": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
                                c_void_p, c_void_p]),
     "dal_gram_entries": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p]),

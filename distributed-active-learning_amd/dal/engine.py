@@ -278,24 +278,41 @@ def density_error(state: PoolState) -> float:
     return float(_lib.load().dal_density_error_bound(max(n_cols, 1)))
 
 
+def candidate_cap(n: int, k: int) -> int:
+    """Initial re-rank candidate capacity (k plus a band; grown on overflow)."""
+    return int(min(n, max(4 * k, k + 8192)))
+
+
+def workspace(nbytes: int, device):
+    """A 256-byte aligned device workspace: (tensor, aligned pointer)."""
+    torch = _torch()
+    ws = torch.empty(int(nbytes) + 256, dtype=torch.uint8, device=device)
+    return ws, (_ptr(ws) + 255) // 256 * 256
+
+
 def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k: int,
                     beta: float, colsum):
-    """dal_dw_select on this shard: exact canonical top-k of the shard."""
+    """dal_dw_select on this shard: exact canonical top-k of the shard.  The
+    candidate capacity grows (and the step re-runs) on DAL_FLAG_CAND_OVERFLOW."""
     torch = _torch()
     lib = _lib.load()
     n = state.n
     _, norm64 = state.normalized()
-    wsb = int(lib.dal_dw_select_workspace_bytes(n, k))
-    ws = torch.empty(wsb + 256, dtype=torch.uint8, device=state.device)
-    wsp = (_ptr(ws) + 255) // 256 * 256
-    out_idx = torch.empty(k, dtype=torch.int64, device=state.device)
-    out_scores = torch.empty(k, dtype=torch.float64, device=state.device)
-    out_keys = torch.empty(k, dtype=torch.int64, device=state.device)
-    call("dal_dw_select", _ptr(keys_lo), _ptr(keys_hi), _ptr(votes), _ptr(flags), n, k,
-         state.row_base, _ptr(lut_dev), float(beta), _ptr(state.x), state.d, state.d, _ptr(norm64),
-         _ptr(colsum), wsp, wsb, _ptr(out_idx), _ptr(out_scores), _ptr(out_keys),
-         _ptr(state.status), _stream(state.device))
-    return out_idx, out_scores, out_keys
+    cap = candidate_cap(n, k)
+    while True:
+        wsb = int(lib.dal_dw_select_workspace_bytes(n, k, cap))
+        ws, wsp = workspace(wsb, state.device)
+        out_idx = torch.empty(k, dtype=torch.int64, device=state.device)
+        out_scores = torch.empty(k, dtype=torch.float64, device=state.device)
+        out_keys = torch.empty(k, dtype=torch.int64, device=state.device)
+        call("dal_dw_select", _ptr(keys_lo), _ptr(keys_hi), _ptr(votes), _ptr(flags), n, k,
+             state.row_base, _ptr(lut_dev), float(beta), _ptr(state.x), state.d, state.d,
+             _ptr(norm64), _ptr(colsum), cap, wsp, wsb, _ptr(out_idx), _ptr(out_scores),
+             _ptr(out_keys), _ptr(state.status), _stream(state.device))
+        if cap >= n or not (int(state.status.item()) & DAL_FLAG_CAND_OVERFLOW):
+            return out_idx, out_scores, out_keys
+        state.status.bitwise_and_(~DAL_FLAG_CAND_OVERFLOW)
+        cap = min(n, cap * 4)
 
 
 def sort_pairs(keys, idx, k: int, payload=None):

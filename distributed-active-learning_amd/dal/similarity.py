@@ -20,4 +20,129 @@ def column_similarities(pool, device=None):
     return ij[0], ij[1], S[ij[0], ij[1]]
 
 
-__all__ = ["column_similarities"]
+
+
+
+# ---------------------------------------------------------------------------
+# Batch-mode diversity (BASELINE config 5): max-cosine to a labeled set
+# ---------------------------------------------------------------------------
+def _bf16_pool(pool, device):
+    import numpy as np
+    import torch
+
+    from .engine import _require_cuda
+
+    dev = _require_cuda(device)
+    if isinstance(pool, torch.Tensor):
+        x = pool.to(device=dev)
+    else:
+        x = torch.from_numpy(np.ascontiguousarray(np.asarray(pool, dtype=np.float32))).to(dev)
+    if x.dtype != torch.bfloat16:
+        x = x.to(torch.float32).to(torch.bfloat16)  # round to nearest even
+    if x.dim() != 2 or x.shape[1] not in (64, 128, 256):
+        raise ValueError("bf16 max-cosine needs a [rows, 64|128|256] pool")
+    return x.contiguous(), dev
+
+
+class LabeledSet:
+    """The labeled rows as the kernel's B operand: bf16 [m_pad, d] (padding
+    rows carry 1/||x|| = NaN, ignored by the max), fp32 1/||x||, and the
+    canonical fp64 unit rows for the exact re-rank."""
+
+    def __init__(self, rows_bf16, device):
+        import torch
+
+        from . import _lib
+        from .engine import _ptr, _stream
+
+        lib = _lib.load()
+        m, d = int(rows_bf16.shape[0]), int(rows_bf16.shape[1])
+        g = int(lib.dal_maxcos_label_rows_granule(d))
+        m_pad = -(-m // g) * g
+        self.m, self.d, self.m_pad = m, d, m_pad
+        self.rows = torch.zeros((m_pad, d), dtype=torch.bfloat16, device=device)
+        self.rows[:m] = rows_bf16
+        self.status = torch.zeros(1, dtype=torch.int32, device=device)
+        self.inv = torch.empty(m_pad, dtype=torch.float32, device=device)
+        _lib.call("dal_inv_norms_bf16", _ptr(self.rows), m, m_pad, d, d, _ptr(self.inv),
+                  _ptr(self.status), _stream(device))
+        self.unit64 = torch.empty((m, d), dtype=torch.float64, device=device)
+        _lib.call("dal_canon_unit_rows_bf16", _ptr(self.rows), m, d, d, _ptr(self.unit64),
+                  _stream(device))
+
+
+def max_cosine(pool, labeled_idx, device=None):
+    """m_i = max_{l in labeled} cos(x_i, x_l) for every pool row (fp32 [N]),
+    bf16 MFMA with fp32 accumulation (|error| <= dal_maxcos_error_bound(d))."""
+    import torch
+
+    from . import _lib
+    from .engine import _as_index, _ptr, _stream
+
+    x, dev = _bf16_pool(pool, device)
+    n, d = int(x.shape[0]), int(x.shape[1])
+    lab = LabeledSet(x[_as_index(labeled_idx, dev)], dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    inv = torch.empty(n, dtype=torch.float32, device=dev)
+    _lib.call("dal_inv_norms_bf16", _ptr(x), n, n, d, d, _ptr(inv), _ptr(status), _stream(dev))
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+    _lib.call("dal_max_cosine", _ptr(x), n, d, _ptr(lab.rows), lab.m_pad, _ptr(lab.inv), _ptr(inv),
+              _ptr(out), _stream(dev))
+    if int(status.item()) | int(lab.status.item()):
+        raise ValueError("zero-norm row: cosine undefined")
+    return out
+
+
+def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, row_base: int = 0):
+    """Select the k candidate rows least similar to the labeled set (smallest
+    max-cosine, ties -> lower index), exact against the canonical fp64
+    max-cosine.  Returns Selection(scores = fp32 max-cos of the candidates,
+    indices [k], selected_scores = canonical fp64 max-cos)."""
+    import numpy as np
+    import torch
+
+    from . import _lib
+    from ._lib import DAL_ASCENDING, DAL_FLAG_CAND_OVERFLOW, DAL_ROW_CANDIDATE
+    from .engine import Selection, _as_index, _ptr, _stream, candidate_cap, workspace
+
+    lib = _lib.load()
+    x, dev = _bf16_pool(pool, device)
+    n, d = int(x.shape[0]), int(x.shape[1])
+    lab_idx = _as_index(labeled_idx, dev)
+    lab = LabeledSet(x[lab_idx], dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    inv = torch.empty(n, dtype=torch.float32, device=dev)
+    _lib.call("dal_inv_norms_bf16", _ptr(x), n, n, d, d, _ptr(inv), _ptr(status), _stream(dev))
+    mx = torch.empty(n, dtype=torch.float32, device=dev)
+    _lib.call("dal_max_cosine", _ptr(x), n, d, _ptr(lab.rows), lab.m_pad, _ptr(lab.inv), _ptr(inv),
+              _ptr(mx), _stream(dev))
+    flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+    cand = (torch.arange(n, device=dev) if candidates is None
+            else _as_index(candidates, dev) - row_base)
+    cand = cand[(cand >= 0) & (cand < n)]
+    flags[cand] = DAL_ROW_CANDIDATE
+    kk = min(int(k), int(cand.shape[0]))
+    lo = torch.empty(n, dtype=torch.int64, device=dev)
+    hi = torch.empty(n, dtype=torch.int64, device=dev)
+    _lib.call("dal_interval_keys_f32", _ptr(mx), n, float(lib.dal_maxcos_error_bound(d)), _ptr(flags),
+              DAL_ASCENDING, _ptr(lo), _ptr(hi), _stream(dev))
+    cap = candidate_cap(n, kk)
+    while True:
+        wsb = int(lib.dal_maxcos_select_workspace_bytes(n, kk, cap))
+        ws, wsp = workspace(wsb, dev)
+        out_idx = torch.empty(kk, dtype=torch.int64, device=dev)
+        out_sc = torch.empty(kk, dtype=torch.float64, device=dev)
+        _lib.call("dal_maxcos_select", _ptr(lo), _ptr(hi), n, kk, int(row_base), _ptr(x), d, d,
+                  _ptr(lab.unit64), lab.m, cap, wsp, wsb, _ptr(out_idx), _ptr(out_sc), 0,
+                  _ptr(status), _stream(dev))
+        st = int(status.item()) | int(lab.status.item())
+        if st & 1:
+            raise ValueError("zero-norm row: cosine undefined")
+        if cap >= n or not (st & DAL_FLAG_CAND_OVERFLOW):
+            break
+        status.zero_()
+        cap = min(n, cap * 4)
+    return Selection(scores=mx[cand], indices=out_idx, selected_scores=out_sc)
+
+
+__all__ = ["column_similarities", "max_cosine", "diversity_select", "LabeledSet"]

@@ -145,22 +145,52 @@ int dal_topk(const uint64_t* keys, int64_t n, int64_t k, int64_t idx_base, void*
 
 /* ---- density-weighted selection with exact fp64 re-rank ----------------
  * Given the interval keys written by dal_forest_score (density mode,
- * DAL_DESCENDING): K = k-th smallest pessimistic key; every row whose
- * optimistic key is < K (or == K with a non-point interval) plus the first k
- * point-interval rows == K (row order) are candidates -- a superset of the
- * canonical top-k.  Each candidate's canonical fp64 score
- *   lut[v] * (sum_f (x_if / norm64[i]) * colsum[f])^beta   (sequential, no FMA)
- * is recomputed and the k best by (score desc, NaN last, index asc) are
- * returned: bit-exact with the fp64 oracle.  out_scores are the canonical
- * fp64 scores, out_keys (nullable) their keys.  More than
- * DAL_SORT_CAP_PAYLOAD candidates sets DAL_FLAG_CAND_OVERFLOW. */
-size_t dal_dw_select_workspace_bytes(int64_t n, int64_t k);
+ * DAL_DESCENDING): K = k-th smallest pessimistic key; candidates = every row
+ * whose optimistic key is < K (or == K with a non-point interval) plus the
+ * first k point-interval rows == K, in row order -- a superset of the
+ * canonical top-k (at most ``cap`` of them).  Each candidate's canonical fp64
+ * score  lut[v] * (sum_f (x_if / norm64[i]) * colsum[f])^beta  (sequential,
+ * no FMA) is recomputed and an exact top-k over the candidates returns the k
+ * best by (score desc, NaN last, index asc): bit-exact with the fp64 oracle.
+ * out_scores are canonical fp64 scores, out_keys (nullable) their keys.  More
+ * than ``cap`` candidates sets DAL_FLAG_CAND_OVERFLOW (retry with a larger cap). */
+size_t dal_dw_select_workspace_bytes(int64_t n, int64_t k, int64_t cap);
 int dal_dw_select(const uint64_t* keys_lo, const uint64_t* keys_hi, const int32_t* votes,
                   const uint8_t* row_flags, int64_t n, int64_t k, int64_t idx_base,
                   const double* lut, double beta, const float* x, int64_t d, int64_t ldx,
-                  const double* norm64, const double* colsum, void* ws, size_t ws_bytes,
-                  int64_t* out_idx, double* out_scores, uint64_t* out_keys,
+                  const double* norm64, const double* colsum, int64_t cap, void* ws,
+                  size_t ws_bytes, int64_t* out_idx, double* out_scores, uint64_t* out_keys,
                   int32_t* dev_status, dal_stream_t stream);
+
+/* ---- (a12, config 5) max-cosine to a labeled set -----------------------
+ * Restates similarity.py:26-43 (columnSimilarities of the normalised pool) as
+ * m_i = max_{l in L} cos(x_i, x_l) over a bf16 pool (row-major [n][d],
+ * d in {64,128,256}) and a bf16 labeled table [m_pad][d] whose rows beyond the
+ * real m carry inv_lab = NaN (ignored).  bf16 MFMA (v_mfma_f32_32x32x16_bf16),
+ * fp32 accumulate, row-max epilogue; the n x m matrix is never stored.
+ * m_pad % dal_maxcos_label_rows_granule(d) == 0, m_pad <= 4096.
+ * |m_gpu - m_canonical| <= dal_maxcos_error_bound(d) (Cauchy-Schwarz). */
+int64_t dal_maxcos_label_rows_granule(int64_t d);
+double dal_maxcos_error_bound(int64_t d);
+int dal_inv_norms_bf16(const uint16_t* x, int64_t n, int64_t n_pad, int64_t d, int64_t ld,
+                       float* inv, int32_t* dev_status, dal_stream_t stream);
+int dal_canon_unit_rows_bf16(const uint16_t* x, int64_t n, int64_t d, int64_t ld, double* u,
+                             dal_stream_t stream);
+int dal_max_cosine(const uint16_t* pool, int64_t n, int64_t d, const uint16_t* lab, int64_t m_pad,
+                   const float* inv_lab, const float* inv_pool, float* out_max, dal_stream_t stream);
+/* Interval keys [v - err, v + err] of fp32 values (pessimistic -> keys_lo). */
+int dal_interval_keys_f32(const float* values, int64_t n, double err, const uint8_t* row_flags,
+                          int order, uint64_t* keys_lo, uint64_t* keys_hi, dal_stream_t stream);
+/* Diversity selection: the k rows with the smallest canonical fp64 max-cosine
+ * (ties -> lower index), from interval keys of dal_max_cosine's output;
+ * ulab = canonical fp64 unit rows of the m labeled rows
+ * (dal_canon_unit_rows_bf16).  Same candidate/re-rank contract as dal_dw_select. */
+size_t dal_maxcos_select_workspace_bytes(int64_t n, int64_t k, int64_t cap);
+int dal_maxcos_select(const uint64_t* keys_lo, const uint64_t* keys_hi, int64_t n, int64_t k,
+                      int64_t idx_base, const uint16_t* pool, int64_t d, int64_t ld,
+                      const double* ulab, int64_t m, int64_t cap, void* ws, size_t ws_bytes,
+                      int64_t* out_idx, double* out_scores, uint64_t* out_keys,
+                      int32_t* dev_status, dal_stream_t stream);
 
 /* ---- multi-GPU merge ----------------------------------------------------
  * Sort n (key, idx) pairs (e.g. the all-gathered per-GPU top-k lists) by

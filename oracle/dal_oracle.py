@@ -312,6 +312,42 @@ def column_similarities(X: np.ndarray):
     return i, j, S[i, j]
 
 
+def bf16_round(X: np.ndarray) -> np.ndarray:
+    """Round fp32 values to bf16 (nearest-even), returned as fp32."""
+    b = np.ascontiguousarray(X, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    r = ((b + 0x7FFF + ((b >> 16) & 1)) >> 16) << 16
+    return r.astype(np.uint32).view(np.float32)
+
+
+def max_cosine_canonical(X: np.ndarray, labeled_idx, block: int = 4096):
+    """Canonical fp64 max-cosine (the definition the diversity selection is
+    bit-exact to): u = x / ||x|| (sequential norm), cos_il = sum_d u_id * u_ld
+    sequential over d (mul, then add), m_i = max over l, first l on ties."""
+    U = l2_normalize(X)
+    UL = U[np.asarray(labeled_idx, dtype=np.int64)]
+    n = U.shape[0]
+    m = np.empty(n)
+    arg = np.empty(n, dtype=np.int64)
+    for b0 in range(0, n, block):
+        Ub = U[b0:b0 + block]
+        S = np.zeros((Ub.shape[0], UL.shape[0]))
+        for d in range(U.shape[1]):
+            S = S + Ub[:, d, None] * UL[None, :, d]
+        a = np.argmax(S, axis=1)
+        arg[b0:b0 + block] = a
+        m[b0:b0 + block] = S[np.arange(S.shape[0]), a]
+    return m, arg
+
+
+def diversity_select_canonical(X, labeled_idx, k: int, candidates=None):
+    """similarity.py restated for batch-mode diversity (BASELINE config 5):
+    the k candidates with the smallest canonical max-cosine to the labeled set
+    (ascending, ties -> lower index)."""
+    m, _ = max_cosine_canonical(X, labeled_idx)
+    idx = np.arange(X.shape[0]) if candidates is None else np.asarray(candidates, dtype=np.int64)
+    return select_topk(m[idx], idx, k, ascending=True)
+
+
 def max_cosine(X: np.ndarray, labeled_idx):
     """Config 5 restatement of similarity.py: m_i = max_{l in L} cos(x_i, x_l)
     and its arg-max (first l on ties).  fp64 on the given inputs."""

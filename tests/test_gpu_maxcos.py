@@ -1,0 +1,65 @@
+"""Max-cosine / diversity selection (similarity.py restated for BASELINE
+config 5): bf16 MFMA kernel vs the canonical fp64 oracle."""
+import numpy as np
+import pytest
+
+from oracle import dal_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+@pytest.mark.parametrize("n,d,m", [(3000, 128, 300), (2500, 64, 1024), (1800, 256, 130), (700, 128, 1)])
+def test_max_cosine_within_bound(cuda, n, d, m):
+    from dal import _lib
+    from dal import similarity as sim
+
+    X = O.bf16_round(O.synthetic_pool(n, d, seed=n + d))
+    L = np.arange(0, n, max(1, n // m))[:m]
+    got = _np(sim.max_cosine(X, L, device=cuda))
+    ref, _ = O.max_cosine_canonical(X, L)
+    bound = _lib.load().dal_maxcos_error_bound(d)
+    assert np.abs(got - ref).max() <= bound
+    assert np.allclose(got[L], 1.0, atol=bound)  # labeled rows match themselves
+
+
+def test_max_cosine_signed_data(cuda):
+    from dal import _lib
+    from dal import similarity as sim
+
+    X = O.bf16_round(O.synthetic_pool(2000, 128, seed=5, dist="normal"))
+    L = np.arange(100, 612)
+    got = _np(sim.max_cosine(X, L, device=cuda))
+    ref, _ = O.max_cosine_canonical(X, L)
+    assert np.abs(got - ref).max() <= _lib.load().dal_maxcos_error_bound(128)
+
+
+@pytest.mark.parametrize("n,d,m,k", [(4000, 128, 256, 50), (3000, 64, 700, 200), (2000, 256, 64, 1)])
+def test_diversity_select_bit_exact(cuda, n, d, m, k):
+    from dal import similarity as sim
+
+    X = O.bf16_round(O.synthetic_pool(n, d, seed=7 * n))
+    X[500:520] = X[600]  # duplicate rows -> exact ties, resolved by index
+    L = np.arange(m)
+    cand = np.arange(m, n)
+    sel = sim.diversity_select(X, L, k, candidates=cand, device=cuda)
+    ref_idx, ref_sc = O.diversity_select_canonical(X, L, k, candidates=cand)
+    assert np.array_equal(_np(sel.indices), ref_idx)
+    assert np.array_equal(_np(sel.selected_scores), ref_sc)
+
+
+def test_diversity_select_scale(cuda):
+    """30k x 128 pool, 1,024 labeled rows, k = 1000 (config-5 shape, scaled)."""
+    from dal import similarity as sim
+
+    n, d, m, k = 30000, 128, 1024, 1000
+    X = O.bf16_round(O.synthetic_pool(n, d, seed=0))
+    L = np.arange(m)
+    cand = np.arange(m, n)
+    sel = sim.diversity_select(X, L, k, candidates=cand, device=cuda)
+    ref_idx, ref_sc = O.diversity_select_canonical(X, L, k, candidates=cand)
+    assert np.array_equal(_np(sel.indices), ref_idx)
+    assert np.array_equal(_np(sel.selected_scores), ref_sc)
