@@ -83,28 +83,33 @@ __global__ __launch_bounds__(256) void canon_colsum_partials_kernel(
     const float* __restrict__ x, int64_t n, int d, int64_t ldx, const double* __restrict__ norm64,
     const uint8_t* __restrict__ flags, double* __restrict__ partials) {
   __shared__ double u[DAL_CANON_CHUNK][kColFeat];
-  __shared__ unsigned char live[DAL_CANON_CHUNK];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t c = blockIdx.x;
   const int f = blockIdx.y * kColFeat + lane;
-  const int64_t r0 = c * DAL_CANON_CHUNK;
-  for (int i = 0; i < 64; ++i) {
-    const int rl = wave * 64 + i;
-    const int64_t r = r0 + rl;
-    double v = 0.0;
-    if (r < n && f < d) v = static_cast<double>(x[r * ldx + f]) / norm64[r];
-    u[rl][lane] = v;
-  }
-  if (tid < DAL_CANON_CHUNK) {
-    const int64_t r = r0 + tid;
-    live[tid] = (r < n) && !(flags && (flags[r] & DAL_ROW_EXCLUDED));
+  const int64_t r0 = c * DAL_CANON_CHUNK + wave * 64;
+  // Excluded / padding rows contribute +0.0: the running sum starts at +0.0
+  // and can never become -0.0, so adding +0.0 is bit-identical to skipping.
+#pragma unroll
+  for (int i0 = 0; i0 < 64; i0 += 16) {
+    float xv[16];
+    double nv[16];
+    bool lv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int64_t r = r0 + i0 + i;
+      lv[i] = r < n && f < d && !(flags && (flags[r] & DAL_ROW_EXCLUDED));
+      xv[i] = lv[i] ? x[r * ldx + f] : 0.0f;
+      nv[i] = lv[i] ? norm64[r] : 1.0;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      u[wave * 64 + i0 + i][lane] = lv[i] ? static_cast<double>(xv[i]) / nv[i] : 0.0;
   }
   __syncthreads();
   if (wave != 0 || f >= d) return;
   double acc = 0.0;
-#pragma unroll 16
-  for (int rl = 0; rl < DAL_CANON_CHUNK; ++rl)
-    if (live[rl]) acc = acc + u[rl][lane];
+#pragma unroll 32
+  for (int rl = 0; rl < DAL_CANON_CHUNK; ++rl) acc = acc + u[rl][lane];
   partials[c * d + f] = acc;
 }
 
@@ -128,10 +133,30 @@ __global__ __launch_bounds__(64) void canon_colsum_reduce_kernel(const double* _
   s[f] = acc;
 }
 
+__global__ __launch_bounds__(256) void mark_rows_kernel(const int64_t* __restrict__ idx, int64_t count,
+                                                        int64_t row_base, int64_t n, unsigned bits,
+                                                        uint8_t* __restrict__ flags) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (t >= count) return;
+  const int64_t r = idx[t] - row_base;
+  if (r >= 0 && r < n) flags[r] |= static_cast<uint8_t>(bits);  // duplicates write the same value
+}
+
 }  // namespace
 }  // namespace dal
 
 using namespace dal;
+
+extern "C" int dal_mark_rows(const int64_t* idx, int64_t count, int64_t row_base, int64_t n, int bits,
+                             uint8_t* flags, dal_stream_t stream) {
+  if ((!idx && count) || !flags) return DAL_ERR_ARG;
+  if (count < 0 || n < 0) return DAL_ERR_SHAPE;
+  if (count == 0) return DAL_OK;
+  hipLaunchKernelGGL(mark_rows_kernel, dim3(static_cast<unsigned>(ceil_div(count, 256))), dim3(256), 0,
+                     as_stream(stream), idx, count, row_base, n, static_cast<unsigned>(bits), flags);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}
 
 extern "C" int64_t dal_pad_rows(int64_t n) { return round_up(n < 1 ? 1 : n, DAL_ROW_GRANULE); }
 

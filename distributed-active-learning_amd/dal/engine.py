@@ -202,14 +202,21 @@ class PoolState:
 
     # ------------------------------------------------------------ helpers
     def row_flags(self, unlabeled_idx):
-        """EXCLUDED bits | CANDIDATE for the (global) unlabeled indices of this shard."""
-        torch = _torch()
+        """EXCLUDED bits | CANDIDATE for the (global) unlabeled indices of this
+        shard, built on the device (no host round trip).  Returns (flags,
+        unlabeled indices, count of unlabeled indices)."""
         unl = _as_index(unlabeled_idx, self.device)
-        loc = unl - self.row_base
-        loc = loc[(loc >= 0) & (loc < self.n)]
         flags = self.flags.clone()
-        flags[loc] |= DAL_ROW_CANDIDATE
-        return flags, unl, loc
+        call("dal_mark_rows", _ptr(unl), int(unl.shape[0]), self.row_base, self.n,
+             DAL_ROW_CANDIDATE, _ptr(flags), _stream(self.device))
+        return flags, unl, int(unl.shape[0])
+
+    def local_positions(self, unl):
+        """Rows of this shard for global indices ``unl`` (single GPU: all of them)."""
+        loc = unl - self.row_base
+        if self.row_base == 0 and self.n == self.n_total:
+            return loc
+        return loc[(loc >= 0) & (loc < self.n)]
 
     def check_status(self):
         st = int(self.status.item())
@@ -235,9 +242,16 @@ def as_pool_state(pool, excluded=None, device=None) -> PoolState:
     return PoolState(pool, excluded=excluded, device=device)
 
 
+_LUT_CACHE = {}
+
+
 def device_lut(strategy: str, n_trees: int, device):
+    """fp64 LUT on the device, uploaded once per (strategy, T, device)."""
     torch = _torch()
-    return torch.from_numpy(make_lut(strategy, n_trees)).to(device)
+    key = (strategy, int(n_trees), str(device))
+    if key not in _LUT_CACHE:
+        _LUT_CACHE[key] = torch.from_numpy(make_lut(strategy, n_trees)).to(device)
+    return _LUT_CACHE[key]
 
 
 def forest_score(state: PoolState, forest: Forest, lut_dev, flags, order: int, density=None,
@@ -309,7 +323,9 @@ def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k
              state.row_base, _ptr(lut_dev), float(beta), _ptr(state.x), state.d, state.d,
              _ptr(norm64), _ptr(colsum), cap, wsp, wsb, _ptr(out_idx), _ptr(out_scores),
              _ptr(out_keys), _ptr(state.status), _stream(state.device))
-        if cap >= n or not (int(state.status.item()) & DAL_FLAG_CAND_OVERFLOW):
+        # the step's one host sync: status word (zero-norm rows, candidate overflow)
+        st = int(state.status.item())
+        if cap >= n or not (st & DAL_FLAG_CAND_OVERFLOW):
             return out_idx, out_scores, out_keys
         state.status.bitwise_and_(~DAL_FLAG_CAND_OVERFLOW)
         cap = min(n, cap * 4)
@@ -332,11 +348,11 @@ def sort_pairs(keys, idx, k: int, payload=None):
 def uncertainty_step(state: PoolState, unlabeled_idx, forest: Forest, k: int,
                      strategy: str = "least_confidence") -> Selection:
     """One iteration of uncertainty_sampling.py:85-112 on the GPU."""
-    flags, unl, loc = state.row_flags(unlabeled_idx)
-    n_cand = int(loc.shape[0])
+    flags, unl, n_cand = state.row_flags(unlabeled_idx)
     if n_cand == 0:
         raise ValueError("unlabeled set is empty (the reference loop breaks here)")
     kk = min(int(k), n_cand)
+    loc = state.local_positions(unl)
     order = DAL_ASCENDING if ASCENDING[strategy] else DAL_DESCENDING
     lut_dev = device_lut(strategy, forest.n_trees, state.device)
     votes, scores, keys, _ = forest_score(state, forest, lut_dev, flags, order)
@@ -350,11 +366,11 @@ def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: 
                  density_fixed=None) -> Selection:
     """One iteration of density_weighting.py:133-176 on the GPU:
     score = ent[v] * d^beta, descending; exact canonical selection."""
-    flags, unl, loc = state.row_flags(unlabeled_idx)
-    n_cand = int(loc.shape[0])
+    flags, unl, n_cand = state.row_flags(unlabeled_idx)
     if n_cand == 0:
         raise ValueError("unlabeled set is empty (the reference loop breaks here)")
     kk = min(int(k), n_cand)
+    loc = state.local_positions(unl)
     dens = state.density_fixed() if density_fixed is None else density_fixed
     lut_dev = device_lut("entropy", forest.n_trees, state.device)
     votes, scores, keys_lo, keys_hi = forest_score(
@@ -362,5 +378,5 @@ def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: 
         density_err=density_error(state), beta=beta, want_hi=True)
     idx, sel_scores, _ = dw_select_local(state, flags, votes, keys_lo, keys_hi, lut_dev, kk, beta,
                                          state.colsum())
-    state.check_status()
+    state.check_status()  # already synchronised by dw_select_local
     return Selection(scores=scores[loc], indices=idx, selected_scores=sel_scores, votes=votes[loc])

@@ -121,8 +121,8 @@ class ShardedSelector:
         scores = torch.full((k,), float("nan"), dtype=torch.float64, device=st.device)
         if st.n == 0:
             return LocalTopk(keys, idx, scores)
-        flags, _, loc = st.row_flags(unlabeled_idx)
-        n_cand = int(loc.shape[0])
+        flags, unl, _ = st.row_flags(unlabeled_idx)
+        n_cand = int(((unl >= st.row_base) & (unl < st.row_base + st.n)).sum().item())
         if n_cand == 0:
             return LocalTopk(keys, idx, scores)
         kk = min(k, n_cand)

@@ -89,6 +89,12 @@ int dal_normalize_rows(const float* x, int64_t n, int64_t d, int64_t ldx,
                        const uint8_t* row_flags, int64_t n_pad, int64_t d_pad,
                        float* u, double* norm64, int32_t* dev_status, dal_stream_t stream);
 
+/* OR ``bits`` into flags[idx[t] - row_base] for every index of this shard
+ * (0 <= idx - row_base < n): builds DAL_ROW_CANDIDATE from an unlabeled index
+ * list without a host round trip. */
+int dal_mark_rows(const int64_t* idx, int64_t count, int64_t row_base, int64_t n, int bits,
+                  uint8_t* flags, dal_stream_t stream);
+
 /* ---- canonical fp64 column sum (re-rank side of the density) -----------
  * partials[c][f] = sum over rows c*256 .. c*256+255 (< n, not EXCLUDED) of
  * x_rf / norm64[r], sequential in row order; rows of a shard start at a
