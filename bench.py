@@ -41,6 +41,9 @@ CONFIGS = {
     "4": dict(workload="config4: synthetic U[0,1) 2,000,000 x 256 fp32 pool, T=10 depth-4 forest, "
                        "entropy x density, k=100, E={0..9}",
               n=2_000_000, d=256, trees=10, depth=4, k=100, dist="uniform"),
+    "5": dict(workload="config5: batch-mode diversity selection (similarity.py max-cosine to the labeled "
+                       "set), U[0,1)->bf16 8,000,000 x 128 pool, L = first 1,024 rows, k=1000, fp32 accumulate",
+              n=8_000_000, d=128, k=1000, m=1024, dist="uniform", mode="div"),
 }
 N_EXCLUDED = 10
 GEN_CHUNK = 65536
@@ -110,6 +113,93 @@ def cpu_baseline(x_host: np.ndarray, cfg, of, budget_s: float = 12.0):
                       f"{dt:.1f} s on the host"}
 
 
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
+
+
+def bench_diversity(args, cfg, world, rank, dev, dist, backend):
+    """Config 5: one step = max-cosine of every pool row to the labeled set
+    (bf16 MFMA, fp32 accumulate) + exact top-k of the least similar rows."""
+    import torch
+
+    from dal import parallel
+    from dal.similarity import diversity_select
+
+    n, d, k, m = cfg["n"], cfg["d"], cfg["k"], cfg["m"]
+    lo, hi, _ = parallel.shard_range(n, world, rank)
+    x = make_pool_rows(lo, hi, d, cfg["dist"], dev).to(torch.bfloat16)
+    lab = make_pool_rows(0, m, d, cfg["dist"], dev).to(torch.bfloat16)
+    cand = torch.arange(max(lo, m), hi, device=dev, dtype=torch.int64)
+    comm = parallel.TorchComm() if world > 1 else None
+
+    def step():
+        if world > 1:
+            return parallel.diversity_select_sharded(x, lo, lab, k, comm, candidates=cand, device=dev)
+        s = diversity_select(x, None, k, candidates=cand, device=dev, labeled_rows=lab)
+        return s.indices, s.selected_scores
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    # kernel-only timing of the max-cosine launch on this rank
+    from dal import _lib
+    from dal.engine import _ptr, _stream
+    from dal.similarity import LabeledSet
+
+    L = LabeledSet(lab, dev)
+    inv = torch.empty(hi - lo, dtype=torch.float32, device=dev)
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.call("dal_inv_norms_bf16", _ptr(x), hi - lo, hi - lo, d, d, _ptr(inv), _ptr(st), _stream(dev))
+    out = torch.empty(hi - lo, dtype=torch.float32, device=dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ms = []
+    for _ in range(3):
+        e0.record()
+        _lib.call("dal_max_cosine", _ptr(x), hi - lo, d, _ptr(L.rows), L.m_pad, _ptr(L.inv), _ptr(inv),
+                  _ptr(out), _stream(dev))
+        e1.record()
+        torch.cuda.synchronize()
+        ms.append(e0.elapsed_time(e1))
+    kms = sorted(ms)[1]
+    tdev = dev if backend == "nccl" else "cpu"
+    t = torch.tensor([elapsed, kms], dtype=torch.float64, device=tdev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t[0])
+    flops = 2.0 * (hi - lo) * m * d
+    achieved = flops / (kms * 1e-3) / 1e12
+    out_line = {
+        "metric": "pool rows scored/sec (diversity: max-cosine to labeled set + exact top-k)",
+        "value": (n - m) * args.steps / elapsed, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed * 1000 / args.steps, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (GPU-generated, fixed seeds per 65,536-row chunk)",
+        "config": {"workload": cfg["workload"], "pool_rows": n, "features": d, "labeled": m, "k": k,
+                   "parallelism": f"row-shard dp{world}" if world > 1 else "single GPU"},
+        "roofline": {"bound": "mfma", "kernel": "dal_max_cosine (v_mfma_f32_32x32x16_bf16)",
+                     "achieved": achieved, "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / BF16_MFMA_PEAK_TFLOPS, "traffic": None, "launch_ms": kms,
+                     "algorithmic_flops_per_launch": flops,
+                     "pool_bytes_per_launch": (hi - lo) * d * 2,
+                     "hbm_frac_of_8TBs": (hi - lo) * d * 2 / (kms * 1e-3) / 8e12},
+        "cpu_baseline": None,
+    }
+    if rank == 0:
+        print(json.dumps(out_line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -128,15 +218,24 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    dev = torch.device("cuda", local_rank)
+    # DAL_BENCH_BACKEND=gloo rehearses the multi-process path with several
+    # ranks on one GPU (all-gathers staged through the host); default: RCCL.
+    backend = os.environ.get("DAL_BENCH_BACKEND", "nccl")
+    n_dev = torch.cuda.device_count()
+    dev = torch.device("cuda", local_rank % max(n_dev, 1))
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from dal import engine, parallel
     from dal.forest import Forest
 
     cfg = CONFIGS[args.config]
+    if cfg.get("mode") == "div":
+        return bench_diversity(args, cfg, world, rank, dev, dist, backend)
     n, d, k = cfg["n"], cfg["d"], cfg["k"]
     lo, hi, shard = parallel.shard_range(n, world, rank)
     x = make_pool_rows(lo, hi, d, cfg["dist"], dev)
@@ -181,7 +280,8 @@ def main():
     events = state.gram_events
     state.gram_events = None
     gram_ms = sum(a.elapsed_time(b) for a, b in events) / max(len(events), 1)
-    t = torch.tensor([elapsed, gram_ms], dtype=torch.float64, device=dev)
+    tdev = dev if backend == "nccl" else "cpu"
+    t = torch.tensor([elapsed, gram_ms], dtype=torch.float64, device=tdev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, gram_ms_max = float(t[0]), float(t[1])
@@ -203,7 +303,7 @@ def main():
                 engine.density_step(state, unl, forest, k)
         torch.cuda.synchronize()
         barrier()
-        tw = torch.tensor([time.perf_counter() - tw], dtype=torch.float64, device=dev)
+        tw = torch.tensor([time.perf_counter() - tw], dtype=torch.float64, device=tdev)
         if world > 1:
             dist.all_reduce(tw, op=dist.ReduceOp.MAX)
         warm_ms = float(tw[0]) * 1000 / args.warm_steps

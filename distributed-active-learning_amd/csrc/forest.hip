@@ -39,7 +39,8 @@ struct ForestArgs {
   int n_trees;
   int depth;
   const double* lut;
-  const long long* density;
+  const void* density;
+  int dkind;  // 0 none (uncertainty), 1 int64 fixed point (GEMM), 2 exact fp64
   double derr;
   const uint8_t* flags;
   double beta;
@@ -131,11 +132,12 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
   const uint8_t fl = A.flags ? A.flags[row] : DAL_ROW_CANDIDATE;
   const double e = A.lut[v];
   double s, err = 0.0;
-  if (A.density) {
-    double d = from_fixed(A.density[row]);
+  if (A.dkind) {
+    double d = A.dkind == 1 ? from_fixed(static_cast<const long long*>(A.density)[row])
+                            : static_cast<const double*>(A.density)[row];
     if (fl & DAL_ROW_EXCLUDED) d = __builtin_nan("");
     s = e * density_pow(d, A.beta);
-    if (e == e && e != 0.0 && d == d) {
+    if (A.dkind == 1 && e == e && e != 0.0 && d == d) {
       err = fabs(e) * density_pow_err(d, A.derr, A.beta);
       // keep the interval ends distinct from s after rounding
       err = fmax(err, fabs(s) * 4.5e-16);
@@ -157,16 +159,18 @@ using namespace dal;
 
 extern "C" int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
                                 const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
-                                const int64_t* density, double density_err, const uint8_t* row_flags,
+                                const void* density, int density_kind, double density_err,
+                                const uint8_t* row_flags,
                                 double beta, int order, int32_t* votes, double* scores, uint64_t* keys,
                                 uint64_t* keys_hi, dal_stream_t stream) {
   if (!x || !inner || !leaf || !lut || !votes || !scores || !keys) return DAL_ERR_ARG;
   if (order != DAL_ASCENDING && order != DAL_DESCENDING) return DAL_ERR_ARG;
+  if (density_kind < 0 || density_kind > 2 || (density_kind && !density)) return DAL_ERR_ARG;
   if (n < 0 || d < 1 || ldx < d || n_trees < 1) return DAL_ERR_SHAPE;
   if (depth < 1 || depth > DAL_MAX_TREE_DEPTH) return DAL_ERR_UNSUPPORTED;
   if (n == 0) return DAL_OK;
   ForestArgs A{x, n, static_cast<int>(d), ldx, reinterpret_cast<const int2*>(inner), leaf, n_trees,
-               depth, lut, reinterpret_cast<const long long*>(density), density_err, row_flags, beta,
+               depth, lut, density_kind ? density : nullptr, density_kind, density_err, row_flags, beta,
                order, votes, scores, keys, keys_hi};
   // rows per block: stage up to 64 KiB of pool rows in LDS
   int R = 256;

@@ -113,6 +113,40 @@ __global__ __launch_bounds__(256) void canon_colsum_partials_kernel(
   partials[c * d + f] = acc;
 }
 
+// Separable canonical density for every row: d_i = sum_f (x_if / norm64[i]) *
+// s_f, sequential over f (the same fp64 operation order as the re-rank and the
+// oracle, so every bit matches); NaN for excluded rows.  64 rows per block:
+// tiles of 64 features staged through LDS with coalesced loads, lane r owns row r.
+__global__ __launch_bounds__(256) void density_separable_kernel(
+    const float* __restrict__ x, int64_t n, int d, int64_t ldx, const double* __restrict__ norm64,
+    const double* __restrict__ colsum, const uint8_t* __restrict__ flags, double* __restrict__ dens) {
+  __shared__ float tile[64][65];
+  __shared__ double sv[64];
+  const int tid = threadIdx.x;
+  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * 64;
+  const int64_t row = row0 + tid;
+  const double nr = (tid < 64 && row < n) ? norm64[row] : 1.0;
+  double acc = 0.0;
+  for (int c0 = 0; c0 < d; c0 += 64) {
+    for (int e = tid; e < 64 * 64; e += 256) {
+      const int r = e / 64, c = e % 64;
+      const int64_t rr = row0 + r;
+      tile[r][c] = (rr < n && c0 + c < d) ? x[rr * ldx + c0 + c] : 0.0f;
+    }
+    if (tid < 64) sv[tid] = c0 + tid < d ? colsum[c0 + tid] : 0.0;
+    __syncthreads();
+    if (tid < 64) {
+      const int cmax = min(64, d - c0);
+      for (int c = 0; c < cmax; ++c) acc = acc + (static_cast<double>(tile[tid][c]) / nr) * sv[c];
+    }
+    __syncthreads();
+  }
+  if (tid < 64 && row < n) {
+    if (flags && (flags[row] & DAL_ROW_EXCLUDED)) acc = __builtin_nan("");
+    dens[row] = acc;
+  }
+}
+
 // s[f] = sum_c partials[c][f], sequential over c; loads batched 32 deep.
 __global__ __launch_bounds__(64) void canon_colsum_reduce_kernel(const double* __restrict__ partials,
                                                                  int64_t n_chunks, int d,
@@ -191,6 +225,17 @@ extern "C" int dal_canon_colsum_partials(const float* x, int64_t n, int64_t d, i
                      dim3(static_cast<unsigned>(chunks), static_cast<unsigned>(ceil_div(d, kColFeat))),
                      dim3(256), 0, as_stream(stream), x, n, static_cast<int>(d), ldx, norm64,
                      row_flags, partials);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}
+
+extern "C" int dal_density_separable(const float* x, int64_t n, int64_t d, int64_t ldx, const double* norm64,
+                                     const double* colsum, const uint8_t* row_flags, double* density,
+                                     dal_stream_t stream) {
+  if (!x || !norm64 || !colsum || !density) return DAL_ERR_ARG;
+  if (n < 1 || d < 1 || ldx < d) return DAL_ERR_SHAPE;
+  hipLaunchKernelGGL(density_separable_kernel, dim3(static_cast<unsigned>(ceil_div(n, 64))), dim3(256), 0,
+                     as_stream(stream), x, n, static_cast<int>(d), ldx, norm64, colsum, row_flags, density);
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
 }

@@ -19,6 +19,9 @@ DAL_FLAG_ZERO_NORM = 1
 DAL_FLAG_CAND_OVERFLOW = 2
 DAL_ROW_CANDIDATE = 1
 DAL_ROW_EXCLUDED = 2
+DAL_DENSITY_NONE = 0
+DAL_DENSITY_FIXED = 1
+DAL_DENSITY_EXACT = 2
 DAL_ASCENDING = 0
 DAL_DESCENDING = 1
 DAL_KEY_NAN = 0xFFFFFFFFFFFFFFFE
@@ -46,8 +49,10 @@ SIGNATURES = {
     "dal_gram_rowsum": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int64, c_void_p,
                                 c_int, c_void_p]),
     "dal_forest_score": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32,
-                                 c_int32, c_void_p, c_void_p, c_double, c_void_p, c_double, c_int,
-                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+                                 c_int32, c_void_p, c_void_p, c_int, c_double, c_void_p, c_double,
+                                 c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "dal_density_separable": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p]),
     "dal_topk_workspace_bytes": (c_size_t, [c_int64, c_int64]),
     "dal_topk": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_size_t, c_void_p, c_void_p,
                          c_void_p]),

@@ -20,28 +20,33 @@ from .engine import PoolState, Selection, as_pool_state, density_step
 from .forest import Forest
 
 
-def information_density(pool, excluded_idx=None, device=None):
+def information_density(pool, excluded_idx=None, device=None, mode: str = "gram"):
     """d_i = sum_{j not in E} cos(x_i, x_j) for every row (fp64, NaN for i in E).
 
     excluded_idx  E; the reference uses L0 = range(window_size).
+    mode          "gram": fused fp32-MFMA Gram row-sum (the reference's N^2
+                  algorithm, within dal_density_error_bound of canonical);
+                  "separable": exact O(N*D) identity, canonical fp64 bits.
     """
     state = as_pool_state(pool, excluded=excluded_idx, device=device)
-    d = state.density()
+    d = state.density(mode)
     state.check_status()
     return d
 
 
 def select(pool, unlabeled_idx, forest: Forest, k: int, beta: float = 1.0, excluded_idx=None,
-           density=None, device=None) -> Selection:
+           density=None, device=None, mode: str = "gram") -> Selection:
     """Score every unlabeled row by entropy x density^beta and select the top k.
 
     excluded_idx  rows dropped from the density (default: none; the reference
                   passes its initial labeled window, range(window_size))
     density       optional int64 fixed-point density from a previous call
                   (PoolState.density_fixed()); by default the pool's cached one
+    mode          "gram" (default, the reference's algorithm on MFMA) or
+                  "separable" (exact O(N*D) identity; same selection)
     """
     state = as_pool_state(pool, excluded=excluded_idx, device=device)
-    return density_step(state, unlabeled_idx, forest, k, beta=beta, density_fixed=density)
+    return density_step(state, unlabeled_idx, forest, k, beta=beta, density_fixed=density, mode=mode)
 
 
 __all__ = ["information_density", "select", "PoolState", "Selection"]

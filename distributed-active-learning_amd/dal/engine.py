@@ -16,8 +16,9 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from ._lib import (DAL_ASCENDING, DAL_DESCENDING, DAL_FLAG_CAND_OVERFLOW, DAL_FLAG_ZERO_NORM,
-                   DAL_ROW_CANDIDATE, DAL_ROW_EXCLUDED, DAL_CANON_CHUNK, DAL_FIXED_SCALE, call)
+from ._lib import (DAL_ASCENDING, DAL_CANON_CHUNK, DAL_DENSITY_EXACT, DAL_DENSITY_FIXED,
+                   DAL_DENSITY_NONE, DAL_DESCENDING, DAL_FIXED_SCALE, DAL_FLAG_CAND_OVERFLOW,
+                   DAL_FLAG_ZERO_NORM, DAL_ROW_CANDIDATE, DAL_ROW_EXCLUDED, call)
 from .forest import Forest
 from .luts import ASCENDING, lut as make_lut
 
@@ -105,11 +106,13 @@ class PoolState:
         self._density = None
         self._colsum_partials = None
         self._colsum = None
+        self._density_exact = None
         self.gram_events = None  # list -> (start, end) HIP events around each Gram call
 
     def clear_caches(self):
         """Drop normalised rows, density and column sums (forces a cold step)."""
         self._u = self._norm64 = self._density = self._colsum = self._colsum_partials = None
+        self._density_exact = None
 
     # ------------------------------------------------------------- caches
     def set_excluded(self, excluded):
@@ -125,6 +128,7 @@ class PoolState:
         if local.size:
             self.flags[torch.from_numpy(local).to(self.device)] = DAL_ROW_EXCLUDED
         self._u = self._norm64 = self._density = self._colsum = self._colsum_partials = None
+        self._density_exact = None
 
     def n_excluded_global(self) -> int:
         return int(self.excluded.size)
@@ -193,9 +197,31 @@ class PoolState:
     def set_density_fixed(self, acc):
         self._density = acc
 
-    def density(self):
-        """fp64 density d[n] (NaN for rows in E): Gram row-sum / 2^32."""
+    def density_exact(self, colsum=None):
+        """Separable canonical fp64 density of this shard's rows (NaN for E):
+        the exact identity sum_j <u_i,u_j> = <u_i, s>, O(N*D), bit-identical to
+        the oracle.  ``colsum`` = the global s (multi-GPU); default this pool's."""
+        if self._density_exact is None or colsum is not None:
+            torch = _torch()
+            _, norm64 = self.normalized()
+            s = self.colsum() if colsum is None else colsum
+            d = torch.empty(self.n, dtype=torch.float64, device=self.device)
+            call("dal_density_separable", _ptr(self.x), self.n, self.d, self.d, _ptr(norm64), _ptr(s),
+                 _ptr(self.flags), _ptr(d), _stream(self.device))
+            if colsum is not None:
+                return d
+            self._density_exact = d
+        return self._density_exact
+
+    def density(self, mode: str = "gram"):
+        """fp64 density d[n] (NaN for rows in E): the MFMA Gram row-sum / 2^32
+        (mode "gram", the reference's algorithm) or the exact separable form
+        (mode "separable")."""
         torch = _torch()
+        if mode == "separable":
+            return self.density_exact()
+        if mode != "gram":
+            raise ValueError(f"density mode must be 'gram' or 'separable', not {mode!r}")
         d = self.density_fixed()[: self.n].to(torch.float64) * (1.0 / DAL_FIXED_SCALE)
         ex = (self.flags & DAL_ROW_EXCLUDED).bool()
         return torch.where(ex, torch.full_like(d, float("nan")), d)
@@ -255,7 +281,8 @@ def device_lut(strategy: str, n_trees: int, device):
 
 
 def forest_score(state: PoolState, forest: Forest, lut_dev, flags, order: int, density=None,
-                 density_err: float = 0.0, beta: float = 1.0, want_hi: bool = False):
+                 density_err: float = 0.0, beta: float = 1.0, want_hi: bool = False,
+                 density_kind=None):
     """Launch dal_forest_score over the shard; returns (votes, scores, keys, keys_hi)."""
     torch = _torch()
     inner, leaf = forest.device(state.device)
@@ -264,8 +291,14 @@ def forest_score(state: PoolState, forest: Forest, lut_dev, flags, order: int, d
     scores = torch.empty(n, dtype=torch.float64, device=state.device)
     keys = torch.empty(n, dtype=torch.int64, device=state.device)
     keys_hi = torch.empty(n, dtype=torch.int64, device=state.device) if want_hi else None
+    if density is None:
+        kind = DAL_DENSITY_NONE
+    elif density_kind is not None:
+        kind = density_kind
+    else:
+        kind = DAL_DENSITY_EXACT if density.dtype == torch.float64 else DAL_DENSITY_FIXED
     call("dal_forest_score", _ptr(state.x), n, state.d, state.d, _ptr(inner), _ptr(leaf),
-         forest.n_trees, forest.depth, _ptr(lut_dev), 0 if density is None else _ptr(density),
+         forest.n_trees, forest.depth, _ptr(lut_dev), 0 if density is None else _ptr(density), kind,
          float(density_err), _ptr(flags), float(beta), int(order), _ptr(votes), _ptr(scores),
          _ptr(keys), 0 if keys_hi is None else _ptr(keys_hi), _stream(state.device))
     return votes, scores, keys, keys_hi
@@ -363,9 +396,18 @@ def uncertainty_step(state: PoolState, unlabeled_idx, forest: Forest, k: int,
 
 
 def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: float = 1.0,
-                 density_fixed=None) -> Selection:
+                 density_fixed=None, mode: str = "gram") -> Selection:
     """One iteration of density_weighting.py:133-176 on the GPU:
-    score = ent[v] * d^beta, descending; exact canonical selection."""
+    score = ent[v] * d^beta, descending; exact canonical selection.
+
+    mode "gram": density from the fused MFMA Gram row-sum (the reference's
+    N^2 algorithm) with an exact fp64 re-rank of the boundary candidates;
+    mode "separable": density from the exact O(N*D) identity (scores are then
+    canonical fp64 for every row and the top-k needs no re-rank)."""
+    if mode == "separable":
+        return _density_step_separable(state, unlabeled_idx, forest, k, beta)
+    if mode != "gram":
+        raise ValueError(f"density mode must be 'gram' or 'separable', not {mode!r}")
     flags, unl, n_cand = state.row_flags(unlabeled_idx)
     if n_cand == 0:
         raise ValueError("unlabeled set is empty (the reference loop breaks here)")
@@ -379,4 +421,20 @@ def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: 
     idx, sel_scores, _ = dw_select_local(state, flags, votes, keys_lo, keys_hi, lut_dev, kk, beta,
                                          state.colsum())
     state.check_status()  # already synchronised by dw_select_local
+    return Selection(scores=scores[loc], indices=idx, selected_scores=sel_scores, votes=votes[loc])
+
+
+def _density_step_separable(state: PoolState, unlabeled_idx, forest: Forest, k: int,
+                            beta: float) -> Selection:
+    flags, unl, n_cand = state.row_flags(unlabeled_idx)
+    if n_cand == 0:
+        raise ValueError("unlabeled set is empty (the reference loop breaks here)")
+    kk = min(int(k), n_cand)
+    loc = state.local_positions(unl)
+    lut_dev = device_lut("entropy", forest.n_trees, state.device)
+    votes, scores, keys, _ = forest_score(state, forest, lut_dev, flags, DAL_DESCENDING,
+                                          density=state.density_exact(), beta=beta)
+    idx, _ = topk_keys(keys, kk, state.row_base)
+    sel_scores = scores[idx - state.row_base]
+    state.check_status()
     return Selection(scores=scores[loc], indices=idx, selected_scores=sel_scores, votes=votes[loc])

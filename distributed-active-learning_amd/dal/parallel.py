@@ -163,6 +163,9 @@ class TorchComm:
 
     def all_gather(self, t):
         torch = __import__("torch")
+        if t.is_cuda and self.dist.get_backend(self.group) == "gloo":
+            # rehearsal path (several ranks sharing one GPU): stage through the host
+            return self.all_gather(t.cpu()).to(t.device)
         out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         self.dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
         return out
@@ -195,3 +198,37 @@ def emulate(selectors, unlabeled_idx, forest, k: int, mode: str = "dw",
     idx_all = torch.cat([t.idx for t in tops])
     sc_all = torch.cat([t.scores for t in tops])
     return merge_topk(keys_all, idx_all, sc_all, k, sort_fn)
+
+
+def diversity_select_sharded(x_local, row_base: int, labeled_rows, k: int, comm, candidates=None,
+                             device=None, sort_fn=hip_sort_positions):
+    """Batch-mode diversity selection (BASELINE config 5) over a row-sharded
+    bf16 pool: every rank scores its rows against the replicated labeled set
+    (no exchange), keeps its exact local top-k, and the all-gathered lists are
+    merged identically on every rank."""
+    from .similarity import diversity_select
+
+    torch = __import__("torch")
+    n = int(x_local.shape[0])
+    dev = x_local.device if device is None else device
+    keys = torch.full((k,), _as_i64(DAL_KEY_NONE), dtype=torch.int64, device=dev)
+    idx = torch.full((k,), -1, dtype=torch.int64, device=dev)
+    sc = torch.full((k,), float("nan"), dtype=torch.float64, device=dev)
+    if n:
+        sel = diversity_select(x_local, None, k, candidates=candidates, device=dev, row_base=row_base,
+                               labeled_rows=labeled_rows)
+        kk = int(sel.indices.shape[0])
+        idx[:kk] = sel.indices
+        sc[:kk] = sel.selected_scores
+        keys[:kk] = _score_keys_asc(sel.selected_scores)
+    return merge_topk(comm.all_gather(keys), comm.all_gather(idx), comm.all_gather(sc), k, sort_fn)
+
+
+def _score_keys_asc(s):
+    """Ascending score keys of finite fp64 scores, computed on the device with
+    the C ABI's encoding (-0 -> +0; negative -> ~bits; else bits | sign bit),
+    stored as int64 bit patterns of the uint64 keys."""
+    torch = __import__("torch")
+    s = torch.where(s == 0, torch.zeros_like(s), s)
+    b = s.view(torch.int64)
+    return torch.where(b < 0, ~b, b | (-(1 << 63)))

@@ -93,11 +93,16 @@ def max_cosine(pool, labeled_idx, device=None):
     return out
 
 
-def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, row_base: int = 0):
+def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, row_base: int = 0,
+                     labeled_rows=None):
     """Select the k candidate rows least similar to the labeled set (smallest
     max-cosine, ties -> lower index), exact against the canonical fp64
     max-cosine.  Returns Selection(scores = fp32 max-cos of the candidates,
-    indices [k], selected_scores = canonical fp64 max-cos)."""
+    indices [k], selected_scores = canonical fp64 max-cos).
+
+    For a row shard (multi-GPU) pass ``row_base`` (global index of row 0),
+    global ``candidates`` and the labeled set as ``labeled_rows`` ([m, d],
+    replicated on every rank) instead of ``labeled_idx``."""
     import numpy as np
     import torch
 
@@ -108,8 +113,11 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
     lib = _lib.load()
     x, dev = _bf16_pool(pool, device)
     n, d = int(x.shape[0]), int(x.shape[1])
-    lab_idx = _as_index(labeled_idx, dev)
-    lab = LabeledSet(x[lab_idx], dev)
+    if labeled_rows is not None:
+        lab_rows, _ = _bf16_pool(labeled_rows, dev)
+    else:
+        lab_rows = x[_as_index(labeled_idx, dev)]
+    lab = LabeledSet(lab_rows, dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     inv = torch.empty(n, dtype=torch.float32, device=dev)
     _lib.call("dal_inv_norms_bf16", _ptr(x), n, n, d, d, _ptr(inv), _ptr(status), _stream(dev))

@@ -58,6 +58,10 @@ enum dal_status {
 #define DAL_ROW_CANDIDATE 1 /* row is in the unlabeled set and may be selected */
 #define DAL_ROW_EXCLUDED 2  /* row is in E: dropped from density as i and as j */
 
+#define DAL_DENSITY_NONE 0
+#define DAL_DENSITY_FIXED 1
+#define DAL_DENSITY_EXACT 2
+
 #define DAL_ASCENDING 0
 #define DAL_DESCENDING 1
 
@@ -104,6 +108,13 @@ int dal_canon_colsum_partials(const float* x, int64_t n, int64_t d, int64_t ldx,
                               double* partials, dal_stream_t stream);
 int dal_canon_colsum_reduce(const double* partials, int64_t n_chunks, int64_t d,
                             double* colsum, dal_stream_t stream);
+/* Separable canonical density (the exact identity sum_j <u_i,u_j> = <u_i, s>):
+ * density[i] = sum_f (x_if / norm64[i]) * colsum[f], sequential, no FMA --
+ * bit-identical to the re-rank and the oracle; NaN for EXCLUDED rows.
+ * O(N*D), HBM-bound; the opt-in alternative to dal_gram_rowsum. */
+int dal_density_separable(const float* x, int64_t n, int64_t d, int64_t ldx,
+                          const double* norm64, const double* colsum, const uint8_t* row_flags,
+                          double* density, dal_stream_t stream);
 
 /* ---- (a2-a4) fused cosine Gram row-sum -------------------------------
  * Replaces density_weighting.py:67-75 (IndexedRowMatrix -> BlockMatrix
@@ -125,8 +136,11 @@ int dal_gram_rowsum(const float* u_rows, int64_t n_rows_pad, const float* u_cols
  *   inner[t][h] = {feature (int32), threshold bits (fp32, rounded toward -inf
  *   from fp64 so that x32 <= t32  <=>  x <= t64)}, h < 2^depth - 1,
  *   leaf[t][l] in {0,1}, l < 2^depth.  x[f] <= thr -> child 2h+1, else 2h+2.
- * lut: fp64[T+1].  density (nullable) -> uncertainty mode: score = lut[v];
- * else score = lut[v] * d^beta with d = density*2^-32 (NaN for EXCLUDED rows).
+ * lut: fp64[T+1].  density_kind 0 (density NULL) -> uncertainty mode:
+ * score = lut[v]; else score = lut[v] * d^beta (NaN for EXCLUDED rows) with
+ * d = ((int64*)density)[i] * 2^-32 (kind DAL_DENSITY_FIXED, the GEMM
+ * accumulator; interval scores) or d = ((double*)density)[i] (kind
+ * DAL_DENSITY_EXACT, canonical fp64; exact scores, keys_hi == keys).
  * keys[i] = dal score key for ``order`` (DAL_KEY_NONE when not CANDIDATE).
  * In density mode the GEMM density is approximate, so each score is an
  * interval [score - err_i, score + err_i], err_i = |lut[v]| * density_err
@@ -135,7 +149,7 @@ int dal_gram_rowsum(const float* u_rows, int64_t n_rows_pad, const float* u_cols
  * exact scores (lut[v] == 0 or NaN) have keys[i] == keys_hi[i]. */
 int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ldx,
                      const int32_t* inner, const uint8_t* leaf, int32_t n_trees, int32_t depth,
-                     const double* lut, const int64_t* density, double density_err,
+                     const double* lut, const void* density, int density_kind, double density_err,
                      const uint8_t* row_flags, double beta, int order,
                      int32_t* votes, double* scores, uint64_t* keys, uint64_t* keys_hi,
                      dal_stream_t stream);

@@ -432,3 +432,32 @@ def test_sharded_emulation_bit_identical(cuda, world, mode):
     assert np.array_equal(_np(idx), _np(ref.indices))
     assert np.array_equal(_np(idx), o_idx)
     assert np.array_equal(_np(sc), o_sc)
+
+
+# ------------------------------------------------ separable density -------
+@pytest.mark.parametrize("name", ["synthetic_512x64_T10.npz", "synthetic_4096x256_T10.npz",
+                                  "synthetic_1500x30_T100.npz", "checkerboard2x2.npz"])
+def test_separable_density_bit_exact(cuda, name):
+    from dal import density_weighting as dw
+
+    g = load_golden(name)
+    d = _np(dw.information_density(g["X"], g["excluded"], device=cuda, mode="separable"))
+    assert np.array_equal(d, g["density"], equal_nan=True)
+
+
+def test_separable_select_config2_bit_exact(cuda):
+    from dal import density_weighting as dw
+    from dal.engine import PoolState
+    from dal.forest import Forest
+
+    X = O.synthetic_pool(100_000, 64, seed=0)
+    of = O.synthetic_forest(10, 4, 64, seed=1)
+    F = Forest.synthetic(10, 4, 64, seed=1)
+    E = np.arange(10)
+    unl = np.arange(10, 100_000)
+    st = PoolState(X, excluded=E, device=cuda)
+    sel = dw.select(st, unl, F, 100, mode="separable")
+    ref_sc, ref_idx, ref_ss = O.density_select(X, unl, of, 100, 1.0, E)
+    assert np.array_equal(_np(sel.indices), ref_idx)
+    assert np.array_equal(_np(sel.selected_scores), ref_ss)
+    assert np.array_equal(_np(sel.scores), ref_sc, equal_nan=True)  # every score canonical

@@ -59,5 +59,5 @@ def test_host_argument_validation_without_gpu():
     assert lib.dal_gram_rowsum(p, 256, p, 512, 48, 64, p, 0, None) == -2
     assert lib.dal_topk(p, 10, 11, 0, p, 1 << 20, p, p, None) == -2
     assert lib.dal_topk(p, 100000, 9000, 0, p, 1 << 30, p, p, None) == -5
-    assert lib.dal_forest_score(p, 10, 4, 4, p, p, 3, 17, p, None, 0.0, None, 1.0, 0, p, p, p,
+    assert lib.dal_forest_score(p, 10, 4, 4, p, p, 3, 17, p, None, 0, 0.0, None, 1.0, 0, p, p, p,
                                 None, None) == -3
