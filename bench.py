@@ -308,6 +308,28 @@ def main():
             dist.all_reduce(tw, op=dist.ReduceOp.MAX)
         warm_ms = float(tw[0]) * 1000 / args.warm_steps
 
+    # separable density mode (exact O(N*D) identity): cold step, reported beside
+    sep_ms = None
+    if args.warm_steps > 0:
+        def sep_step():
+            state.clear_caches()
+            if world > 1:
+                sel._density = None
+                return parallel.select(sel, comm, unl, forest, k, mode="dw", density_mode="separable")
+            return engine.density_step(state, unl, forest, k, mode="separable")
+        sep_step()
+        torch.cuda.synchronize()
+        barrier()
+        ts = time.perf_counter()
+        for _ in range(args.warm_steps):
+            sep_step()
+        torch.cuda.synchronize()
+        barrier()
+        ts = torch.tensor([time.perf_counter() - ts], dtype=torch.float64, device=tdev)
+        if world > 1:
+            dist.all_reduce(ts, op=dist.ReduceOp.MAX)
+        sep_ms = float(ts[0]) * 1000 / args.warm_steps
+
     # roofline of the dominant kernel (density Gram row-sum), this rank's launch
     rows_local = (hi - lo) - int(np.sum((excluded >= lo) & (excluded < hi)))
     flops = 2.0 * rows_local * (n - N_EXCLUDED) * d
@@ -342,6 +364,10 @@ def main():
         "selection_latency_ms": ms_per_step,
         "warm_selection_latency_ms": warm_ms,
         "warm_rows_per_s": (n_scored / (warm_ms * 1e-3)) if warm_ms else None,
+        "separable": ({"cold_selection_latency_ms": sep_ms, "rows_per_s": n_scored / (sep_ms * 1e-3),
+                       "note": "density via the exact O(N*D) identity sum_j<u_i,u_j> = <u_i, sum_j u_j> "
+                               "(canonical fp64, same selection); HBM-bound, not the MFMA path"}
+                      if sep_ms else None),
         "roofline": {"bound": "mfma", "kernel": "dal_gram_rowsum (v_mfma_f32_32x32x2_f32)",
                      "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic,

@@ -110,7 +110,8 @@ class ShardedSelector:
         return self._density
 
     def local_select(self, u_full, partials_full, unlabeled_idx, forest, k: int, mode: str = "dw",
-                     strategy: str = "least_confidence", beta: float = 1.0) -> LocalTopk:
+                     strategy: str = "least_confidence", beta: float = 1.0,
+                     density_mode: str = "gram") -> LocalTopk:
         from .engine import (density_error, device_lut, dw_select_local, forest_score, topk_keys)
         from .luts import ASCENDING
 
@@ -126,7 +127,14 @@ class ShardedSelector:
         if n_cand == 0:
             return LocalTopk(keys, idx, scores)
         kk = min(k, n_cand)
-        if mode == "dw":
+        if mode == "dw" and density_mode == "separable":
+            colsum = st.colsum(partials_full)
+            lut_dev = device_lut("entropy", forest.n_trees, st.device)
+            votes, sc, kys, _ = forest_score(st, forest, lut_dev, flags, DAL_DESCENDING,
+                                             density=st.density_exact(colsum), beta=beta)
+            i, kk_keys = topk_keys(kys, kk, st.row_base)
+            s = sc[i - st.row_base]
+        elif mode == "dw":
             dens = self.local_density(u_full)
             colsum = st.colsum(partials_full)
             lut_dev = device_lut("entropy", forest.n_trees, st.device)
@@ -172,13 +180,16 @@ class TorchComm:
 
 
 def select(sel: ShardedSelector, comm, unlabeled_idx, forest, k: int, mode: str = "dw",
-           strategy: str = "least_confidence", beta: float = 1.0, sort_fn=hip_sort_positions):
+           strategy: str = "least_confidence", beta: float = 1.0, sort_fn=hip_sort_positions,
+           density_mode: str = "gram"):
     """One selection step across all ranks; returns (indices [k], scores [k]),
     identical on every rank."""
     u_local, parts = sel.prep()
-    u_full = comm.all_gather(u_local) if mode == "dw" and sel._density is None else None
+    need_u = mode == "dw" and density_mode == "gram" and sel._density is None
+    u_full = comm.all_gather(u_local) if need_u else None
     parts_full = comm.all_gather(parts) if mode == "dw" else None
-    top = sel.local_select(u_full, parts_full, unlabeled_idx, forest, k, mode, strategy, beta)
+    top = sel.local_select(u_full, parts_full, unlabeled_idx, forest, k, mode, strategy, beta,
+                           density_mode)
     keys_all = comm.all_gather(top.keys)
     idx_all = comm.all_gather(top.idx)
     sc_all = comm.all_gather(top.scores)
@@ -186,13 +197,15 @@ def select(sel: ShardedSelector, comm, unlabeled_idx, forest, k: int, mode: str 
 
 
 def emulate(selectors, unlabeled_idx, forest, k: int, mode: str = "dw",
-            strategy: str = "least_confidence", beta: float = 1.0, sort_fn=hip_sort_positions):
+            strategy: str = "least_confidence", beta: float = 1.0, sort_fn=hip_sort_positions,
+            density_mode: str = "gram"):
     """Run P shards in one process (tests): the all-gathers become concatenations."""
     torch = __import__("torch")
     preps = [s.prep() for s in selectors]
     u_full = torch.cat([p[0] for p in preps]) if mode == "dw" else None
     parts_full = torch.cat([p[1] for p in preps]) if mode == "dw" else None
-    tops = [s.local_select(u_full, parts_full, unlabeled_idx, forest, k, mode, strategy, beta)
+    tops = [s.local_select(u_full, parts_full, unlabeled_idx, forest, k, mode, strategy, beta,
+                           density_mode)
             for s in selectors]
     keys_all = torch.cat([t.keys for t in tops])
     idx_all = torch.cat([t.idx for t in tops])

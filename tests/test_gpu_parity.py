@@ -400,7 +400,7 @@ def test_config2_scale_selection_bit_exact(cuda):
 
 # ------------------------------------------------ multi-shard (1 GPU) -----
 @pytest.mark.parametrize("world", [2, 3, 4])
-@pytest.mark.parametrize("mode", ["dw", "us"])
+@pytest.mark.parametrize("mode", ["dw", "us", "dw-separable"])
 def test_sharded_emulation_bit_identical(cuda, world, mode):
     """P row shards (emulated in one process, all-gathers as concatenation)
     give the same density bits and the same selection as P = 1 and the oracle."""
@@ -419,9 +419,14 @@ def test_sharded_emulation_bit_identical(cuda, world, mode):
     for r in range(world):
         lo, hi, _ = parallel.shard_range(n, world, r)
         sels.append(parallel.ShardedSelector(X[lo:hi], n, r, world, excluded=E, device=cuda))
-    idx, sc = parallel.emulate(sels, unl, F, 50, mode=mode)
+    dmode = "separable" if mode == "dw-separable" else "gram"
+    mode = "dw" if mode.startswith("dw") else mode
+    idx, sc = parallel.emulate(sels, unl, F, 50, mode=mode, density_mode=dmode)
     st = PoolState(X, excluded=E, device=cuda)
-    if mode == "dw":
+    if mode == "dw" and dmode == "separable":
+        ref = density_step(st, unl, F, 50, mode="separable")
+        _, o_idx, o_sc = O.density_select(X, unl, of, 50, 1.0, E)
+    elif mode == "dw":
         ref = density_step(st, unl, F, 50)
         _, o_idx, o_sc = O.density_select(X, unl, of, 50, 1.0, E)
         dens = torch.cat([s.state.density_fixed()[: s.state.n] for s in sels])

@@ -55,7 +55,7 @@ class OracleShard(parallel.ShardedSelector):
         return u, parts
 
     def local_select(self, u_full, parts_full, unl, forest, k, mode="dw", strategy="least_confidence",
-                     beta=1.0):
+                     beta=1.0, density_mode="gram"):
         keys = torch.full((k,), parallel._as_i64(0xFFFFFFFFFFFFFFFF), dtype=torch.int64)
         idx = torch.full((k,), -1, dtype=torch.int64)
         sc = torch.full((k,), float("nan"), dtype=torch.float64)
@@ -75,8 +75,6 @@ class OracleShard(parallel.ShardedSelector):
         score = lut("entropy", self.of.n_trees)[v] * dd
         si, ss = O.select_topk(score, mine, k, ascending=False)
         kk = si.size
-        # key: rank of the canonical order, encoded monotonically (test-only)
-        order_key = np.arange(kk) + 1
         keys[:kk] = torch.from_numpy(_float_key(ss))
         idx[:kk] = torch.from_numpy(si)
         sc[:kk] = torch.from_numpy(ss)
@@ -104,6 +102,16 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        _run(rank, world, q)
+    except Exception as e:  # surface worker failures instead of a queue timeout
+        q.put((rank, repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(rank, world, q):
+    if True:
         X = O.synthetic_pool(N, D, seed=4)
         of = O.synthetic_forest(10, 4, D, seed=1)
         E = np.arange(10)
@@ -112,8 +120,6 @@ def _worker(rank, world, port, q):
         idx, sc = parallel.select(sel, parallel.TorchComm(), unl, None, K, mode="dw",
                                   sort_fn=_cpu_sort_positions)
         q.put((rank, idx.numpy(), sc.numpy()))
-    finally:
-        dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -132,6 +138,7 @@ def test_gloo_sharded_density_select_matches_oracle(world):
     of = O.synthetic_forest(10, 4, D, seed=1)
     _, ref_idx, ref_sc = O.density_select(X, np.arange(10, N), of, K, 1.0, np.arange(10))
     for rank, idx, sc in res:
+        assert not isinstance(idx, str), idx
         assert np.array_equal(idx, ref_idx), rank
         assert np.array_equal(sc, ref_sc), rank
 
