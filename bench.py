@@ -157,16 +157,14 @@ def bench_diversity(args, cfg, world, rank, dev, dist, backend):
     from dal.similarity import LabeledSet
 
     L = LabeledSet(lab, dev)
-    inv = torch.empty(hi - lo, dtype=torch.float32, device=dev)
     st = torch.zeros(1, dtype=torch.int32, device=dev)
-    _lib.call("dal_inv_norms_bf16", _ptr(x), hi - lo, hi - lo, d, d, _ptr(inv), _ptr(st), _stream(dev))
     out = torch.empty(hi - lo, dtype=torch.float32, device=dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ms = []
     for _ in range(3):
         e0.record()
-        _lib.call("dal_max_cosine", _ptr(x), hi - lo, d, _ptr(L.rows), L.m_pad, _ptr(L.inv), _ptr(inv),
-                  _ptr(out), _stream(dev))
+        _lib.call("dal_max_cosine", _ptr(x), hi - lo, d, _ptr(L.rows), L.m_pad, _ptr(L.inv), 0,
+                  _ptr(out), _ptr(st), _stream(dev))
         e1.record()
         torch.cuda.synchronize()
         ms.append(e0.elapsed_time(e1))
@@ -178,6 +176,13 @@ def bench_diversity(args, cfg, world, rank, dev, dist, backend):
     elapsed = float(t[0])
     flops = 2.0 * (hi - lo) * m * d
     achieved = flops / (kms * 1e-3) / 1e12
+    traffic = None
+    tpath = os.path.join(REPO, "profiles", "hbm_traffic.json")
+    if os.path.exists(tpath) and world == 1:
+        try:
+            traffic = json.load(open(tpath)).get(f"config{args.config}", {}).get("maxcos_bytes_per_launch")
+        except Exception:
+            traffic = None
     out_line = {
         "metric": "pool rows scored/sec (diversity: max-cosine to labeled set + exact top-k)",
         "value": (n - m) * args.steps / elapsed, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
@@ -188,7 +193,7 @@ def bench_diversity(args, cfg, world, rank, dev, dist, backend):
                    "parallelism": f"row-shard dp{world}" if world > 1 else "single GPU"},
         "roofline": {"bound": "mfma", "kernel": "dal_max_cosine (v_mfma_f32_32x32x16_bf16)",
                      "achieved": achieved, "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / BF16_MFMA_PEAK_TFLOPS, "traffic": None, "launch_ms": kms,
+                     "frac": achieved / BF16_MFMA_PEAK_TFLOPS, "traffic": traffic, "launch_ms": kms,
                      "algorithmic_flops_per_launch": flops,
                      "pool_bytes_per_launch": (hi - lo) * d * 2,
                      "hbm_frac_of_8TBs": (hi - lo) * d * 2 / (kms * 1e-3) / 8e12},

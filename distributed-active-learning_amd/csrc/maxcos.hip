@@ -10,11 +10,22 @@
 // MI355X design: v_mfma_f32_32x32x16_bf16 (fp32 accumulate; bf16 x bf16
 // products are exact in fp32).  A block = 4 waves x 64 pool rows held as A
 // fragments in VGPRs (loaded once from HBM: the pool is streamed exactly
-// once); the labeled rows stream through a 2 x 64 KiB LDS ring by LDS-DMA
-// (source-address XOR swizzle -> conflict-free ds_read_b128).  Each 32x32
-// output tile is scaled by 1/||x_l|| (per lane = per column) and max-reduced
-// into a running per-lane maximum; a 32-lane butterfly max and the row's
-// 1/||x_i|| finish the row.  The similarity matrix is never stored.
+// once); the labeled rows stream through a 2-stage LDS ring by LDS-DMA
+// (source-address XOR swizzle -> conflict-free ds_read_b128, SQ_LDS_BANK_
+// CONFLICT = 0).  Each 32x32 output tile is scaled by 1/||x_l|| (per lane =
+// per column) and max-reduced into a running per-lane maximum; a recursive-
+// halving max over the 32 column lanes and the row's 1/||x_i|| (computed
+// in-kernel from the resident fragments) finish the row.  The similarity
+// matrix is never stored.
+//
+// Measured at 8M x 128, m = 1024 (scripts/maxcos_ab.py, bit-identical
+// outputs): one wave per SIMD with 64 KiB stages 2.78 ms (30% of dense bf16
+// peak; exposed per-block A fetch, 5-step butterfly reduction); two waves per
+// SIMD 2.04 ms; + v_max3 pairs, hoisted DMA offsets, halving reduction
+// 1.80 ms; + immediate-offset B reads 1.75 ms (48%, MFMA busy 61% at the
+// 1.89 GHz the chip holds under this load).
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace dal {
@@ -26,30 +37,41 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kMcThreads = 256;
 constexpr int kMcRows = 256;     // pool rows per block (64 per wave)
-constexpr int kStageF4 = 4096;   // 64 KiB per LDS stage
 constexpr int kMaxLab = 4096;    // labeled rows whose 1/||x|| fit the LDS table
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t b) {
   return __uint_as_float(static_cast<unsigned>(b) << 16);
 }
 
-template <int DK>
-struct McCfg {
-  static constexpr int ROWB = DK * 2;          // bytes per row
-  static constexpr int SLOTS = ROWB / 16;      // 16-B slots per row
-  static constexpr int SR = 65536 / ROWB;      // labeled rows per stage
-  static constexpr int NCT = SR / 32;          // 32-row column tiles per stage
-  static constexpr int NKS = DK / 16;          // k-steps of 16 features
+// Two waves per SIMD (OCC = 2: 32 KiB stages, 1/||x_l|| table in dynamic LDS
+// so two blocks fit a CU): one wave's A-fragment fetch, norm and epilogue VALU
+// run under the other wave's MFMAs.  Column tiles in pairs so the running max
+// takes one v_max3 per two products; branch-free A loads (rows clamped to
+// n-1, never stored); the stage-0 DMA is issued before the A fetch so both are
+// in flight together; d = 128 unrolls the stage loop twice so every B-fragment
+// address is a per-lane base plus an immediate.
+template <int DK, int OCC>
+struct Mc2Cfg {
+  static constexpr int STAGE = OCC == 2 ? 32768 : 65536;
+  static constexpr int F4 = STAGE / 16;
+  static constexpr int ROWB = DK * 2;
+  static constexpr int SLOTS = ROWB / 16;
+  static constexpr int SR = STAGE / ROWB;
+  static constexpr int NCT = SR / 32;
+  static constexpr int NKS = DK / 16;
   static constexpr int SWZ = (SLOTS < 16 ? SLOTS : 16) - 1;
+  static constexpr int PIECES = STAGE / (4 * 1024);  // 1 KiB LDS-DMA pieces per wave per stage
 };
 
-template <int DK>
-__global__ __launch_bounds__(kMcThreads, 1) void maxcos_kernel(
+template <int DK, int OCC>
+__global__ __launch_bounds__(kMcThreads, OCC) void maxcos2_kernel(
     const uint16_t* __restrict__ pool, int64_t n, const uint16_t* __restrict__ lab, int64_t m_pad,
-    const float* __restrict__ inv_lab, const float* __restrict__ inv_pool, float* __restrict__ out) {
-  using C = McCfg<DK>;
-  __shared__ __attribute__((aligned(16))) float4 lds[2 * kStageF4];
-  __shared__ float invl[kMaxLab];
+    const float* __restrict__ inv_lab, const float* __restrict__ inv_pool, float* __restrict__ out,
+    int32_t* __restrict__ status) {
+  using C = Mc2Cfg<DK, OCC>;
+  extern __shared__ __attribute__((aligned(16))) float4 mc_dyn[];
+  float4* lds = mc_dyn;
+  float* invl = reinterpret_cast<float*>(mc_dyn + 2 * C::F4);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int li = lane & 31, lh = lane >> 5;
   const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kMcRows + wave * 64;
@@ -57,89 +79,177 @@ __global__ __launch_bounds__(kMcThreads, 1) void maxcos_kernel(
 
   for (int i = tid; i < m_pad; i += kMcThreads) invl[i] = inv_lab[i];
 
-  auto issue = [&](int buf, int stage) {
-    const char* sbase = reinterpret_cast<const char*>(lab) + static_cast<int64_t>(stage) * 65536;
+  // per-piece source offsets (swizzled) and the wave's LDS base, computed once
+  unsigned voff[C::PIECES];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int base = (wave * 16 + q) * 64;
-      const int p = base + lane;
-      const int row = p / C::SLOTS;
-      const int slot = (p % C::SLOTS) ^ (row & C::SWZ);
-      const unsigned voff = static_cast<unsigned>(row * C::ROWB + slot * 16);
-      const unsigned dst = __builtin_amdgcn_readfirstlane(
-          static_cast<unsigned>(reinterpret_cast<uintptr_t>((AS3 float4*)(lds + buf * kStageF4 + base))));
+  for (int q = 0; q < C::PIECES; ++q) {
+    const int p = (wave * C::PIECES + q) * 64 + lane;
+    const int row = p / C::SLOTS;
+    const int slot = (p % C::SLOTS) ^ (row & C::SWZ);
+    voff[q] = static_cast<unsigned>(row * C::ROWB + slot * 16);
+  }
+  const unsigned dst0 = __builtin_amdgcn_readfirstlane(
+      static_cast<unsigned>(reinterpret_cast<uintptr_t>((AS3 float4*)(lds + wave * C::PIECES * 64))));
+  auto issue = [&](int buf, int stage) {
+    const char* sbase = reinterpret_cast<const char*>(lab) + static_cast<int64_t>(stage) * C::STAGE;
+#pragma unroll
+    for (int q = 0; q < C::PIECES; ++q) {
+      const unsigned dst = dst0 + static_cast<unsigned>(buf * C::STAGE + q * 1024);
       unsigned keep;
       asm volatile(
           "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
           "global_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %0"
           : "=&s"(keep)
-          : "v"(voff), "s"(dst), "s"(sbase)
+          : "v"(voff[q]), "s"(dst), "s"(sbase)
           : "memory");
     }
   };
+  // stage 0 first: the compiler's own waits for the (younger) A loads then
+  // also cover it, which is conservative and correct
+  issue(0, 0);
 
-  // A fragments: lane (li, lh) holds features 16s + 8lh .. +7 of its two rows
   bf16x8 a[2][C::NKS];
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt) {
-    const int64_t row = row0 + rt * 32 + li;
+    int64_t row = row0 + rt * 32 + li;
+    row = row < n ? row : n - 1;
+#pragma unroll
+    for (int s = 0; s < C::NKS; ++s)
+      a[rt][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pool + row * DK + 16 * s + 8 * lh));
+  }
+
+  // 1/||x_i||: fp64 sum of squares of the register-resident fragments; v*v is
+  // exact in fp64, so fma(v, v, s) == s + v*v (dal_inv_norms_bf16's value)
+  float inv_row[2];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    double s2 = 0.0;
 #pragma unroll
     for (int s = 0; s < C::NKS; ++s) {
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (row < n) v = *reinterpret_cast<const uint4*>(pool + row * DK + 16 * s + 8 * lh);
-      a[rt][s] = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const double v = static_cast<double>(static_cast<float>(a[rt][s][e]));
+        s2 = __builtin_fma(v, v, s2);
+      }
     }
+    s2 = s2 + __shfl_xor(s2, 32);
+    inv_row[rt] = static_cast<float>(1.0 / __builtin_sqrt(s2));
   }
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // A landed; keep hipcc from re-waiting under the DMA
 
   float mx0[16], mx1[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) mx0[r] = mx1[r] = -__builtin_inff();
   const f32x16 zero = {};
 
-  issue(0, 0);
-  for (int st = 0; st < n_stages; ++st) {
+  // per-lane LDS offsets of the B fragment of each k-step (float4 units);
+  // column-tile and ring-buffer offsets are compile-time immediates
+  int boff[C::NKS];
+#pragma unroll
+  for (int s = 0; s < C::NKS; ++s) boff[s] = li * C::SLOTS + ((2 * s + lh) ^ (li & C::SWZ));
+
+  auto stage_body = [&](auto bufc, int st) {
+    constexpr int buf = decltype(bufc)::value;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (st + 1 < n_stages) issue(buf ^ 1, st + 1);
+    const float4* B = lds + buf * C::F4;
+#pragma unroll
+    for (int ct = 0; ct < C::NCT; ct += 2) {
+      f32x16 c0, c1, d0, d1;
+#pragma unroll
+      for (int s = 0; s < C::NKS; ++s) {
+        const bf16x8 b = __builtin_bit_cast(bf16x8, B[ct * 32 * C::SLOTS + boff[s]]);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][s], b, s == 0 ? zero : c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][s], b, s == 0 ? zero : c1, 0, 0, 0);
+      }
+#pragma unroll
+      for (int s = 0; s < C::NKS; ++s) {
+        const bf16x8 b = __builtin_bit_cast(bf16x8, B[(ct + 1) * 32 * C::SLOTS + boff[s]]);
+        d0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][s], b, s == 0 ? zero : d0, 0, 0, 0);
+        d1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][s], b, s == 0 ? zero : d1, 0, 0, 0);
+      }
+      // padded labeled rows carry NaN -> ignored by fmaxf
+      const float ila = invl[st * C::SR + ct * 32 + li], ilb = invl[st * C::SR + ct * 32 + 32 + li];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        mx0[r] = fmaxf(fmaxf(mx0[r], c0[r] * ila), d0[r] * ilb);  // one v_max3
+        mx1[r] = fmaxf(fmaxf(mx1[r], c1[r] * ila), d1[r] * ilb);
+      }
+    }
+  };
+  auto stage_body_rt = [&](int st) {
     const int buf = st & 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (st + 1 < n_stages) issue(buf ^ 1, st + 1);
-    const float4* B = lds + buf * kStageF4;
+    const float4* B = lds + buf * C::F4;
 #pragma unroll
-    for (int ct = 0; ct < C::NCT; ++ct) {
-      const int rowj = ct * 32 + li;
-      f32x16 c0, c1;
+    for (int ct = 0; ct < C::NCT; ct += 2) {
+      f32x16 c0, c1, d0, d1;
 #pragma unroll
       for (int s = 0; s < C::NKS; ++s) {
-        const bf16x8 b = __builtin_bit_cast(bf16x8, B[rowj * C::SLOTS + ((2 * s + lh) ^ (rowj & C::SWZ))]);
+        const bf16x8 b = __builtin_bit_cast(bf16x8, B[ct * 32 * C::SLOTS + boff[s]]);
         c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][s], b, s == 0 ? zero : c0, 0, 0, 0);
         c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][s], b, s == 0 ? zero : c1, 0, 0, 0);
       }
-      // column j = lane's labeled row; padded rows carry NaN -> ignored by fmaxf
-      const float il = invl[st * C::SR + rowj];
+#pragma unroll
+      for (int s = 0; s < C::NKS; ++s) {
+        const bf16x8 b = __builtin_bit_cast(bf16x8, B[(ct + 1) * 32 * C::SLOTS + boff[s]]);
+        d0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][s], b, s == 0 ? zero : d0, 0, 0, 0);
+        d1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][s], b, s == 0 ? zero : d1, 0, 0, 0);
+      }
+      // padded labeled rows carry NaN -> ignored by fmaxf
+      const float ila = invl[st * C::SR + ct * 32 + li], ilb = invl[st * C::SR + ct * 32 + 32 + li];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        mx0[r] = fmaxf(mx0[r], c0[r] * il);
-        mx1[r] = fmaxf(mx1[r], c1[r] * il);
+        mx0[r] = fmaxf(fmaxf(mx0[r], c0[r] * ila), d0[r] * ilb);  // one v_max3
+        mx1[r] = fmaxf(fmaxf(mx1[r], c1[r] * ila), d1[r] * ilb);
       }
     }
+  };
+  if constexpr (OCC == 2 && DK == 128) {
+    // the label granule (65536 / (2d) rows) is two 32 KiB stages: n_stages is even
+    for (int st = 0; st < n_stages; st += 2) {
+      stage_body(std::integral_constant<int, 0>{}, st);
+      stage_body(std::integral_constant<int, 1>{}, st + 1);
+    }
+  } else {
+    // d = 64 unrolled twice exceeds the 256-register budget: keep one body
+    for (int st = 0; st < n_stages; ++st) stage_body_rt(st);
   }
-  // max over the 32 column lanes of each half; row = (r&3) + 8(r>>2) + 4h
+  // max over the 32 column lanes by recursive halving: at mask m a lane keeps
+  // the half of its 2m values selected by (li & m) and folds in the partner's
+  // copy of that half (31 shuffles).  Lane li ends with value j = li, i.e.
+  // row tile li>>4, accumulator element r = li&15.
+  float v[32];
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
+    v[r] = mx0[r];
+    v[16 + r] = mx1[r];
+  }
 #pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-      mx0[r] = fmaxf(mx0[r], __shfl_xor(mx0[r], o));
-      mx1[r] = fmaxf(mx1[r], __shfl_xor(mx1[r], o));
+  for (int step = 0; step < 5; ++step) {
+    const int m = 16 >> step;
+    // bit-mask selects (a ternary on array elements becomes dynamic indexing)
+    const unsigned upm = (li & m) ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+    for (int j = 0; j < m; ++j) {
+      const unsigned lo = __float_as_uint(v[j]), hi = __float_as_uint(v[j + m]);
+      const float send = __uint_as_float((lo & upm) | (hi & ~upm));
+      const float keep = __uint_as_float((hi & upm) | (lo & ~upm));
+      v[j] = fmaxf(keep, __shfl_xor(send, m));
     }
   }
-  float mine = 0.0f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    if (r == (li & 15)) mine = (li >> 4) ? mx1[r] : mx0[r];
-  }
+  const float mine = v[0];
   const int r = li & 15;
-  const int64_t row = row0 + (li >> 4) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-  if (row < n) out[row] = mine * inv_pool[row];
+  const int rl = (li >> 4) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+  const float inv0 = __shfl(inv_row[0], rl & 31), inv1 = __shfl(inv_row[1], rl & 31);
+  const int64_t row = row0 + rl;
+  if (row < n) {
+    const float iv = inv_pool ? inv_pool[row] : ((rl >> 5) ? inv1 : inv0);
+    if (!(iv < __builtin_inff())) atomicOr(status, DAL_FLAG_ZERO_NORM);
+    out[row] = mine * iv;
+  }
 }
 
 // 1/||x|| (fp32) of bf16 rows, ||x||^2 summed in fp64; zero rows flag status.
@@ -163,9 +273,10 @@ __global__ __launch_bounds__(256) void inv_norms_bf16_kernel(const uint16_t* __r
   inv[i] = static_cast<float>(1.0 / __builtin_sqrt(s));
 }
 
-// Canonical fp64 unit rows of a bf16 table (sequential norm, then divide).
+// Canonical fp64 unit rows of a bf16 table (sequential norm, then divide),
+// stored row-major u[i * d + f] or feature-major u[f * n + i].
 __global__ __launch_bounds__(64) void canon_unit_rows_bf16_kernel(const uint16_t* __restrict__ x, int64_t n,
-                                                                  int d, int64_t ld,
+                                                                  int d, int64_t ld, int feature_major,
                                                                   double* __restrict__ u) {
   const int64_t i = blockIdx.x;
   if (i >= n) return;
@@ -175,15 +286,23 @@ __global__ __launch_bounds__(64) void canon_unit_rows_bf16_kernel(const uint16_t
     s = s + v * v;
   }
   const double nr = __builtin_sqrt(s);
-  for (int f = threadIdx.x; f < d; f += 64) u[i * d + f] = static_cast<double>(bf16_to_f32(x[i * ld + f])) / nr;
+  for (int f = threadIdx.x; f < d; f += 64) {
+    const double v = static_cast<double>(bf16_to_f32(x[i * ld + f])) / nr;
+    u[feature_major ? f * n + i : i * d + f] = v;
+  }
 }
 
 template <int DK>
 int launch_maxcos(const uint16_t* pool, int64_t n, const uint16_t* lab, int64_t m_pad, const float* inv_lab,
-                  const float* inv_pool, float* out, hipStream_t st) {
+                  const float* inv_pool, float* out, int32_t* status, hipStream_t st) {
   const int64_t blocks = ceil_div(n, kMcRows);
-  hipLaunchKernelGGL(maxcos_kernel<DK>, dim3(static_cast<unsigned>(blocks)), dim3(kMcThreads), 0, st, pool,
-                     n, lab, m_pad, inv_lab, inv_pool, out);
+  constexpr int OCC = DK <= 128 ? 2 : 1;
+  const size_t shm = 2 * Mc2Cfg<DK, OCC>::STAGE + static_cast<size_t>(m_pad) * 4;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(maxcos2_kernel<DK, OCC>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm)) != hipSuccess)
+    return DAL_ERR_HIP;
+  hipLaunchKernelGGL((maxcos2_kernel<DK, OCC>), dim3(static_cast<unsigned>(blocks)), dim3(kMcThreads), shm, st,
+                     pool, n, lab, m_pad, inv_lab, inv_pool, out, status);
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
 }
@@ -205,12 +324,12 @@ extern "C" int dal_inv_norms_bf16(const uint16_t* x, int64_t n, int64_t n_pad, i
   return DAL_OK;
 }
 
-extern "C" int dal_canon_unit_rows_bf16(const uint16_t* x, int64_t n, int64_t d, int64_t ld, double* u,
-                                        dal_stream_t stream) {
+extern "C" int dal_canon_unit_rows_bf16(const uint16_t* x, int64_t n, int64_t d, int64_t ld,
+                                        int feature_major, double* u, dal_stream_t stream) {
   if (!x || !u) return DAL_ERR_ARG;
   if (n < 1 || d < 1 || ld < d) return DAL_ERR_SHAPE;
   hipLaunchKernelGGL(canon_unit_rows_bf16_kernel, dim3(static_cast<unsigned>(n)), dim3(64), 0,
-                     as_stream(stream), x, n, static_cast<int>(d), ld, u);
+                     as_stream(stream), x, n, static_cast<int>(d), ld, feature_major, u);
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
 }
@@ -223,13 +342,13 @@ extern "C" double dal_maxcos_error_bound(int64_t d) {
 
 extern "C" int dal_max_cosine(const uint16_t* pool, int64_t n, int64_t d, const uint16_t* lab, int64_t m_pad,
                               const float* inv_lab, const float* inv_pool, float* out_max,
-                              dal_stream_t stream) {
-  if (!pool || !lab || !inv_lab || !inv_pool || !out_max) return DAL_ERR_ARG;
+                              int32_t* dev_status, dal_stream_t stream) {
+  if (!pool || !lab || !inv_lab || !out_max || !dev_status) return DAL_ERR_ARG;
   if (n < 1 || (d != 64 && d != 128 && d != 256)) return DAL_ERR_SHAPE;
   if (m_pad < 1 || m_pad % dal_maxcos_label_rows_granule(d) || m_pad > kMaxLab) return DAL_ERR_SHAPE;
   if ((reinterpret_cast<uintptr_t>(pool) | reinterpret_cast<uintptr_t>(lab)) & 15) return DAL_ERR_SHAPE;
   hipStream_t st = as_stream(stream);
-  if (d == 64) return launch_maxcos<64>(pool, n, lab, m_pad, inv_lab, inv_pool, out_max, st);
-  if (d == 128) return launch_maxcos<128>(pool, n, lab, m_pad, inv_lab, inv_pool, out_max, st);
-  return launch_maxcos<256>(pool, n, lab, m_pad, inv_lab, inv_pool, out_max, st);
+  if (d == 64) return launch_maxcos<64>(pool, n, lab, m_pad, inv_lab, inv_pool, out_max, dev_status, st);
+  if (d == 128) return launch_maxcos<128>(pool, n, lab, m_pad, inv_lab, inv_pool, out_max, dev_status, st);
+  return launch_maxcos<256>(pool, n, lab, m_pad, inv_lab, inv_pool, out_max, dev_status, st);
 }

@@ -357,49 +357,126 @@ __global__ __launch_bounds__(256) void rerank_kernel(const TopkHdr* __restrict__
 // way; max keeps the first (lowest l) maximum.
 __device__ __forceinline__ float bf16f(uint16_t b) { return __uint_as_float(static_cast<unsigned>(b) << 16); }
 
+// Canonical fp64 max-cosine of the candidates (oracle: max_cosine_canonical):
+// u_i = x_i / sqrt(sum_f x_if^2) (sequential), cos_il = sum_f u_if * ulab_lf
+// (sequential in f, no FMA), max over l, ties -> lowest l.  A block takes
+// kRrC candidates: their unit rows are computed once into LDS, then each
+// lane carries kRrC x kRrJ independent accumulators over labeled rows
+// l = lane + 64 * (wave + 4 j) (+ 1024 per outer pass), reading the
+// feature-major table ulabT[f * m + l] coalesced; the per-(c, l) sums keep
+// the canonical sequential order in f.
+constexpr int kRrC = 4;
+constexpr int kRrJ = 4;
 __global__ __launch_bounds__(256) void rerank_maxcos_kernel(const TopkHdr* __restrict__ h, int64_t idx_base,
                                                             const uint16_t* __restrict__ pool, int d,
-                                                            int64_t ld, const double* __restrict__ ulab,
+                                                            int64_t ld, const double* __restrict__ ulabT,
                                                             int64_t m, uint64_t* __restrict__ ckey,
                                                             const int64_t* __restrict__ cidx,
                                                             double* __restrict__ cpay, int64_t cap) {
-  const int lane = threadIdx.x & 63;
-  const int64_t c = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  if (c >= cap) return;
-  if (c >= h->cand_count) {
-    if (lane == 0) ckey[c] = DAL_KEY_NONE;
+  __shared__ double su[256][kRrC];  // [f][candidate]
+  __shared__ double rb[4][kRrC];
+  __shared__ long long ra[4][kRrC];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int64_t c0 = static_cast<int64_t>(blockIdx.x) * kRrC;
+  const int64_t count = h->cand_count;
+  if (c0 >= count) {
+    if (tid < kRrC && c0 + tid < cap) ckey[c0 + tid] = DAL_KEY_NONE;
     return;
   }
-  const int64_t i = cidx[c] - idx_base;
-  const uint16_t* xr = pool + i * ld;
-  double n2 = 0.0;
-  for (int f = 0; f < d; ++f) {
-    const double v = bf16f(xr[f]);
-    n2 = n2 + v * v;
-  }
-  const double nr = __builtin_sqrt(n2);
-  double best = -__builtin_inf();
-  int64_t arg = 0x7FFFFFFFFFFFFFFFll;
-  for (int64_t l = lane; l < m; l += 64) {
-    const double* ul = ulab + l * d;
-    double acc = 0.0;
-    for (int f = 0; f < d; ++f) acc = acc + (static_cast<double>(bf16f(xr[f])) / nr) * ul[f];
-    if (acc > best) {
-      best = acc;
-      arg = l;
+  // wave w builds candidate c0 + w's canonical unit row (every lane runs the
+  // same sequential norm; lanes then divide their features)
+  if (wave < kRrC) {
+    const int64_t c = c0 + wave;
+    if (c < count) {
+      const uint16_t* xr = pool + (cidx[c] - idx_base) * ld;
+      double n2 = 0.0;
+      for (int f = 0; f < d; ++f) {
+        const double v = bf16f(xr[f]);
+        n2 = n2 + v * v;
+      }
+      const double nr = __builtin_sqrt(n2);
+      for (int f = lane; f < d; f += 64) su[f][wave] = static_cast<double>(bf16f(xr[f])) / nr;
+    } else {
+      for (int f = lane; f < d; f += 64) su[f][wave] = 0.0;
     }
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    const double ob = __shfl_xor(best, o);
-    const long long oa = __shfl_xor(static_cast<long long>(arg), o);
-    if (ob > best || (ob == best && oa < arg)) {
-      best = ob;
-      arg = oa;
+  __syncthreads();
+  double best[kRrC];
+  long long arg[kRrC];
+#pragma unroll
+  for (int q = 0; q < kRrC; ++q) {
+    best[q] = -__builtin_inf();
+    arg[q] = 0x7FFFFFFFFFFFFFFFll;
+  }
+  for (int64_t lb = 0; lb < m; lb += 256 * kRrJ) {
+    int64_t l[kRrJ];
+    bool ok[kRrJ];
+#pragma unroll
+    for (int j = 0; j < kRrJ; ++j) {
+      l[j] = lb + lane + 64 * (wave + 4 * j);
+      ok[j] = l[j] < m;
+      if (!ok[j]) l[j] = m - 1;
+    }
+    double acc[kRrC][kRrJ];
+#pragma unroll
+    for (int q = 0; q < kRrC; ++q)
+#pragma unroll
+      for (int j = 0; j < kRrJ; ++j) acc[q][j] = 0.0;
+    for (int f = 0; f < d; ++f) {
+      double ul[kRrJ];
+#pragma unroll
+      for (int j = 0; j < kRrJ; ++j) ul[j] = ulabT[static_cast<int64_t>(f) * m + l[j]];
+#pragma unroll
+      for (int q = 0; q < kRrC; ++q) {
+        const double uq = su[f][q];
+#pragma unroll
+        for (int j = 0; j < kRrJ; ++j) acc[q][j] = acc[q][j] + uq * ul[j];
+      }
+    }
+    // l increases with j: strict > keeps the lowest l among equal values
+#pragma unroll
+    for (int j = 0; j < kRrJ; ++j) {
+#pragma unroll
+      for (int q = 0; q < kRrC; ++q) {
+        if (ok[j] && acc[q][j] > best[q]) {
+          best[q] = acc[q][j];
+          arg[q] = l[j];
+        }
+      }
     }
   }
-  if (lane == 0) {
-    cpay[c] = best;
-    ckey[c] = score_key(best, DAL_ASCENDING);
+#pragma unroll
+  for (int q = 0; q < kRrC; ++q) {
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ob = __shfl_xor(best[q], o);
+      const long long oa = __shfl_xor(arg[q], o);
+      if (ob > best[q] || (ob == best[q] && oa < arg[q])) {
+        best[q] = ob;
+        arg[q] = oa;
+      }
+    }
+    if (lane == 0) {
+      rb[wave][q] = best[q];
+      ra[wave][q] = arg[q];
+    }
+  }
+  __syncthreads();
+  if (tid < kRrC) {
+    const int64_t c = c0 + tid;
+    double b = rb[0][tid];
+    long long a = ra[0][tid];
+    for (int w = 1; w < 4; ++w) {
+      if (rb[w][tid] > b || (rb[w][tid] == b && ra[w][tid] < a)) {
+        b = rb[w][tid];
+        a = ra[w][tid];
+      }
+    }
+    if (c < count) {
+      cpay[c] = b;
+      ckey[c] = score_key(b, DAL_ASCENDING);
+    } else if (c < cap) {
+      ckey[c] = DAL_KEY_NONE;
+    }
   }
 }
 
@@ -619,10 +696,10 @@ extern "C" int dal_maxcos_select(const uint64_t* keys_lo, const uint64_t* keys_h
                                  int32_t* dev_status, dal_stream_t stream) {
   if (!keys_lo || !keys_hi || !pool || !ulab || !ws || !out_idx || !out_scores || !dev_status)
     return DAL_ERR_ARG;
-  if (d < 1 || ld < d || m < 1) return DAL_ERR_SHAPE;
+  if (d < 1 || d > 256 || ld < d || m < 1) return DAL_ERR_SHAPE;
   hipStream_t st = as_stream(stream);
   auto rerank = [&](TopkHdr* h, uint64_t* ckey, int64_t* cidx, double* cpay, int64_t cp) {
-    hipLaunchKernelGGL(rerank_maxcos_kernel, dim3(static_cast<unsigned>(ceil_div(cp, 4))), dim3(256), 0, st,
+    hipLaunchKernelGGL(rerank_maxcos_kernel, dim3(static_cast<unsigned>(ceil_div(cp, kRrC))), dim3(256), 0, st,
                        h, idx_base, pool, static_cast<int>(d), ld, ulab, m, ckey, cidx, cpay, cp);
   };
   return select_with_rerank(keys_lo, keys_hi, n, k, idx_base, cap, ws, ws_bytes, rerank, out_idx, out_scores,

@@ -47,7 +47,7 @@ def _bf16_pool(pool, device):
 class LabeledSet:
     """The labeled rows as the kernel's B operand: bf16 [m_pad, d] (padding
     rows carry 1/||x|| = NaN, ignored by the max), fp32 1/||x||, and the
-    canonical fp64 unit rows for the exact re-rank."""
+    canonical fp64 unit rows (feature-major) for the exact re-rank."""
 
     def __init__(self, rows_bf16, device):
         import torch
@@ -66,8 +66,10 @@ class LabeledSet:
         self.inv = torch.empty(m_pad, dtype=torch.float32, device=device)
         _lib.call("dal_inv_norms_bf16", _ptr(self.rows), m, m_pad, d, d, _ptr(self.inv),
                   _ptr(self.status), _stream(device))
-        self.unit64 = torch.empty((m, d), dtype=torch.float64, device=device)
-        _lib.call("dal_canon_unit_rows_bf16", _ptr(self.rows), m, d, d, _ptr(self.unit64),
+        # canonical fp64 unit rows, feature-major [d][m] (the re-rank reads
+        # them coalesced across labeled rows)
+        self.unit64_t = torch.empty((d, m), dtype=torch.float64, device=device)
+        _lib.call("dal_canon_unit_rows_bf16", _ptr(self.rows), m, d, d, 1, _ptr(self.unit64_t),
                   _stream(device))
 
 
@@ -83,11 +85,9 @@ def max_cosine(pool, labeled_idx, device=None):
     n, d = int(x.shape[0]), int(x.shape[1])
     lab = LabeledSet(x[_as_index(labeled_idx, dev)], dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
-    inv = torch.empty(n, dtype=torch.float32, device=dev)
-    _lib.call("dal_inv_norms_bf16", _ptr(x), n, n, d, d, _ptr(inv), _ptr(status), _stream(dev))
     out = torch.empty(n, dtype=torch.float32, device=dev)
-    _lib.call("dal_max_cosine", _ptr(x), n, d, _ptr(lab.rows), lab.m_pad, _ptr(lab.inv), _ptr(inv),
-              _ptr(out), _stream(dev))
+    _lib.call("dal_max_cosine", _ptr(x), n, d, _ptr(lab.rows), lab.m_pad, _ptr(lab.inv), 0,
+              _ptr(out), _ptr(status), _stream(dev))
     if int(status.item()) | int(lab.status.item()):
         raise ValueError("zero-norm row: cosine undefined")
     return out
@@ -119,17 +119,23 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
         lab_rows = x[_as_index(labeled_idx, dev)]
     lab = LabeledSet(lab_rows, dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
-    inv = torch.empty(n, dtype=torch.float32, device=dev)
-    _lib.call("dal_inv_norms_bf16", _ptr(x), n, n, d, d, _ptr(inv), _ptr(status), _stream(dev))
     mx = torch.empty(n, dtype=torch.float32, device=dev)
-    _lib.call("dal_max_cosine", _ptr(x), n, d, _ptr(lab.rows), lab.m_pad, _ptr(lab.inv), _ptr(inv),
-              _ptr(mx), _stream(dev))
-    flags = torch.zeros(n, dtype=torch.uint8, device=dev)
-    cand = (torch.arange(n, device=dev) if candidates is None
-            else _as_index(candidates, dev) - row_base)
-    cand = cand[(cand >= 0) & (cand < n)]
-    flags[cand] = DAL_ROW_CANDIDATE
-    kk = min(int(k), int(cand.shape[0]))
+    _lib.call("dal_max_cosine", _ptr(x), n, d, _ptr(lab.rows), lab.m_pad, _ptr(lab.inv), 0,
+              _ptr(mx), _ptr(status), _stream(dev))
+    if candidates is None:
+        flags = torch.full((n,), DAL_ROW_CANDIDATE, dtype=torch.uint8, device=dev)
+        cand = torch.arange(n, device=dev)
+        n_cand = n
+    else:
+        flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+        gidx = _as_index(candidates, dev)
+        _lib.call("dal_mark_rows", _ptr(gidx), int(gidx.shape[0]), int(row_base), n, DAL_ROW_CANDIDATE,
+                  _ptr(flags), _stream(dev))
+        cand = gidx - row_base
+        if row_base != 0:
+            cand = cand[(cand >= 0) & (cand < n)]
+        n_cand = int(cand.shape[0])
+    kk = min(int(k), n_cand)
     lo = torch.empty(n, dtype=torch.int64, device=dev)
     hi = torch.empty(n, dtype=torch.int64, device=dev)
     _lib.call("dal_interval_keys_f32", _ptr(mx), n, float(lib.dal_maxcos_error_bound(d)), _ptr(flags),
@@ -141,7 +147,7 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
         out_idx = torch.empty(kk, dtype=torch.int64, device=dev)
         out_sc = torch.empty(kk, dtype=torch.float64, device=dev)
         _lib.call("dal_maxcos_select", _ptr(lo), _ptr(hi), n, kk, int(row_base), _ptr(x), d, d,
-                  _ptr(lab.unit64), lab.m, cap, wsp, wsb, _ptr(out_idx), _ptr(out_sc), 0,
+                  _ptr(lab.unit64_t), lab.m, cap, wsp, wsb, _ptr(out_idx), _ptr(out_sc), 0,
                   _ptr(status), _stream(dev))
         st = int(status.item()) | int(lab.status.item())
         if st & 1:

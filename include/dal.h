@@ -188,23 +188,28 @@ int dal_dw_select(const uint64_t* keys_lo, const uint64_t* keys_hi, const int32_
  * d in {64,128,256}) and a bf16 labeled table [m_pad][d] whose rows beyond the
  * real m carry inv_lab = NaN (ignored).  bf16 MFMA (v_mfma_f32_32x32x16_bf16),
  * fp32 accumulate, row-max epilogue; the n x m matrix is never stored.
- * m_pad % dal_maxcos_label_rows_granule(d) == 0, m_pad <= 4096.
+ * m_pad % dal_maxcos_label_rows_granule(d) == 0, m_pad <= 4096.  inv_pool
+ * (nullable): per-row 1/||x_i||; NULL computes it in-kernel (fp64 sum of
+ * squares from the register-resident row fragments).
  * |m_gpu - m_canonical| <= dal_maxcos_error_bound(d) (Cauchy-Schwarz). */
 int64_t dal_maxcos_label_rows_granule(int64_t d);
 double dal_maxcos_error_bound(int64_t d);
 int dal_inv_norms_bf16(const uint16_t* x, int64_t n, int64_t n_pad, int64_t d, int64_t ld,
                        float* inv, int32_t* dev_status, dal_stream_t stream);
-int dal_canon_unit_rows_bf16(const uint16_t* x, int64_t n, int64_t d, int64_t ld, double* u,
-                             dal_stream_t stream);
+/* Canonical fp64 unit rows (sequential fp64 norm, then divide) of n bf16
+ * rows: u[i * d + f] (feature_major = 0) or u[f * n + i] (feature_major = 1). */
+int dal_canon_unit_rows_bf16(const uint16_t* x, int64_t n, int64_t d, int64_t ld, int feature_major,
+                             double* u, dal_stream_t stream);
 int dal_max_cosine(const uint16_t* pool, int64_t n, int64_t d, const uint16_t* lab, int64_t m_pad,
-                   const float* inv_lab, const float* inv_pool, float* out_max, dal_stream_t stream);
+                   const float* inv_lab, const float* inv_pool, float* out_max,
+                   int32_t* dev_status, dal_stream_t stream);
 /* Interval keys [v - err, v + err] of fp32 values (pessimistic -> keys_lo). */
 int dal_interval_keys_f32(const float* values, int64_t n, double err, const uint8_t* row_flags,
                           int order, uint64_t* keys_lo, uint64_t* keys_hi, dal_stream_t stream);
 /* Diversity selection: the k rows with the smallest canonical fp64 max-cosine
  * (ties -> lower index), from interval keys of dal_max_cosine's output;
- * ulab = canonical fp64 unit rows of the m labeled rows
- * (dal_canon_unit_rows_bf16).  Same candidate/re-rank contract as dal_dw_select. */
+ * ulab = canonical fp64 unit rows of the m labeled rows, feature-major
+ * [d][m] (dal_canon_unit_rows_bf16 with feature_major = 1); d <= 256.  Same candidate/re-rank contract as dal_dw_select. */
 size_t dal_maxcos_select_workspace_bytes(int64_t n, int64_t k, int64_t cap);
 int dal_maxcos_select(const uint64_t* keys_lo, const uint64_t* keys_hi, int64_t n, int64_t k,
                       int64_t idx_base, const uint16_t* pool, int64_t d, int64_t ld,

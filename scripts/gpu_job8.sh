@@ -1,0 +1,10 @@
+set -u
+R=$GRAFT_REPO_ROOT
+mkdir -p $R/gpurun_out/pmc_mc
+cd /tmp && export TMPDIR=/tmp
+export AB_VARIANTS=v2
+timeout -s KILL 90 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d $R/gpurun_out/pmc_mc/p1 -o run --output-format csv -- python3 $R/scripts/maxcos_ab.py 2 > $R/gpurun_out/pmc_mc/p1.log 2>&1; rc=$?; echo "p1 rc=$rc"
+[ $rc -eq 0 ] || exit $rc
+timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM_RD SQ_LDS_DATA_FIFO_FULL -d $R/gpurun_out/pmc_mc/p2 -o run --output-format csv -- python3 $R/scripts/maxcos_ab.py 2 > $R/gpurun_out/pmc_mc/p2.log 2>&1; rc=$?; echo "p2 rc=$rc"
+[ $rc -eq 0 ] || exit $rc
+timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_mc/p3 -o run --output-format csv -- python3 $R/scripts/maxcos_ab.py 2 > $R/gpurun_out/pmc_mc/p3.log 2>&1; rc=$?; echo "p3 rc=$rc"
