@@ -114,6 +114,27 @@ def cpu_baseline(x_host: np.ndarray, cfg, of, budget_s: float = 12.0):
 
 
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
+F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 MFMA (same cycles as bf16)
+
+
+def gram_roofline(gram, achieved, traffic, gram_ms, gram_ms_max, flops):
+    """Roofline entry of the density GEMM.  achieved = ALGORITHMIC flops
+    (2 per feature per (row, column) pair) / launch time.  The split kernel
+    issues three fp16 MFMA products per algorithmic product, so its ceiling is
+    the dense fp16 peak / 3; the native fp32-MFMA peak is reported beside."""
+    if gram == "f32":
+        return {"bound": "mfma", "kernel": "dal_gram_rowsum (v_mfma_f32_32x32x2_f32)",
+                "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic, "launch_ms": gram_ms,
+                "launch_ms_max_over_ranks": gram_ms_max, "algorithmic_flops_per_launch": flops}
+    peak = F16_MFMA_PEAK_TFLOPS / 3.0
+    return {"bound": "mfma",
+            "kernel": "dal_gram_rowsum_split (3 x v_mfma_f32_32x32x16_f16 per 16 features: h.h, h.l, l.h)",
+            "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+            "peak_note": "dense fp16 MFMA peak 2500 TF/s / 3 products per algorithmic product",
+            "executed_fp16_tflops": 3.0 * achieved, "vs_fp32_mfma_peak": achieved / FP32_MFMA_PEAK_TFLOPS,
+            "traffic": traffic, "launch_ms": gram_ms, "launch_ms_max_over_ranks": gram_ms_max,
+            "algorithmic_flops_per_launch": flops}
 
 
 def bench_diversity(args, cfg, world, rank, dev, dist, backend):
@@ -284,7 +305,8 @@ def main():
     elapsed = time.perf_counter() - t0
     events = state.gram_events
     state.gram_events = None
-    gram_ms = sum(a.elapsed_time(b) for a, b in events) / max(len(events), 1)
+    # the Gram launches of one step (one, or own-shard + rest when N > 1), averaged over steps
+    gram_ms = sum(a.elapsed_time(b) for a, b in events) / max(args.steps, 1)
     tdev = dev if backend == "nccl" else "cpu"
     t = torch.tensor([elapsed, gram_ms], dtype=torch.float64, device=tdev)
     if world > 1:
@@ -345,7 +367,8 @@ def main():
         try:
             tr = json.load(open(tpath)).get(f"config{args.config}")
             if tr and world == 1:
-                traffic = tr.get("gram_rowsum_bytes_per_launch")
+                traffic = tr.get("gram_rowsum_split_bytes_per_launch" if state.gram == "split"
+                                 else "gram_rowsum_bytes_per_launch")
         except Exception:
             traffic = None
 
@@ -361,7 +384,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32" if state.gram == "f32" else "f32 (fp16-split MFMA, fp32 accumulate)",
         "data": "synthetic (GPU-generated, fixed seeds per 65,536-row chunk); forest synthetic (seed 1)",
         "config": {"workload": cfg["workload"], "pool_rows": n, "features": d, "trees": cfg["trees"],
                    "depth": cfg["depth"], "k": k, "excluded": N_EXCLUDED, "rows_scored": n_scored,
@@ -373,11 +396,7 @@ def main():
                        "note": "density via the exact O(N*D) identity sum_j<u_i,u_j> = <u_i, sum_j u_j> "
                                "(canonical fp64, same selection); HBM-bound, not the MFMA path"}
                       if sep_ms else None),
-        "roofline": {"bound": "mfma", "kernel": "dal_gram_rowsum (v_mfma_f32_32x32x2_f32)",
-                     "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic,
-                     "launch_ms": gram_ms, "launch_ms_max_over_ranks": gram_ms_max,
-                     "algorithmic_flops_per_launch": flops},
+        "roofline": gram_roofline(state.gram, achieved, traffic, gram_ms, gram_ms_max, flops),
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -78,8 +78,9 @@ class PoolState:
     """
 
     def __init__(self, pool, excluded=None, device=None, row_base: int = 0, n_total=None,
-                 n_pad=None):
+                 n_pad=None, gram: str = None):
         torch = _torch()
+        self.gram = _gram_kind(gram)
         dev = _require_cuda(device)
         lib = _lib.load()
         if isinstance(pool, torch.Tensor):
@@ -102,6 +103,7 @@ class PoolState:
         self.set_excluded(excluded)
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self._u = None
+        self._split = None
         self._norm64 = None
         self._density = None
         self._colsum_partials = None
@@ -112,7 +114,7 @@ class PoolState:
     def clear_caches(self):
         """Drop normalised rows, density and column sums (forces a cold step)."""
         self._u = self._norm64 = self._density = self._colsum = self._colsum_partials = None
-        self._density_exact = None
+        self._split = self._density_exact = None
 
     # ------------------------------------------------------------- caches
     def set_excluded(self, excluded):
@@ -128,7 +130,7 @@ class PoolState:
         if local.size:
             self.flags[torch.from_numpy(local).to(self.device)] = DAL_ROW_EXCLUDED
         self._u = self._norm64 = self._density = self._colsum = self._colsum_partials = None
-        self._density_exact = None
+        self._split = self._density_exact = None
 
     def n_excluded_global(self) -> int:
         return int(self.excluded.size)
@@ -147,6 +149,20 @@ class PoolState:
                  self.n_pad, self.d_pad, _ptr(self._u), _ptr(self._norm64), _ptr(self.status),
                  _stream(self.device))
         return self._u, self._norm64
+
+    def gram_operand(self):
+        """The density GEMM's operand for this shard's rows: the fp32 unit rows
+        (gram "f32") or their two-term fp16 split [n_pad, 2*d_pad] (gram
+        "split", dal_split_f16).  All-gathered as is in the multi-GPU path."""
+        u, _ = self.normalized()
+        if self.gram == "f32":
+            return u
+        if self._split is None:
+            torch = _torch()
+            self._split = torch.empty((self.n_pad, 2 * self.d_pad), dtype=torch.int16, device=self.device)
+            call("dal_split_f16", _ptr(u), self.n_pad, self.d_pad, self.d_pad, _ptr(self._split),
+                 _stream(self.device))
+        return self._split
 
     def colsum_partials(self):
         """Canonical fp64 column-sum partials of this shard ([chunks, d])."""
@@ -176,23 +192,36 @@ class PoolState:
         against every column of ``u_cols`` (default: this pool)."""
         if self._density is None or u_cols is not None:
             torch = _torch()
-            u, _ = self.normalized()
+            op = self.gram_operand()
             acc = torch.zeros(self.n_pad, dtype=torch.int64, device=self.device)
-            cols = u if u_cols is None else u_cols
+            cols = op if u_cols is None else u_cols
             ncp = self.n_pad if n_cols_pad is None else int(n_cols_pad)
-            ev = None
-            if self.gram_events is not None:
-                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                ev[0].record()
-            call("dal_gram_rowsum", _ptr(u), self.n_pad, _ptr(cols), ncp, self.d_pad, self.d_pad,
-                 _ptr(acc), 0, _stream(self.device))
-            if ev is not None:
-                ev[1].record()
-                self.gram_events.append(ev)
+            self.gram_accumulate(acc, cols, ncp)
             if u_cols is not None:
                 return acc
             self._density = acc
         return self._density
+
+    def gram_accumulate(self, acc, cols, n_cols_pad: int, grid_blocks: int = 0):
+        """acc += fixed-point row sums of this shard's rows against the first
+        ``n_cols_pad`` (a multiple of 512) rows of ``cols`` (a Gram operand of
+        the pool's kind).  Exact: any column split adds up to the same bits."""
+        torch = _torch()
+        op = self.gram_operand()
+        ev = None
+        if self.gram_events is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        if self.gram == "f32":
+            call("dal_gram_rowsum", _ptr(op), self.n_pad, _ptr(cols), int(n_cols_pad), self.d_pad,
+                 self.d_pad, _ptr(acc), int(grid_blocks), _stream(self.device))
+        else:
+            call("dal_gram_rowsum_split", _ptr(op), self.n_pad, _ptr(cols), int(n_cols_pad),
+                 self.d_pad, _ptr(acc), int(grid_blocks), _stream(self.device))
+        if ev is not None:
+            ev[1].record()
+            self.gram_events.append(ev)
+        return acc
 
     def set_density_fixed(self, acc):
         self._density = acc
@@ -251,6 +280,22 @@ class PoolState:
                              "(the reference would propagate NaN into every density)")
         if st & DAL_FLAG_CAND_OVERFLOW:
             raise _lib.DalError("density re-rank candidate set exceeded DAL_SORT_CAP_PAYLOAD")
+
+
+GRAM_KINDS = ("split", "f32")
+
+
+def _gram_kind(gram) -> str:
+    """Density GEMM kernel: "split" (default; fp16 MFMA, two-term split, three
+    products) or "f32" (fp32 MFMA).  DAL_GRAM in the environment overrides the
+    default.  Both are within their rigorous bound of the canonical density and
+    give the same (bit-exact) selection."""
+    import os
+
+    g = gram if gram is not None else os.environ.get("DAL_GRAM", "split")
+    if g not in GRAM_KINDS:
+        raise ValueError(f"gram must be one of {GRAM_KINDS}, not {g!r}")
+    return g
 
 
 def _as_index(idx, device):
@@ -320,9 +365,13 @@ def topk_keys(keys, k: int, idx_base: int = 0):
 
 
 def density_error(state: PoolState) -> float:
-    """Bound on |d_gemm - d_canonical| (rigorous; dal_density_error_bound)."""
-    n_cols = state.n_total - state.n_excluded_global()
-    return float(_lib.load().dal_density_error_bound(max(n_cols, 1)))
+    """Bound on |d_gemm - d_canonical| (rigorous; dal_density_error_bound or
+    dal_density_error_bound_split, by the pool's Gram kernel)."""
+    n_cols = max(state.n_total - state.n_excluded_global(), 1)
+    lib = _lib.load()
+    if state.gram == "f32":
+        return float(lib.dal_density_error_bound(n_cols))
+    return float(lib.dal_density_error_bound_split(n_cols))
 
 
 def candidate_cap(n: int, k: int) -> int:

@@ -10,9 +10,12 @@ multiple of DAL_ROW_GRANULE, identical on every rank; the last rank holds the
 remainder).  Two exchanges, both all-gathers over ``torch.distributed``
 (backend "nccl" = RCCL on ROCm):
 
-  1. the normalised shards u_r (fp32, [shard, d_pad]) and the canonical fp64
-     column-sum partials -> every rank holds U (the density needs every
-     column) -- replaces the BlockMatrix shuffle;
+  1. the shards' Gram operands (fp16 split [shard, 2*d_pad] by default, or
+     fp32 unit rows) and the canonical fp64 column-sum partials -> every rank
+     holds U (the density needs every column) -- replaces the BlockMatrix
+     shuffle.  The operand all-gather runs asynchronously on RCCL's stream
+     while each rank multiplies its rows by its OWN shard's columns (CUs
+     reserved for RCCL), then by the rest (ShardedSelector.exchange_density);
   2. each rank's exact local top-k (key, index, score) -> an identical
      deterministic merge on every rank -- replaces sortBy + take.
 
@@ -32,6 +35,10 @@ import numpy as np
 
 from . import _lib
 from ._lib import DAL_ASCENDING, DAL_CANON_CHUNK, DAL_DESCENDING, DAL_KEY_NONE, DAL_ROW_GRANULE
+
+# CUs left to RCCL while the own-shard Gram launch runs beside the all-gather
+# (a persistent Gram grid would otherwise hold every CU's registers and LDS).
+RCCL_RESERVED_CUS = 8
 
 
 def shard_rows(n_total: int, world: int) -> int:
@@ -78,7 +85,8 @@ def _as_i64(u: int) -> int:
 class ShardedSelector:
     """One rank's shard of the pool and its share of a selection step."""
 
-    def __init__(self, x_local, n_total: int, rank: int, world: int, excluded=None, device=None):
+    def __init__(self, x_local, n_total: int, rank: int, world: int, excluded=None, device=None,
+                 gram: str = None):
         from .engine import PoolState
 
         self.n_total, self.rank, self.world = int(n_total), int(rank), int(world)
@@ -86,21 +94,45 @@ class ShardedSelector:
         if int(x_local.shape[0]) != self.hi - self.lo:
             raise ValueError(f"rank {rank}: expected {self.hi - self.lo} rows, got {x_local.shape[0]}")
         self.state = PoolState(x_local, excluded=excluded, device=device, row_base=self.lo,
-                               n_total=self.n_total, n_pad=self.shard)
+                               n_total=self.n_total, n_pad=self.shard, gram=gram)
         self._density = None
 
     # ---- phase A: local normalisation + canonical partials ------------
     def prep(self):
-        """(u_local [shard, d_pad] fp32, partials [shard/256, d] fp64)."""
+        """(Gram operand of the shard -- fp32 unit rows [shard, d_pad] or their
+        fp16 split [shard, 2*d_pad] --, partials [shard/256, d] fp64)."""
         torch = __import__("torch")
         st = self.state
-        u, _ = st.normalized()
+        u = st.gram_operand()
         parts = torch.zeros((self.shard // DAL_CANON_CHUNK, st.d), dtype=torch.float64,
                             device=st.device)
         if st.n:
             p = st.colsum_partials()
             parts[: p.shape[0]] = p
         return u, parts
+
+    # ---- exchange 1 overlapped with the own-shard columns ---------------
+    def exchange_density(self, comm, u_local, reserve_cus: int = RCCL_RESERVED_CUS):
+        """All-gather the shards' Gram operands while this rank's rows run
+        against its OWN columns (the operand it already holds), then against
+        the other shards' columns; returns the gathered operand.  Every column
+        range is a whole number of shards (multiples of 512), so the exact
+        fixed-point sum is the same bits as one call over all columns.  The
+        own-shard launch leaves ``reserve_cus`` CUs free for RCCL's kernels."""
+        torch = __import__("torch")
+        st = self.state
+        u_full, work = comm.all_gather_start(u_local)
+        acc = torch.zeros(st.n_pad, dtype=torch.int64, device=st.device)
+        if st.n:
+            grid = max(1, 2 * (_device_cus(st.device) - reserve_cus)) if work is not None else 0
+            st.gram_accumulate(acc, u_local, self.shard, grid_blocks=grid)
+        comm.wait(work)
+        if st.n:
+            for c0, c1 in other_column_ranges(self.rank, self.world, self.shard):
+                st.gram_accumulate(acc, u_full[c0:c1], c1 - c0)
+        self._density = acc
+        st.set_density_fixed(acc)
+        return u_full
 
     # ---- phase B: density against all columns + local exact top-k ------
     def local_density(self, u_full):
@@ -152,6 +184,22 @@ class ShardedSelector:
         return LocalTopk(keys, idx, scores)
 
 
+def other_column_ranges(rank: int, world: int, shard: int):
+    """Column ranges [c0, c1) of the gathered operand outside this rank's own
+    shard (at most two contiguous ranges: before and after it)."""
+    out = []
+    if rank > 0:
+        out.append((0, rank * shard))
+    if rank < world - 1:
+        out.append(((rank + 1) * shard, world * shard))
+    return out
+
+
+def _device_cus(device) -> int:
+    torch = __import__("torch")
+    return int(torch.cuda.get_device_properties(device).multi_processor_count)
+
+
 def hip_sort_positions(keys, pos, k):
     from .engine import sort_pairs
 
@@ -170,13 +218,28 @@ class TorchComm:
         self.world = dist.get_world_size(group)
 
     def all_gather(self, t):
+        out, work = self.all_gather_start(t)
+        self.wait(work)
+        return out
+
+    def all_gather_start(self, t):
+        """Start an all-gather; returns (output, work handle or None).  With
+        RCCL it runs asynchronously on the communicator's stream."""
         torch = __import__("torch")
         if t.is_cuda and self.dist.get_backend(self.group) == "gloo":
             # rehearsal path (several ranks sharing one GPU): stage through the host
-            return self.all_gather(t.cpu()).to(t.device)
+            return self.all_gather(t.cpu()).to(t.device), None
         out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        if t.is_cuda:
+            work = self.dist.all_gather_into_tensor(out, t.contiguous(), group=self.group, async_op=True)
+            return out, work
         self.dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
-        return out
+        return out, None
+
+    def wait(self, work):
+        """Order the current stream after the collective (no host block)."""
+        if work is not None:
+            work.wait()
 
 
 def select(sel: ShardedSelector, comm, unlabeled_idx, forest, k: int, mode: str = "dw",
@@ -186,7 +249,7 @@ def select(sel: ShardedSelector, comm, unlabeled_idx, forest, k: int, mode: str 
     identical on every rank."""
     u_local, parts = sel.prep()
     need_u = mode == "dw" and density_mode == "gram" and sel._density is None
-    u_full = comm.all_gather(u_local) if need_u else None
+    u_full = sel.exchange_density(comm, u_local) if need_u else None
     parts_full = comm.all_gather(parts) if mode == "dw" else None
     top = sel.local_select(u_full, parts_full, unlabeled_idx, forest, k, mode, strategy, beta,
                            density_mode)

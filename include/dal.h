@@ -129,6 +129,26 @@ int dal_gram_rowsum(const float* u_rows, int64_t n_rows_pad, const float* u_cols
                     int64_t n_cols_pad, int64_t d_pad, int64_t ld, int64_t* acc,
                     int grid_blocks, dal_stream_t stream);
 
+/* ---- (a2-a4) the same row-sum on fp16 MFMA with a two-term split ------
+ * Same contract and replaced reference lines as dal_gram_rowsum, at the fp16
+ * matrix-core rate.  dal_split_f16 writes each normalised fp32 row u (from
+ * dal_normalize_rows, ld >= d_pad) as h = fp16(u), l = fp16((u - h) * 2^12)
+ * in the layout [n_pad][d_pad / KS][KS hi halves | KS lo halves], KS = 32 if
+ * d_pad == 32 else 64 (dal_split_f16_halves(n_pad, d_pad) halves in all);
+ * dal_gram_rowsum_split then accumulates acc[i] += round(sum_j <u_i,u_j> * 2^32)
+ * from three v_mfma_f32_32x32x16_f16 products (h.h, h.l, l.h) per 16
+ * features, folded exactly per 256-column group (bit-identical for any grid,
+ * column split or GPU count).  Rigorous bound: dal_density_error_bound_split.
+ * n_rows_pad % 256 == 0, n_cols_pad % 512 == 0; grid_blocks <= 0 selects
+ * two blocks per CU. */
+int64_t dal_split_f16_halves(int64_t n_pad, int64_t d_pad);
+int dal_split_f16(const float* u, int64_t n_pad, int64_t d_pad, int64_t ld, uint16_t* out,
+                  dal_stream_t stream);
+int dal_gram_rowsum_split(const uint16_t* rows, int64_t n_rows_pad, const uint16_t* cols,
+                          int64_t n_cols_pad, int64_t d_pad, int64_t* acc, int grid_blocks,
+                          dal_stream_t stream);
+double dal_density_error_bound_split(int64_t n_cols);
+
 /* ---- (a5-a10) forest votes + uncertainty / density-weighted score ------
  * Replaces uncertainty_sampling.py:88-98 / density_weighting.py:136-167:
  * T x DecisionTreeModel.predict, groupByKey vote sum, the LUT score and the

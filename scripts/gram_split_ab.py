@@ -1,0 +1,68 @@
+"""A/B of the fp32-MFMA Gram row-sum (dal_gram_rowsum) against the split-fp16
+one (dal_gram_rowsum_split): time, agreement with the canonical fp64 density
+(separable form), the rigorous bounds, and grid-size invariance of the split
+kernel.  usage: python scripts/gram_split_ab.py [rounds]"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                "distributed-active-learning_amd"))
+from dal import _lib  # noqa: E402
+from dal.engine import PoolState, _ptr, _stream  # noqa: E402
+
+rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+shapes = [(s.split("x")) for s in os.environ.get("AB_SHAPES", "100000x64,200000x30,500000x256").split(",")]
+dev = torch.device("cuda:0")
+lib = _lib.load()
+for n, d in [(int(a), int(b)) for a, b in shapes]:
+    g = torch.Generator(device=dev)
+    g.manual_seed(n)
+    x = torch.rand((n, d), generator=g, device=dev).clamp_(min=1e-7)
+    st = PoolState(x, excluded=np.arange(10), device=dev)
+    u, _ = st.normalized()
+    sp = torch.empty(int(lib.dal_split_f16_halves(st.n_pad, st.d_pad)), dtype=torch.int16, device=dev)
+    _lib.call("dal_split_f16", _ptr(u), st.n_pad, st.d_pad, st.d_pad, _ptr(sp), _stream(dev))
+    flops = 2.0 * (n - 10) * (n - 10) * d
+    t = {"f32": [], "split": []}
+    accs = {}
+
+    def run(kind, grid=0):
+        acc = torch.zeros(st.n_pad, dtype=torch.int64, device=dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        if kind == "f32":
+            _lib.call("dal_gram_rowsum", _ptr(u), st.n_pad, _ptr(u), st.n_pad, st.d_pad, st.d_pad,
+                      _ptr(acc), grid, _stream(dev))
+        else:
+            _lib.call("dal_gram_rowsum_split", _ptr(sp), st.n_pad, _ptr(sp), st.n_pad, st.d_pad,
+                      _ptr(acc), grid, _stream(dev))
+        e1.record()
+        torch.cuda.synchronize()
+        return acc, e0.elapsed_time(e1)
+
+    for r in range(rounds + 1):
+        for kind in ("f32", "split"):
+            acc, ms = run(kind)
+            if r:
+                t[kind].append(ms)
+            accs[kind] = acc
+    canon = st.density_exact()[10:n]
+    for kind in ("f32", "split"):
+        dk = accs[kind][10:n].to(torch.float64) / 2.0**32
+        err = (dk - canon).abs()
+        bound = (lib.dal_density_error_bound if kind == "f32" else lib.dal_density_error_bound_split)(n - 10)
+        ms = float(np.median(t[kind]))
+        print(f"n={n} d={d} {kind:5s} median {ms:8.3f} ms  {flops / ms / 1e9:7.1f} TF/s "
+              f"({100 * flops / ms / 1e9 / 157.3:5.1f}% of fp32 peak)  max|err| {float(err.max()):.3e} "
+              f"max rel {float((err / canon.abs()).max()):.3e}  bound {bound:.3e}  "
+              f"within={bool(float(err.max()) <= bound)}", flush=True)
+    a2, _ = run("split", grid=37)
+    a3, _ = run("split", grid=1000)
+    print(f"   split grid-invariant: {torch.equal(a2, accs['split']) and torch.equal(a3, accs['split'])}",
+          flush=True)
+    del sp, st, u, x
+    torch.cuda.empty_cache()

@@ -4,8 +4,9 @@ committed golden fixtures.  Needs an MI355X: ``pytest -m gpu``.
 Bars (DESIGN.md "Parity"):
   * votes, LUT scores, selected indices (+ their order), canonical selected
     scores: bit-exact;
-  * GEMM density: within the rigorous bound dal_density_error_bound(N) and
-    1e-5 relative of the fp64 oracle;
+  * GEMM density (both kernels: fp16 split, fp32): within its rigorous bound
+    (dal_density_error_bound_split / dal_density_error_bound) and 1e-5
+    relative of the fp64 oracle;
   * fp32 cosine entries: 2e-6 absolute.
 """
 import numpy as np
@@ -74,26 +75,76 @@ def test_canonical_colsum_bit_exact(cuda, n, d):
     assert np.array_equal(_np(st.colsum()), ref)
 
 
+@pytest.mark.parametrize("gram", ["split", "f32"])
 @pytest.mark.parametrize("n,d,dist", [(4096, 256, "uniform"), (5000, 64, "uniform"),
                                       (3000, 30, "normal"), (2100, 128, "uniform"),
                                       (1200, 500, "uniform")])
-def test_gram_density_within_bound(cuda, n, d, dist):
+def test_gram_density_within_bound(cuda, n, d, dist, gram):
     from dal import _lib
     from dal.engine import PoolState
 
     X = O.synthetic_pool(n, d, seed=7, dist=dist)
     E = list(range(10))
-    st = PoolState(X, excluded=E, device=cuda)
+    st = PoolState(X, excluded=E, device=cuda, gram=gram)
     got = _np(st.density())
     ref = O.density_canonical(X, E)
     assert np.array_equal(np.isnan(got), np.isnan(ref))
     ok = ~np.isnan(ref)
     err = np.abs(got[ok] - ref[ok])
-    bound = _lib.load().dal_density_error_bound(n - len(E))
+    lib = _lib.load()
+    bound = (lib.dal_density_error_bound if gram == "f32" else lib.dal_density_error_bound_split)(n - len(E))
     assert err.max() <= bound
     # accuracy bar of the north star: 1e-5 relative (signed data: relative to sum |S_ij|)
     scale = np.abs(O.l2_normalize(X) @ O.l2_normalize(X)[ok].T).sum(axis=1)[ok]
     assert (err / scale).max() <= DENSITY_RTOL
+
+
+@pytest.mark.parametrize("d", [30, 64, 200])
+def test_split_operand_bit_exact(cuda, d):
+    """dal_split_f16: h = fp16(u), l = fp16((u - h) * 2^12) (RNE), layout
+    [n_pad][d_pad/KS][KS hi | KS lo]."""
+    from dal.engine import PoolState
+
+    X = O.synthetic_pool(1000, d, seed=d, dist="normal")
+    st = PoolState(X, excluded=[5], device=cuda, gram="split")
+    u = _np(st.normalized()[0])
+    sp = _np(st.gram_operand()).view(np.float16)
+    d_pad = st.d_pad
+    ks = 32 if d_pad == 32 else 64
+    h = u.astype(np.float16)
+    l = ((u - h.astype(np.float32)) * np.float32(4096)).astype(np.float16)
+    ref = np.empty((st.n_pad, 2 * d_pad), dtype=np.float16)
+    for s0 in range(0, d_pad, ks):
+        ref[:, 2 * s0:2 * s0 + ks] = h[:, s0:s0 + ks]
+        ref[:, 2 * s0 + ks:2 * s0 + 2 * ks] = l[:, s0:s0 + ks]
+    assert np.array_equal(sp.view(np.uint16), ref.view(np.uint16))
+    # reconstruction error of the split: |u - h - l 2^-12| <= 2^-22 |u| + 2^-37
+    rec = h.astype(np.float64) + l.astype(np.float64) * 2.0**-12
+    assert (np.abs(rec - u) <= 2.0**-22 * np.abs(u) + 2.0**-37).all()
+
+
+@pytest.mark.parametrize("gram", ["split", "f32"])
+@pytest.mark.parametrize("d", [32, 64, 256])
+def test_gram_kernels_deterministic_across_grids_and_column_splits(cuda, gram, d):
+    """int64 fixed-point accumulation: identical bits for any grid/unit split
+    and for any split of the columns into 512-multiples (multi-GPU contract)."""
+    import torch
+    from dal.engine import PoolState
+
+    X = O.synthetic_pool(5000, d, seed=3)
+    st = PoolState(X, device=cuda, gram=gram)
+    op = st.gram_operand()
+    outs = []
+    for grid in (0, 1, 7, 64, 300, 1000):
+        acc = torch.zeros(st.n_pad, dtype=torch.int64, device=cuda)
+        st.gram_accumulate(acc, op, st.n_pad, grid_blocks=grid)
+        outs.append(_np(acc))
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0])
+    part = torch.zeros(st.n_pad, dtype=torch.int64, device=cuda)
+    for c0, c1 in ((2048, 4096), (0, 1024), (4096, st.n_pad), (1024, 2048)):
+        st.gram_accumulate(part, op[c0:], c1 - c0)
+    assert np.array_equal(_np(part), outs[0])
 
 
 def test_gram_density_deterministic_across_grids(cuda):
@@ -370,8 +421,10 @@ def test_cosine_entries_and_column_similarities(cuda):
 
 
 # ------------------------------------------- config-2 scale properties ----
-def test_config2_scale_selection_bit_exact(cuda):
-    """100k x 64, T=10, k=100 (BASELINE config 2) against the oracle."""
+@pytest.mark.parametrize("gram", ["split", "f32"])
+def test_config2_scale_selection_bit_exact(cuda, gram):
+    """100k x 64, T=10, k=100 (BASELINE config 2) against the oracle, with
+    either density GEMM kernel."""
     from dal import density_weighting as dw
     from dal import uncertainty_sampling as us
     from dal.engine import PoolState
@@ -382,7 +435,7 @@ def test_config2_scale_selection_bit_exact(cuda):
     F = Forest.synthetic(10, 4, 64, seed=1)
     E = np.arange(10)
     unl = np.arange(10, 100_000)
-    st = PoolState(X, excluded=E, device=cuda)
+    st = PoolState(X, excluded=E, device=cuda, gram=gram)
     sel = dw.select(st, unl, F, 100)
     ref_sc, ref_idx, ref_ss = O.density_select(X, unl, of, 100, 1.0, E)
     assert np.array_equal(_np(sel.indices), ref_idx)
@@ -400,7 +453,7 @@ def test_config2_scale_selection_bit_exact(cuda):
 
 # ------------------------------------------------ multi-shard (1 GPU) -----
 @pytest.mark.parametrize("world", [2, 3, 4])
-@pytest.mark.parametrize("mode", ["dw", "us", "dw-separable"])
+@pytest.mark.parametrize("mode", ["dw", "us", "dw-separable", "dw-f32"])
 def test_sharded_emulation_bit_identical(cuda, world, mode):
     """P row shards (emulated in one process, all-gathers as concatenation)
     give the same density bits and the same selection as P = 1 and the oracle."""
@@ -415,14 +468,15 @@ def test_sharded_emulation_bit_identical(cuda, world, mode):
     F = Forest.synthetic(10, 4, d, seed=1)
     E = np.arange(10)
     unl = np.arange(10, n)
+    gram = "f32" if mode == "dw-f32" else "split"
     sels = []
     for r in range(world):
         lo, hi, _ = parallel.shard_range(n, world, r)
-        sels.append(parallel.ShardedSelector(X[lo:hi], n, r, world, excluded=E, device=cuda))
+        sels.append(parallel.ShardedSelector(X[lo:hi], n, r, world, excluded=E, device=cuda, gram=gram))
     dmode = "separable" if mode == "dw-separable" else "gram"
     mode = "dw" if mode.startswith("dw") else mode
     idx, sc = parallel.emulate(sels, unl, F, 50, mode=mode, density_mode=dmode)
-    st = PoolState(X, excluded=E, device=cuda)
+    st = PoolState(X, excluded=E, device=cuda, gram=gram)
     if mode == "dw" and dmode == "separable":
         ref = density_step(st, unl, F, 50, mode="separable")
         _, o_idx, o_sc = O.density_select(X, unl, of, 50, 1.0, E)

@@ -43,6 +43,9 @@ def test_host_helpers():
     assert lib.dal_status_string(-2).decode().startswith("shape")
     b = lib.dal_density_error_bound(100000)
     assert 1.0 < b < 10.0  # ~3.1e-5 * N
+    bs = lib.dal_density_error_bound_split(100000)
+    assert b < bs < 20.0  # ~1.25e-4 * N (conservative MFMA accumulation model)
+    assert lib.dal_split_f16_halves(512, 64) == 512 * 128
     assert lib.dal_topk_workspace_bytes(1 << 21, 1000) > 0
 
 
@@ -57,6 +60,12 @@ def test_host_argument_validation_without_gpu():
     assert lib.dal_gram_rowsum(p, 100, p, 512, 64, 64, p, 0, None) == -2
     assert lib.dal_gram_rowsum(p, 256, p, 500, 64, 64, p, 0, None) == -2
     assert lib.dal_gram_rowsum(p, 256, p, 512, 48, 64, p, 0, None) == -2
+    assert lib.dal_gram_rowsum_split(None, 256, None, 512, 64, None, 0, None) == -1
+    assert lib.dal_gram_rowsum_split(p, 100, p, 512, 64, p, 0, None) == -2
+    assert lib.dal_gram_rowsum_split(p, 256, p, 500, 64, p, 0, None) == -2
+    assert lib.dal_gram_rowsum_split(p, 256, p, 512, 48, p, 0, None) == -2
+    assert lib.dal_split_f16(None, 512, 64, 64, None, None) == -1
+    assert lib.dal_split_f16(p, 500, 64, 64, p, None) == -2
     assert lib.dal_topk(p, 10, 11, 0, p, 1 << 20, p, p, None) == -2
     assert lib.dal_topk(p, 100000, 9000, 0, p, 1 << 30, p, p, None) == -5
     assert lib.dal_forest_score(p, 10, 4, 4, p, p, 3, 17, p, None, 0, 0.0, None, 1.0, 0, p, p, p,

@@ -54,6 +54,9 @@ class OracleShard(parallel.ShardedSelector):
                 parts[c] = torch.from_numpy(acc)
         return u, parts
 
+    def exchange_density(self, comm, u_local):
+        return comm.all_gather(u_local)
+
     def local_select(self, u_full, parts_full, unl, forest, k, mode="dw", strategy="least_confidence",
                      beta=1.0, density_mode="gram"):
         keys = torch.full((k,), parallel._as_i64(0xFFFFFFFFFFFFFFFF), dtype=torch.int64)
@@ -153,3 +156,15 @@ def test_shard_ranges_cover_pool():
                 rows.append((lo, hi))
             assert rows[0][0] == 0 and rows[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(rows, rows[1:]))
+
+
+def test_other_column_ranges_cover_the_rest():
+    for world in (1, 2, 3, 8):
+        shard = 1024
+        for rank in range(world):
+            cols = set()
+            for c0, c1 in parallel.other_column_ranges(rank, world, shard):
+                assert c0 % 512 == 0 and c1 % 512 == 0 and c0 < c1
+                cols.update(range(c0, c1))
+            own = set(range(rank * shard, (rank + 1) * shard))
+            assert cols.isdisjoint(own) and cols | own == set(range(world * shard))
