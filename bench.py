@@ -129,7 +129,7 @@ def gram_roofline(gram, achieved, traffic, gram_ms, gram_ms_max, flops):
                 "launch_ms_max_over_ranks": gram_ms_max, "algorithmic_flops_per_launch": flops}
     peak = F16_MFMA_PEAK_TFLOPS / 3.0
     return {"bound": "mfma",
-            "kernel": "dal_gram_rowsum_split (3 x v_mfma_f32_32x32x16_f16 per 16 features: h.h, h.l, l.h)",
+            "kernel": "dal_gram_rowsum_split (3 x v_mfma_f32_16x16x32_f16 per 32 features: h.h, h.l, l.h)",
             "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
             "peak_note": "dense fp16 MFMA peak 2500 TF/s / 3 products per algorithmic product",
             "executed_fp16_tflops": 3.0 * achieved, "vs_fp32_mfma_peak": achieved / FP32_MFMA_PEAK_TFLOPS,

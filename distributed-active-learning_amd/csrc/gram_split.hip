@@ -37,6 +37,8 @@
 //  * Persistent grid of 2 blocks per CU over (row block, column chunk) units
 //    in equal contiguous ranges.
 
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "common.hpp"
@@ -53,40 +55,80 @@ constexpr int kSpRows = 256;       // rows per block (64 per wave = 2 MFMA row t
 constexpr int kSpStage = 32768;    // bytes per LDS stage
 constexpr int kSpFoldCols = 256;   // columns per exact fold group
 
-template <int KS>
+template <int KS, int MT>
 struct SpCfg {
   static constexpr int ROWB = KS * 4;                   // bytes per column row: KS hi + KS lo halves
   static constexpr int SLOTS = ROWB / 16;               // 16-B slots per column row
   static constexpr int HI = KS / 8;                     // slots of the hi part
   static constexpr int SC = kSpStage / ROWB;            // columns per stage
-  static constexpr int NCT = SC / 32;                   // MFMA column tiles per stage
-  static constexpr int NKS = KS / 16;                   // MFMA k-steps per slice
   static constexpr int FS = kSpFoldCols / SC;           // stages per fold group (1 or 2)
   static constexpr int SWZ = (SLOTS < 16 ? SLOTS : 16) - 1;
   static constexpr int PIECES = kSpStage / (4 * 1024);  // 1-KiB DMA pieces per wave per stage
   static constexpr int F4 = kSpStage / 16;
+  // MFMA geometry: MT x MT output tiles (32: v_mfma_f32_32x32x16_f16,
+  // 16: v_mfma_f32_16x16x32_f16)
+  static constexpr int RT = 64 / MT;                    // row tiles per wave
+  static constexpr int LG = 64 / MT;                    // lane groups (K sub-blocks of 8)
+  static constexpr int KSTEP = 8 * LG;                  // features per MFMA
+  static constexpr int NKS = KS / KSTEP;                // k-steps per slice
+  static constexpr int NCT = SC / MT;                   // column tiles per stage
+  static constexpr int NV = MT * MT / 64;               // accumulator values per lane
   static_assert(FS == 1 || FS == 2, "a stage pair must hold whole fold groups");
+  static_assert(NKS >= 1, "slice narrower than one k-step");
+};
+
+template <int MT>
+struct SpAcc;
+template <>
+struct SpAcc<32> {
+  typedef float type __attribute__((ext_vector_type(16)));
+  static __device__ __forceinline__ type mfma(f16x8 a, f16x8 b, type c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+  // row (within the tile) of accumulator value r of lane group q
+  static __device__ __forceinline__ int row(int r, int q) { return (r & 3) + 8 * (r >> 2) + 4 * q; }
+};
+template <>
+struct SpAcc<16> {
+  typedef float type __attribute__((ext_vector_type(4)));
+  static __device__ __forceinline__ type mfma(f16x8 a, f16x8 b, type c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ int row(int r, int q) { return 4 * q + r; }
 };
 
 __device__ __forceinline__ double fold_fixed(float v) {
   return static_cast<double>(__builtin_rintf(v * 4294967296.0f));
 }
 
-template <int KS>
+template <int KS, int MT>
 __global__ __launch_bounds__(kSpThreads, 2) void gram_split_kernel(
     const uint16_t* __restrict__ urows, const uint16_t* __restrict__ ucols, int64_t ldh,
-    int slice_off, int64_t n_pairs, int chunk_pairs, int64_t n_chunks, int64_t n_units,
-    unsigned long long* __restrict__ acc_out) {
-  using C = SpCfg<KS>;
+    int slice_off, int64_t n_pairs, int chunk_pairs, int64_t n_chunks, int64_t n_row_blocks,
+    int sync_sweep, unsigned long long* __restrict__ acc_out) {
+  using C = SpCfg<KS, MT>;
+  using A = SpAcc<MT>;
+  using acc_t = typename A::type;
   __shared__ __attribute__((aligned(16))) float4 lds[2 * C::F4];
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
-  const int li = lane & 31, lh = lane >> 5;
+  const int li = lane % MT, lq = lane / MT;
 
+  // Work units = (row block, column chunk).  sync_sweep: units in chunk-major
+  // order dealt round-robin (block g takes g, g+G, ...), so at any moment every
+  // block of every XCD reads the same one or two column chunks in lockstep and
+  // each B stage is fetched into an XCD's L2 about once; the A fragments are
+  // reloaded per unit.  Otherwise: equal contiguous ranges of row-major units
+  // (A reloaded only when a range crosses into the next row block).
   const int64_t G = gridDim.x, g = blockIdx.x;
-  const int64_t u_begin = (g * n_units) / G, u_end = ((g + 1) * n_units) / G;
+  const int64_t n_units = n_row_blocks * n_chunks;
+  const int64_t u_begin = sync_sweep ? g : (g * n_units) / G;
+  const int64_t u_end = sync_sweep ? n_units : ((g + 1) * n_units) / G;
+  const int64_t u_step = sync_sweep ? G : 1;
   if (u_begin >= u_end) return;
+  auto unit_rb = [&](int64_t u) { return sync_sweep ? u % n_row_blocks : u / n_chunks; };
+  auto unit_pair0 = [&](int64_t u) { return (sync_sweep ? u / n_row_blocks : u % n_chunks) * chunk_pairs; };
 
   // per-piece source offsets (stage-relative, swizzled) and the wave's LDS base
   unsigned voff[C::PIECES];
@@ -117,38 +159,42 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_split_kernel(
   };
 
   int64_t unit = u_begin;
-  int64_t rb = unit / n_chunks;
-  int64_t pr = (unit % n_chunks) * chunk_pairs;
+  int64_t rb = unit_rb(unit);
+  int64_t pr = unit_pair0(unit);
   int64_t pr_end = pr + chunk_pairs < n_pairs ? pr + chunk_pairs : n_pairs;
 
-  f16x8 ah[2][C::NKS], al[2][C::NKS];
+  // resident A fragments: rows rb*256 + wave*64 + rt*MT + li, features of
+  // k-step c and lane group lq = slot c*LG + lq of the hi / lo halves
+  f16x8 ah[C::RT][C::NKS], al[C::RT][C::NKS];
   auto load_a = [&](int64_t rbk) {
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      const int64_t row = rbk * kSpRows + wave * 64 + rt * 32 + li;
+    for (int rt = 0; rt < C::RT; ++rt) {
+      const int64_t row = rbk * kSpRows + wave * 64 + rt * MT + li;
       const uint16_t* src = urows + row * ldh + slice_off;
 #pragma unroll
       for (int c = 0; c < C::NKS; ++c) {
-        ah[rt][c] = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(src + (2 * c + lh) * 8));
-        al[rt][c] = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(src + KS + (2 * c + lh) * 8));
+        ah[rt][c] = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(src + (c * C::LG + lq) * 8));
+        al[rt][c] = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(src + KS + (c * C::LG + lq) * 8));
       }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): A (and any in-flight DMA) landed
   };
 
-  // B-fragment LDS offsets (float4 units) per k-step; column tiles add ct*32*SLOTS
+  // B-fragment LDS offsets (float4 units) per k-step; column tiles add ct*MT*SLOTS
   int boh[C::NKS], bol[C::NKS];
 #pragma unroll
   for (int c = 0; c < C::NKS; ++c) {
-    boh[c] = li * C::SLOTS + ((2 * c + lh) ^ (li & C::SWZ));
-    bol[c] = li * C::SLOTS + ((C::HI + 2 * c + lh) ^ (li & C::SWZ));
+    boh[c] = li * C::SLOTS + ((c * C::LG + lq) ^ (li & C::SWZ));
+    bol[c] = li * C::SLOTS + ((C::HI + c * C::LG + lq) ^ (li & C::SWZ));
   }
 
-  f32x16 m0, m1, x0, x1;
-  double facc[2][16];
+  acc_t m[C::RT], x[C::RT];
+  double facc[C::RT][C::NV];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) facc[0][r] = facc[1][r] = 0.0;
-  const f32x16 zero = {};
+  for (int rt = 0; rt < C::RT; ++rt)
+#pragma unroll
+    for (int r = 0; r < C::NV; ++r) facc[rt][r] = 0.0;
+  const acc_t zero = {};
 
   auto compute = [&](auto firstc, const float4* B) {
     constexpr bool FIRST = decltype(firstc)::value;
@@ -156,52 +202,49 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_split_kernel(
     for (int ct = 0; ct < C::NCT; ++ct) {
 #pragma unroll
       for (int c = 0; c < C::NKS; ++c) {
-        const f16x8 bh = __builtin_bit_cast(f16x8, B[ct * 32 * C::SLOTS + boh[c]]);
-        const f16x8 bl = __builtin_bit_cast(f16x8, B[ct * 32 * C::SLOTS + bol[c]]);
+        const f16x8 bh = __builtin_bit_cast(f16x8, B[ct * MT * C::SLOTS + boh[c]]);
+        const f16x8 bl = __builtin_bit_cast(f16x8, B[ct * MT * C::SLOTS + bol[c]]);
         const bool z = FIRST && ct == 0 && c == 0;
-        m0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[0][c], bh, z ? zero : m0, 0, 0, 0);
-        m1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[1][c], bh, z ? zero : m1, 0, 0, 0);
-        x0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[0][c], bl, z ? zero : x0, 0, 0, 0);
-        x1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[1][c], bl, z ? zero : x1, 0, 0, 0);
-        x0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[0][c], bh, x0, 0, 0, 0);
-        x1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[1][c], bh, x1, 0, 0, 0);
+#pragma unroll
+        for (int rt = 0; rt < C::RT; ++rt) m[rt] = A::mfma(ah[rt][c], bh, z ? zero : m[rt]);
+#pragma unroll
+        for (int rt = 0; rt < C::RT; ++rt) x[rt] = A::mfma(ah[rt][c], bl, z ? zero : x[rt]);
+#pragma unroll
+        for (int rt = 0; rt < C::RT; ++rt) x[rt] = A::mfma(al[rt][c], bh, x[rt]);
       }
     }
   };
   auto fold = [&]() {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      facc[0][r] += fold_fixed(__builtin_fmaf(x0[r], 0x1p-12f, m0[r]));
-      facc[1][r] += fold_fixed(__builtin_fmaf(x1[r], 0x1p-12f, m1[r]));
-    }
+    for (int rt = 0; rt < C::RT; ++rt)
+#pragma unroll
+      for (int r = 0; r < C::NV; ++r) facc[rt][r] += fold_fixed(__builtin_fmaf(x[rt][r], 0x1p-12f, m[rt][r]));
   };
 
   auto finish_unit = [&]() {
-    // exact (integer-valued) fp64 butterfly over the 32 column lanes of each half
+    // exact (integer-valued) fp64 butterfly over the MT column lanes of each group
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
+    for (int rt = 0; rt < C::RT; ++rt) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
+      for (int r = 0; r < C::NV; ++r) {
         double v = facc[rt][r];
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        v += __shfl_xor(v, 4);
-        v += __shfl_xor(v, 8);
-        v += __shfl_xor(v, 16);
+#pragma unroll
+        for (int sh = 1; sh < MT; sh <<= 1) v += __shfl_xor(v, sh);
         facc[rt][r] = v;
       }
     }
+    // lane (li, lq) publishes value li = (rt, r): the wave's 64 rows, one atomic
     double mine = 0.0;
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
+    for (int rt = 0; rt < C::RT; ++rt) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (rt * 16 + r == li) mine = facc[rt][r];
+      for (int r = 0; r < C::NV; ++r) {
+        if (rt * C::NV + r == li) mine = facc[rt][r];
         facc[rt][r] = 0.0;
       }
     }
-    const int r = li & 15;
-    const int64_t row = rb * kSpRows + wave * 64 + (li >> 4) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+    const int rt = li / C::NV, r = li % C::NV;
+    const int64_t row = rb * kSpRows + wave * 64 + rt * MT + A::row(r, lq);
     atomicAdd(acc_out + row, static_cast<unsigned long long>(static_cast<long long>(mine)));
   };
 
@@ -214,8 +257,8 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_split_kernel(
     const bool last_of_unit = (pr + 1 == pr_end);
     int64_t n_unit = unit, n_pr = pr + 1;
     if (last_of_unit) {
-      n_unit = unit + 1;
-      n_pr = (n_unit % n_chunks) * chunk_pairs;
+      n_unit = unit + u_step;
+      n_pr = unit_pair0(n_unit);
     }
     const bool has_next = n_unit < u_end;
 
@@ -237,7 +280,7 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_split_kernel(
     if (!has_next) break;
     if (last_of_unit) {
       unit = n_unit;
-      const int64_t nrb = unit / n_chunks;
+      const int64_t nrb = unit_rb(unit);
       if (nrb != rb) {
         rb = nrb;
         load_a(rb);
@@ -282,23 +325,64 @@ int device_cus_split() {
   return cus;
 }
 
-template <int KS>
+// Round-robin (sync_sweep) makespan of n_chunks column chunks: blocks take
+// units g, g+G, ... of the chunk-major list; returns total / (G * makespan).
+double sweep_efficiency(int64_t n_row_blocks, int64_t n_pairs, int64_t chunks, int64_t G) {
+  const int64_t cs = ceil_div(n_pairs, chunks);
+  const int64_t nc = ceil_div(n_pairs, cs);
+  const int64_t n_units = n_row_blocks * nc;
+  int64_t makespan = 0;
+  // per-block load depends only on which chunks its units fall in; blocks
+  // 0..G-1 differ by at most one unit, so check the heaviest candidates
+  for (int64_t g = 0; g < G && g < n_units; ++g) {
+    int64_t load = 0;
+    for (int64_t u = g; u < n_units; u += G) {
+      const int64_t c = u / n_row_blocks;
+      load += (c == nc - 1) ? n_pairs - c * cs : cs;
+    }
+    makespan = load > makespan ? load : makespan;
+  }
+  return makespan ? static_cast<double>(n_row_blocks * n_pairs) / (static_cast<double>(G) * makespan) : 0.0;
+}
+
+template <int KS, int MT>
 int launch_split(const uint16_t* rows, int64_t n_rows_pad, const uint16_t* cols, int64_t n_cols_pad,
                  int64_t ldh, int slice_off, int64_t* acc, int grid_blocks, hipStream_t stream) {
-  using C = SpCfg<KS>;
+  using C = SpCfg<KS, MT>;
   const int64_t n_row_blocks = n_rows_pad / kSpRows;
   const int64_t n_pairs = n_cols_pad / (2 * C::SC);
   const int G0 = grid_blocks > 0 ? grid_blocks : 2 * device_cus_split();
-  // ~32 units per block: short tails, long enough units to amortise the butterfly
-  int64_t cs = (n_pairs * n_row_blocks) / (static_cast<int64_t>(G0) * 32);
-  cs = cs < 1 ? 1 : (cs > 32 ? 32 : cs);
-  if (cs > n_pairs) cs = n_pairs;
+  const char* env = getenv("DAL_GRAM_SCHED");
+  const int sync_sweep = env ? atoi(env) : 1;
+  int64_t cs;
+  if (sync_sweep) {
+    // fewest chunks (fewest A reloads) whose round-robin makespan is within 3% of ideal
+    int64_t best_c = 1;
+    double best_e = 0.0;
+    for (int64_t c = 1; c <= 64 && c <= n_pairs; ++c) {
+      const double e = sweep_efficiency(n_row_blocks, n_pairs, c, G0);
+      if (e > best_e + 1e-9) {
+        best_e = e;
+        best_c = c;
+      }
+      if (e >= 0.97) {
+        best_c = c;
+        break;
+      }
+    }
+    cs = ceil_div(n_pairs, best_c);
+  } else {
+    // ~32 units per block: short tails, long enough units to amortise the butterfly
+    cs = (n_pairs * n_row_blocks) / (static_cast<int64_t>(G0) * 32);
+    cs = cs < 1 ? 1 : (cs > 32 ? 32 : cs);
+    if (cs > n_pairs) cs = n_pairs;
+  }
   const int64_t n_chunks = ceil_div(n_pairs, cs);
   const int64_t n_units = n_row_blocks * n_chunks;
   const int64_t G = n_units < G0 ? n_units : G0;
-  hipLaunchKernelGGL(gram_split_kernel<KS>, dim3(static_cast<unsigned>(G)), dim3(kSpThreads), 0, stream,
-                     rows, cols, ldh, slice_off, n_pairs, static_cast<int>(cs), n_chunks, n_units,
-                     reinterpret_cast<unsigned long long*>(acc));
+  hipLaunchKernelGGL((gram_split_kernel<KS, MT>), dim3(static_cast<unsigned>(G)), dim3(kSpThreads), 0, stream,
+                     rows, cols, ldh, slice_off, n_pairs, static_cast<int>(cs), n_chunks, n_row_blocks,
+                     sync_sweep, reinterpret_cast<unsigned long long*>(acc));
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
 }
@@ -312,15 +396,17 @@ using namespace dal;
 
 extern "C" double dal_density_error_bound_split(int64_t n_cols) {
   // Per entry, with u = 2^-23 (a conservative unit roundoff for the MFMA's
-  // internal fp32 accumulation) and chains of at most 1040 additions per fold:
-  //   accumulation  gamma_1040 * sum_d |h_i h_j| (+ the 2^-10-smaller cross chain)
-  //   split         3 * 2^-22 * sum_d |u_i u_j|  (+2^-37 per feature, subnormal halves)
-  //   combine fma   2^-24,  fold rounding  2^-33 per 8 columns
+  // internal fp32 accumulation, counted as sequential adds) and at most 1088
+  // additions per fold chain (256 columns / MT column lanes x KS products):
+  //   main chain    gamma_1088 * sum_d |h_i h_j|,  |h| <= (1 + 2^-11) |u|
+  //   cross chain   gamma_2176 * 2^-10 * sum_d |u_i u_j|  (~2.4e-7)
+  //   split         3.01 * 2^-22 * sum_d |u_i u_j| (+2^-37 per feature, subnormal halves)
+  //   combine fma   2^-24,  fold rounding 2^-33 per fold (<= 1e-10 per column)
   // and sum_d |u_i u_j| <= 1 (Cauchy-Schwarz on unit rows).
   const double u = 1.0 / 8388608.0;  // 2^-23
-  const double gamma = 1040.0 * u / (1.0 - 1040.0 * u);
+  const double gamma = 1088.0 * u / (1.0 - 1088.0 * u);
   const double s = 1.0 / 4194304.0;  // 2^-22
-  return (gamma + 4.0 * s + 1e-12) * static_cast<double>(n_cols) + 1e-9;
+  return (gamma * (1.0 + 1.0 / 512.0) + 5.0 * s + 1e-10) * static_cast<double>(n_cols) + 1e-9;
 }
 
 extern "C" int64_t dal_split_f16_halves(int64_t n_pad, int64_t d_pad) { return n_pad * 2 * d_pad; }
@@ -349,10 +435,17 @@ extern "C" int dal_gram_rowsum_split(const uint16_t* rows, int64_t n_rows_pad, c
   hipStream_t st = as_stream(stream);
   const int ks = split_ks(d_pad);
   const int64_t ldh = 2 * d_pad;
+  const char* env = getenv("DAL_GRAM_MT");
+  const int mt = env ? atoi(env) : 16;
   for (int64_t off = 0; off < d_pad; off += ks) {
     const int so = static_cast<int>(2 * off);  // halves: slice s starts at s * 2 * KS
-    const int rc = ks == 32 ? launch_split<32>(rows, n_rows_pad, cols, n_cols_pad, ldh, so, acc, grid_blocks, st)
-                            : launch_split<64>(rows, n_rows_pad, cols, n_cols_pad, ldh, so, acc, grid_blocks, st);
+    int rc;
+    if (mt == 16)
+      rc = ks == 32 ? launch_split<32, 16>(rows, n_rows_pad, cols, n_cols_pad, ldh, so, acc, grid_blocks, st)
+                    : launch_split<64, 16>(rows, n_rows_pad, cols, n_cols_pad, ldh, so, acc, grid_blocks, st);
+    else
+      rc = ks == 32 ? launch_split<32, 32>(rows, n_rows_pad, cols, n_cols_pad, ldh, so, acc, grid_blocks, st)
+                    : launch_split<64, 32>(rows, n_rows_pad, cols, n_cols_pad, ldh, so, acc, grid_blocks, st);
     if (rc != DAL_OK) return rc;
   }
   return DAL_OK;

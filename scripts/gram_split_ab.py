@@ -26,7 +26,8 @@ for n, d in [(int(a), int(b)) for a, b in shapes]:
     sp = torch.empty(int(lib.dal_split_f16_halves(st.n_pad, st.d_pad)), dtype=torch.int16, device=dev)
     _lib.call("dal_split_f16", _ptr(u), st.n_pad, st.d_pad, st.d_pad, _ptr(sp), _stream(dev))
     flops = 2.0 * (n - 10) * (n - 10) * d
-    t = {"f32": [], "split": []}
+    kinds = os.environ.get("AB_KINDS", "f32,split").split(",")
+    t = {k: [] for k in kinds}
     accs = {}
 
     def run(kind, grid=0):
@@ -34,6 +35,8 @@ for n, d in [(int(a), int(b)) for a, b in shapes]:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         e0.record()
+        os.environ["DAL_GRAM_SCHED"] = "0" if kind.endswith("s0") else "1"
+        os.environ["DAL_GRAM_MT"] = "32" if "32" in kind else "16"
         if kind == "f32":
             _lib.call("dal_gram_rowsum", _ptr(u), st.n_pad, _ptr(u), st.n_pad, st.d_pad, st.d_pad,
                       _ptr(acc), grid, _stream(dev))
@@ -45,21 +48,27 @@ for n, d in [(int(a), int(b)) for a, b in shapes]:
         return acc, e0.elapsed_time(e1)
 
     for r in range(rounds + 1):
-        for kind in ("f32", "split"):
+        for kind in kinds:
             acc, ms = run(kind)
             if r:
                 t[kind].append(ms)
             accs[kind] = acc
     canon = st.density_exact()[10:n]
-    for kind in ("f32", "split"):
+    for kind in kinds:
         dk = accs[kind][10:n].to(torch.float64) / 2.0**32
         err = (dk - canon).abs()
-        bound = (lib.dal_density_error_bound if kind == "f32" else lib.dal_density_error_bound_split)(n - 10)
+        bound = (lib.dal_density_error_bound if kind.startswith("f32") else lib.dal_density_error_bound_split)(n - 10)
         ms = float(np.median(t[kind]))
-        print(f"n={n} d={d} {kind:5s} median {ms:8.3f} ms  {flops / ms / 1e9:7.1f} TF/s "
+        print(f"n={n} d={d} {kind:6s} median {ms:8.3f} ms  {flops / ms / 1e9:7.1f} TF/s "
               f"({100 * flops / ms / 1e9 / 157.3:5.1f}% of fp32 peak)  max|err| {float(err.max()):.3e} "
               f"max rel {float((err / canon.abs()).max()):.3e}  bound {bound:.3e}  "
               f"within={bool(float(err.max()) <= bound)}", flush=True)
+    sk = [k for k in kinds if k.startswith("split")]
+    if len(sk) > 1:
+        print(f"   all split variants same bits: {all(torch.equal(accs[sk[0]], accs[k]) for k in sk)}",
+              flush=True)
+    if "split" not in kinds:
+        continue
     a2, _ = run("split", grid=37)
     a3, _ = run("split", grid=1000)
     print(f"   split grid-invariant: {torch.equal(a2, accs['split']) and torch.equal(a3, accs['split'])}",
