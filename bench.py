@@ -127,6 +127,17 @@ def gram_roofline(gram, achieved, traffic, gram_ms, gram_ms_max, flops):
                 "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic, "launch_ms": gram_ms,
                 "launch_ms_max_over_ranks": gram_ms_max, "algorithmic_flops_per_launch": flops}
+    if gram == "sym":
+        peak = 2.0 * F16_MFMA_PEAK_TFLOPS / 3.0
+        return {"bound": "mfma",
+                "kernel": "dal_gram_rowsum_sym (symmetric block pairs once; 3 x v_mfma_f32_16x16x32_f16 "
+                          "per 32 features: h.h, h.l, l.h)",
+                "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+                "peak_note": "dense fp16 MFMA peak 2500 TF/s / 3 products per algorithmic product, x2: "
+                             "each block-pair product serves S_ij and S_ji (row and column sums)",
+                "executed_fp16_tflops": 1.5 * achieved, "vs_fp32_mfma_peak": achieved / FP32_MFMA_PEAK_TFLOPS,
+                "traffic": traffic, "launch_ms": gram_ms, "launch_ms_max_over_ranks": gram_ms_max,
+                "algorithmic_flops_per_launch": flops}
     peak = F16_MFMA_PEAK_TFLOPS / 3.0
     return {"bound": "mfma",
             "kernel": "dal_gram_rowsum_split (3 x v_mfma_f32_16x16x32_f16 per 32 features: h.h, h.l, l.h)",
@@ -367,8 +378,9 @@ def main():
         try:
             tr = json.load(open(tpath)).get(f"config{args.config}")
             if tr and world == 1:
-                traffic = tr.get("gram_rowsum_split_bytes_per_launch" if state.gram == "split"
-                                 else "gram_rowsum_bytes_per_launch")
+                traffic = tr.get({"sym": "gram_rowsum_sym_bytes_per_launch",
+                                  "split": "gram_rowsum_split_bytes_per_launch"}.get(
+                                      state.gram, "gram_rowsum_bytes_per_launch"))
         except Exception:
             traffic = None
 

@@ -291,6 +291,278 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_split_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Symmetric (SYRK-style) variant: S = U U^T is symmetric, so each unordered
+// pair of 256-row blocks {I, J} is multiplied ONCE and yields both the row sums
+// of S_IJ (-> rows of I) and its column sums (-> rows of J): half the MFMAs.
+// Orientation rule, a function of the global block indices only (so the bits
+// do not depend on the GPU count): row block I takes column block J when
+//   J == I (diagonal: row sums only),  J > I and I+J even,  J < I and I+J odd.
+// Every row block then takes ~nb/2 column blocks, so work is balanced across
+// row blocks, units and row-sharded GPUs.  Column block = fold group = one
+// pair of 128-column stages.  Per 16x16 (or 32x32) output tile the per-tile
+// accumulators are combined on the VALU: t = fma(X, 2^-12, M) is added into
+// the fp32 row accumulator (the same 16-tile chain per fold as the asymmetric
+// kernel) and summed over the lane's rows into a column partial, which is
+// rounded to a multiple of 2^-32 and added into an LDS fp64 column
+// accumulator (integer-valued: exact, order-free); after the pair the 256
+// column sums go to global int64 atomics.  The LDS column accumulator is
+// double-buffered so its flush (at the next pair's first barrier) never races
+// the next pair's adds.
+template <int KS, int MT>
+struct SymCfg {
+  static constexpr int ROWB = KS * 4;
+  static constexpr int SLOTS = ROWB / 16;
+  static constexpr int HI = KS / 8;
+  static constexpr int SC = 128;                        // columns per stage (two per column block)
+  static constexpr int STAGE = SC * ROWB;               // 32 KiB (KS 64) or 16 KiB (KS 32)
+  static constexpr int F4 = STAGE / 16;
+  static constexpr int SWZ = (SLOTS < 16 ? SLOTS : 16) - 1;
+  static constexpr int PIECES = STAGE / (4 * 1024);
+  static constexpr int RT = 64 / MT;
+  static constexpr int LG = 64 / MT;
+  static constexpr int KSTEP = 8 * LG;
+  static constexpr int NKS = KS / KSTEP;
+  static constexpr int NCT = SC / MT;
+  static constexpr int NV = MT * MT / 64;
+  static_assert(NKS >= 1 && PIECES >= 1, "bad slice");
+};
+
+template <int KS, int MT>
+__global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
+    const uint16_t* __restrict__ urows, int row_block0, int n_rb,
+    const uint16_t* __restrict__ ucols, int col_block0, int j_lo, int j_hi,
+    int nb_active, int64_t ldh, int slice_off, int chunk_blocks, int n_chunks,
+    unsigned long long* __restrict__ acc_out) {
+  using C = SymCfg<KS, MT>;
+  using A = SpAcc<MT>;
+  using acc_t = typename A::type;
+  __shared__ __attribute__((aligned(16))) float4 lds[2 * C::F4];
+  __shared__ double colacc[2][256];
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int li = lane % MT, lq = lane / MT;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int n_units = n_rb * n_chunks;
+
+  colacc[0][tid] = 0.0;
+  colacc[1][tid] = 0.0;
+
+  // unit u (chunk-major, dealt round-robin): row block I, column blocks [c_lo, c_hi)
+  // (32-bit block bookkeeping: keeps the persistent loop's scalar state small)
+  auto unit_I = [&](int u) { return row_block0 + u % n_rb; };
+  auto unit_clo = [&](int u) { return j_lo + (u / n_rb) * chunk_blocks; };
+  auto unit_chi = [&](int u) {
+    const int e = j_lo + (u / n_rb + 1) * chunk_blocks;
+    return e < j_hi ? e : j_hi;
+  };
+  auto first_J = [&](int I, int lo, int hi) -> int {
+    if (I >= nb_active) return -1;
+    int J = lo;
+    if (J < I) {
+      if (((I + J) & 1) == 0) ++J;  // J < I needs I+J odd (J may become I)
+    } else if (J > I) {
+      if ((I + J) & 1) ++J;         // J > I needs I+J even
+    }
+    return J < hi ? J : -1;
+  };
+  auto next_J = [&](int I, int J, int hi) -> int {
+    const int n = (J == I - 1) ? I : J + 2;
+    return n < hi ? n : -1;
+  };
+  // next unit (from u, stepping by G) that has at least one column block
+  auto seek = [&](int u, int& J) {
+    while (u < n_units) {
+      J = first_J(unit_I(u), unit_clo(u), unit_chi(u));
+      if (J >= 0) break;
+      u += G;
+    }
+    return u;
+  };
+
+  unsigned voff[C::PIECES];
+#pragma unroll
+  for (int q = 0; q < C::PIECES; ++q) {
+    const int p = (wave * C::PIECES + q) * 64 + lane;
+    const int row = p / C::SLOTS;
+    const int slot = (p % C::SLOTS) ^ (row & C::SWZ);
+    voff[q] = static_cast<unsigned>(row * ldh * 2 + slot * 16);
+  }
+  const unsigned dst0 = __builtin_amdgcn_readfirstlane(
+      static_cast<unsigned>(reinterpret_cast<uintptr_t>((AS3 float4*)(lds + wave * C::PIECES * 64))));
+  // stage h (0/1) of global column block J
+  auto issue = [&](int buf, int J, int h) {
+    const uint16_t* sbase =
+        ucols + (static_cast<int64_t>(J - col_block0) * 256 + h * C::SC) * ldh + slice_off;
+#pragma unroll
+    for (int q = 0; q < C::PIECES; ++q) {
+      const unsigned dst = dst0 + static_cast<unsigned>(buf * C::STAGE + q * 1024);
+      unsigned keep;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+          "global_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "v"(voff[q]), "s"(dst), "s"(sbase)
+          : "memory");
+    }
+  };
+
+  f16x8 ah[C::RT][C::NKS], al[C::RT][C::NKS];
+  auto load_a = [&](int I) {
+#pragma unroll
+    for (int rt = 0; rt < C::RT; ++rt) {
+      const int64_t row = static_cast<int64_t>(I - row_block0) * kSpRows + wave * 64 + rt * MT + li;
+      const uint16_t* src = urows + row * ldh + slice_off;
+#pragma unroll
+      for (int c = 0; c < C::NKS; ++c) {
+        ah[rt][c] = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(src + (c * C::LG + lq) * 8));
+        al[rt][c] = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(src + KS + (c * C::LG + lq) * 8));
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+  };
+
+  int boh[C::NKS], bol[C::NKS];
+#pragma unroll
+  for (int c = 0; c < C::NKS; ++c) {
+    boh[c] = li * C::SLOTS + ((c * C::LG + lq) ^ (li & C::SWZ));
+    bol[c] = li * C::SLOTS + ((C::HI + c * C::LG + lq) ^ (li & C::SWZ));
+  }
+
+  float racc[C::RT][C::NV];
+  double facc[C::RT][C::NV];
+#pragma unroll
+  for (int rt = 0; rt < C::RT; ++rt)
+#pragma unroll
+    for (int r = 0; r < C::NV; ++r) {
+      racc[rt][r] = 0.0f;
+      facc[rt][r] = 0.0;
+    }
+
+  // one 128-column stage: per column tile, fresh accumulators -> row and column sums
+  auto compute = [&](const float4* B, bool cols_too, double* cacc) {
+#pragma unroll
+    for (int ct = 0; ct < C::NCT; ++ct) {
+      acc_t m[C::RT], x[C::RT];
+#pragma unroll
+      for (int c = 0; c < C::NKS; ++c) {
+        const f16x8 bh = __builtin_bit_cast(f16x8, B[ct * MT * C::SLOTS + boh[c]]);
+        const f16x8 bl = __builtin_bit_cast(f16x8, B[ct * MT * C::SLOTS + bol[c]]);
+        const acc_t zero = {};
+#pragma unroll
+        for (int rt = 0; rt < C::RT; ++rt) m[rt] = A::mfma(ah[rt][c], bh, c == 0 ? zero : m[rt]);
+#pragma unroll
+        for (int rt = 0; rt < C::RT; ++rt) x[rt] = A::mfma(ah[rt][c], bl, c == 0 ? zero : x[rt]);
+#pragma unroll
+        for (int rt = 0; rt < C::RT; ++rt) x[rt] = A::mfma(al[rt][c], bh, x[rt]);
+      }
+      float cp = 0.0f;
+#pragma unroll
+      for (int rt = 0; rt < C::RT; ++rt) {
+#pragma unroll
+        for (int r = 0; r < C::NV; ++r) {
+          const float t = __builtin_fmaf(x[rt][r], 0x1p-12f, m[rt][r]);
+          racc[rt][r] += t;
+          cp += t;
+        }
+      }
+      if (cols_too) atomicAdd(cacc + ct * MT + li, fold_fixed(cp));
+      // pin the row accumulators here: otherwise LLVM sinks the adds to the
+      // fold and keeps every tile's values live (hundreds of spilled VGPRs)
+#pragma unroll
+      for (int rt = 0; rt < C::RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < C::NV; ++r) asm volatile("" : "+v"(racc[rt][r]));
+    }
+  };
+  auto fold_rows = [&]() {
+#pragma unroll
+    for (int rt = 0; rt < C::RT; ++rt)
+#pragma unroll
+      for (int r = 0; r < C::NV; ++r) {
+        facc[rt][r] += fold_fixed(racc[rt][r]);
+        racc[rt][r] = 0.0f;
+      }
+  };
+  auto finish_unit = [&](int I) {
+#pragma unroll
+    for (int rt = 0; rt < C::RT; ++rt) {
+#pragma unroll
+      for (int r = 0; r < C::NV; ++r) {
+        double v = facc[rt][r];
+#pragma unroll
+        for (int sh = 1; sh < MT; sh <<= 1) v += __shfl_xor(v, sh);
+        facc[rt][r] = v;
+      }
+    }
+    double mine = 0.0;
+#pragma unroll
+    for (int rt = 0; rt < C::RT; ++rt) {
+#pragma unroll
+      for (int r = 0; r < C::NV; ++r) {
+        if (rt * C::NV + r == li) mine = facc[rt][r];
+        facc[rt][r] = 0.0;
+      }
+    }
+    const int rt = li / C::NV, r = li % C::NV;
+    const int64_t row = static_cast<int64_t>(I) * kSpRows + wave * 64 + rt * MT + A::row(r, lq);
+    atomicAdd(acc_out + row, static_cast<unsigned long long>(static_cast<long long>(mine)));
+  };
+  auto flush_cols = [&](int buf, int J) {
+    const double v = colacc[buf][tid];
+    if (v != 0.0)
+      atomicAdd(acc_out + static_cast<int64_t>(J) * 256 + tid,
+                static_cast<unsigned long long>(static_cast<long long>(v)));
+    colacc[buf][tid] = 0.0;
+  };
+
+  int J = -1;
+  int unit = seek(g, J);
+  if (unit >= n_units) return;
+  int I = unit_I(unit), c_hi = unit_chi(unit);
+  issue(0, J, 0);
+  load_a(I);
+  const float4* B0 = lds;
+  const float4* B1 = lds + C::F4;
+  int cb = 0;             // colacc buffer of the current pair
+  int flushJ = -1;        // column block whose sums wait in colacc[cb ^ 1]
+
+  while (true) {
+    int nJ = next_J(I, J, c_hi), n_unit = unit;
+    if (nJ < 0) n_unit = seek(unit + G, nJ);
+    const bool has_next = n_unit < n_units;
+    const bool last_of_unit = n_unit != unit;
+    const bool cols_too = J != I;
+
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (flushJ >= 0) flush_cols(cb ^ 1, flushJ);
+    issue(1, J, 1);
+    compute(B0, cols_too, &colacc[cb][0]);
+
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (has_next) issue(0, nJ, 0);
+    compute(B1, cols_too, &colacc[cb][C::SC]);
+    fold_rows();
+    flushJ = cols_too ? J : -1;
+    cb ^= 1;
+    if (last_of_unit) finish_unit(I);
+
+    if (!has_next) break;
+    if (last_of_unit) {
+      unit = n_unit;
+      I = unit_I(unit);
+      c_hi = unit_chi(unit);
+      load_a(I);
+    }
+    J = nJ;
+  }
+  __syncthreads();
+  if (flushJ >= 0) flush_cols(cb ^ 1, flushJ);
+}
+
 // fp32 unit rows -> two-term fp16 split, layout [n_pad][d_pad/KS][hi KS | lo KS].
 // One thread per 8 features (one 16-B slot of hi and of lo).
 __global__ __launch_bounds__(256) void split_f16_kernel(const float* __restrict__ u, int64_t n_pad,
@@ -387,6 +659,29 @@ int launch_split(const uint16_t* rows, int64_t n_rows_pad, const uint16_t* cols,
   return DAL_OK;
 }
 
+template <int KS, int MT>
+int launch_sym(const uint16_t* rows, int64_t row_block0, int64_t n_rb, const uint16_t* cols,
+               int64_t col_block0, int64_t j_lo, int64_t j_hi, int64_t nb_active, int64_t ldh,
+               int slice_off, int64_t* acc, int grid_blocks, hipStream_t stream) {
+  const int G0 = grid_blocks > 0 ? grid_blocks : 2 * device_cus_split();
+  const int64_t nj = j_hi - j_lo;
+  // chunks of column blocks: enough units for a balanced round-robin (each
+  // unit does ~half its chunk's blocks), few enough to limit A reloads
+  int64_t nc = 1;
+  while (nc < nj && n_rb * nc < 8LL * G0) ++nc;
+  const int64_t cbk = ceil_div(nj, nc);
+  const int64_t n_chunks = ceil_div(nj, cbk);
+  const int64_t n_units = n_rb * n_chunks;
+  const int64_t G = n_units < G0 ? n_units : G0;
+  hipLaunchKernelGGL((gram_sym_kernel<KS, MT>), dim3(static_cast<unsigned>(G)), dim3(kSpThreads), 0, stream,
+                     rows, static_cast<int>(row_block0), static_cast<int>(n_rb), cols,
+                     static_cast<int>(col_block0), static_cast<int>(j_lo), static_cast<int>(j_hi),
+                     static_cast<int>(nb_active), ldh, slice_off, static_cast<int>(cbk),
+                     static_cast<int>(n_chunks), reinterpret_cast<unsigned long long*>(acc));
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}
+
 inline int split_ks(int64_t d_pad) { return d_pad == 32 ? 32 : 64; }
 
 }  // namespace
@@ -446,6 +741,30 @@ extern "C" int dal_gram_rowsum_split(const uint16_t* rows, int64_t n_rows_pad, c
     else
       rc = ks == 32 ? launch_split<32, 32>(rows, n_rows_pad, cols, n_cols_pad, ldh, so, acc, grid_blocks, st)
                     : launch_split<64, 32>(rows, n_rows_pad, cols, n_cols_pad, ldh, so, acc, grid_blocks, st);
+    if (rc != DAL_OK) return rc;
+  }
+  return DAL_OK;
+}
+
+extern "C" int dal_gram_rowsum_sym(const uint16_t* rows, int64_t row_block0, int64_t n_row_blocks,
+                                   const uint16_t* cols, int64_t col_block0, int64_t j_lo, int64_t j_hi,
+                                   int64_t nb_active, int64_t d_pad, int64_t* acc, int grid_blocks,
+                                   dal_stream_t stream) {
+  if (!rows || !cols || !acc) return DAL_ERR_ARG;
+  if (row_block0 < 0 || n_row_blocks <= 0 || col_block0 < 0 || nb_active <= 0) return DAL_ERR_SHAPE;
+  if (j_lo < col_block0 || j_hi < j_lo || j_hi > nb_active) return DAL_ERR_SHAPE;
+  if (d_pad != dal_pad_features(d_pad)) return DAL_ERR_SHAPE;
+  if ((reinterpret_cast<uintptr_t>(rows) | reinterpret_cast<uintptr_t>(cols)) & 15) return DAL_ERR_SHAPE;
+  if (j_hi == j_lo || row_block0 >= nb_active) return DAL_OK;
+  hipStream_t st = as_stream(stream);
+  const int ks = split_ks(d_pad);
+  const int64_t ldh = 2 * d_pad;
+  for (int64_t off = 0; off < d_pad; off += ks) {
+    const int so = static_cast<int>(2 * off);
+    const int rc = ks == 32 ? launch_sym<32, 16>(rows, row_block0, n_row_blocks, cols, col_block0, j_lo,
+                                                 j_hi, nb_active, ldh, so, acc, grid_blocks, st)
+                            : launch_sym<64, 16>(rows, row_block0, n_row_blocks, cols, col_block0, j_lo,
+                                                 j_hi, nb_active, ldh, so, acc, grid_blocks, st);
     if (rc != DAL_OK) return rc;
   }
   return DAL_OK;

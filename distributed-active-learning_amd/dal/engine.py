@@ -157,7 +157,7 @@ class PoolState:
         u, _ = self.normalized()
         if self.gram == "f32":
             return u
-        if self._split is None:
+        if self._split is None:  # "split" and "sym" share the operand
             torch = _torch()
             self._split = torch.empty((self.n_pad, 2 * self.d_pad), dtype=torch.int16, device=self.device)
             call("dal_split_f16", _ptr(u), self.n_pad, self.d_pad, self.d_pad, _ptr(self._split),
@@ -193,6 +193,10 @@ class PoolState:
         if self._density is None or u_cols is not None:
             torch = _torch()
             op = self.gram_operand()
+            if self.gram == "sym" and u_cols is not None:
+                raise ValueError("gram 'sym' over a gathered operand: use ShardedSelector")
+            if self.gram == "sym" and (self.row_base or self.n_total != self.n):
+                raise ValueError("gram 'sym' on a shard: use ShardedSelector")
             acc = torch.zeros(self.n_pad, dtype=torch.int64, device=self.device)
             cols = op if u_cols is None else u_cols
             ncp = self.n_pad if n_cols_pad is None else int(n_cols_pad)
@@ -202,17 +206,34 @@ class PoolState:
             self._density = acc
         return self._density
 
-    def gram_accumulate(self, acc, cols, n_cols_pad: int, grid_blocks: int = 0):
+    def nb_active(self) -> int:
+        """Global count of 256-row blocks (pad512(N_total) / 256)."""
+        return (self.n_total + 511) // 512 * 2
+
+    def gram_accumulate(self, acc, cols, n_cols_pad: int, grid_blocks: int = 0, col_row0: int = 0):
         """acc += fixed-point row sums of this shard's rows against the first
         ``n_cols_pad`` (a multiple of 512) rows of ``cols`` (a Gram operand of
-        the pool's kind).  Exact: any column split adds up to the same bits."""
+        the pool's kind), whose first row is global row ``col_row0``.  Exact:
+        any column split adds up to the same bits.
+
+        gram "sym": acc is indexed by GLOBAL row (length >= nb_active * 256)
+        and also receives the column sums of the pairs this shard owns (the
+        other ranks' rows included); the ranks' accs are summed afterwards."""
         torch = _torch()
         op = self.gram_operand()
         ev = None
         if self.gram_events is not None:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        if self.gram == "f32":
+        if self.gram == "sym":
+            nb = self.nb_active()
+            j_lo = col_row0 // 256
+            j_hi = min(j_lo + int(n_cols_pad) // 256, nb)
+            if j_hi > j_lo and self.row_base // 256 < nb:
+                call("dal_gram_rowsum_sym", _ptr(op), self.row_base // 256, self.n_pad // 256,
+                     _ptr(cols), j_lo, j_lo, j_hi, nb, self.d_pad, _ptr(acc), int(grid_blocks),
+                     _stream(self.device))
+        elif self.gram == "f32":
             call("dal_gram_rowsum", _ptr(op), self.n_pad, _ptr(cols), int(n_cols_pad), self.d_pad,
                  self.d_pad, _ptr(acc), int(grid_blocks), _stream(self.device))
         else:
@@ -282,17 +303,18 @@ class PoolState:
             raise _lib.DalError("density re-rank candidate set exceeded DAL_SORT_CAP_PAYLOAD")
 
 
-GRAM_KINDS = ("split", "f32")
+GRAM_KINDS = ("sym", "split", "f32")
 
 
 def _gram_kind(gram) -> str:
-    """Density GEMM kernel: "split" (default; fp16 MFMA, two-term split, three
-    products) or "f32" (fp32 MFMA).  DAL_GRAM in the environment overrides the
-    default.  Both are within their rigorous bound of the canonical density and
-    give the same (bit-exact) selection."""
+    """Density GEMM kernel: "sym" (default; fp16 MFMA on the two-term split,
+    three products, each symmetric block pair once), "split" (same arithmetic,
+    every block pair) or "f32" (fp32 MFMA).  DAL_GRAM in the environment
+    overrides the default.  All are within their rigorous bound of the
+    canonical density and give the same (bit-exact) selection."""
     import os
 
-    g = gram if gram is not None else os.environ.get("DAL_GRAM", "split")
+    g = gram if gram is not None else os.environ.get("DAL_GRAM", "sym")
     if g not in GRAM_KINDS:
         raise ValueError(f"gram must be one of {GRAM_KINDS}, not {g!r}")
     return g
@@ -371,6 +393,7 @@ def density_error(state: PoolState) -> float:
     lib = _lib.load()
     if state.gram == "f32":
         return float(lib.dal_density_error_bound(n_cols))
+    # "split" and "sym": same per-entry arithmetic and fold structure
     return float(lib.dal_density_error_bound_split(n_cols))
 
 

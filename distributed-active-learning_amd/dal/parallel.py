@@ -118,27 +118,48 @@ class ShardedSelector:
         the other shards' columns; returns the gathered operand.  Every column
         range is a whole number of shards (multiples of 512), so the exact
         fixed-point sum is the same bits as one call over all columns.  The
-        own-shard launch leaves ``reserve_cus`` CUs free for RCCL's kernels."""
-        torch = __import__("torch")
+        own-shard launch leaves ``reserve_cus`` CUs free for RCCL's kernels.
+        gram "sym": the accumulator spans every global row (this rank's pairs
+        also yield column sums for other ranks' rows) and is reduce-scattered."""
         st = self.state
         u_full, work = comm.all_gather_start(u_local)
-        acc = torch.zeros(st.n_pad, dtype=torch.int64, device=st.device)
+        acc = self._new_acc()
         if st.n:
             grid = max(1, 2 * (_device_cus(st.device) - reserve_cus)) if work is not None else 0
-            st.gram_accumulate(acc, u_local, self.shard, grid_blocks=grid)
+            st.gram_accumulate(acc, u_local, self.shard, grid_blocks=grid, col_row0=self.lo)
         comm.wait(work)
         if st.n:
             for c0, c1 in other_column_ranges(self.rank, self.world, self.shard):
-                st.gram_accumulate(acc, u_full[c0:c1], c1 - c0)
-        self._density = acc
-        st.set_density_fixed(acc)
+                st.gram_accumulate(acc, u_full[c0:c1], c1 - c0, col_row0=c0)
+        if st.gram == "sym":
+            acc = comm.reduce_scatter_sum(acc)
+        self.set_density(acc)
         return u_full
+
+    def _new_acc(self):
+        torch = __import__("torch")
+        n = self.world * self.shard if self.state.gram == "sym" else self.state.n_pad
+        return torch.zeros(n, dtype=torch.int64, device=self.state.device)
+
+    def density_contribution(self, u_full):
+        """This rank's fixed-point density contribution against every column of
+        the gathered operand: its own rows' sums ([shard]), or for gram "sym"
+        a global-length vector that must be summed over ranks."""
+        acc = self._new_acc()
+        if self.state.n:
+            self.state.gram_accumulate(acc, u_full, int(u_full.shape[0]), col_row0=0)
+        return acc
+
+    def set_density(self, acc_local):
+        self._density = acc_local
+        self.state.set_density_fixed(acc_local)
 
     # ---- phase B: density against all columns + local exact top-k ------
     def local_density(self, u_full):
         if self._density is None:
-            self._density = self.state.density_fixed(u_cols=u_full, n_cols_pad=int(u_full.shape[0]))
-            self.state.set_density_fixed(self._density)
+            if self.state.gram == "sym":
+                raise RuntimeError("gram 'sym' needs the cross-rank sum: use exchange_density / emulate")
+            self.set_density(self.density_contribution(u_full))
         return self._density
 
     def local_select(self, u_full, partials_full, unlabeled_idx, forest, k: int, mode: str = "dw",
@@ -236,6 +257,19 @@ class TorchComm:
         self.dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
         return out, None
 
+    def reduce_scatter_sum(self, t):
+        """Sum over ranks of a [world * m] tensor; returns this rank's [m] slice."""
+        torch = __import__("torch")
+        m = t.shape[0] // self.world
+        rank = self.dist.get_rank(self.group)
+        if self.dist.get_backend(self.group) == "gloo":
+            h = t.cpu()
+            self.dist.all_reduce(h, op=self.dist.ReduceOp.SUM, group=self.group)
+            return h[rank * m:(rank + 1) * m].to(t.device)
+        out = torch.empty(m, dtype=t.dtype, device=t.device)
+        self.dist.reduce_scatter_tensor(out, t.contiguous(), op=self.dist.ReduceOp.SUM, group=self.group)
+        return out
+
     def wait(self, work):
         """Order the current stream after the collective (no host block)."""
         if work is not None:
@@ -267,6 +301,15 @@ def emulate(selectors, unlabeled_idx, forest, k: int, mode: str = "dw",
     preps = [s.prep() for s in selectors]
     u_full = torch.cat([p[0] for p in preps]) if mode == "dw" else None
     parts_full = torch.cat([p[1] for p in preps]) if mode == "dw" else None
+    if mode == "dw" and density_mode == "gram" and selectors and selectors[0]._density is None:
+        contrib = [s.density_contribution(u_full) for s in selectors]
+        if selectors[0].state.gram == "sym":
+            total = torch.stack(contrib).sum(dim=0)  # the reduce-scatter
+            for s in selectors:
+                s.set_density(total[s.rank * s.shard:(s.rank + 1) * s.shard].clone())
+        else:
+            for s, c in zip(selectors, contrib):
+                s.set_density(c)
     tops = [s.local_select(u_full, parts_full, unlabeled_idx, forest, k, mode, strategy, beta,
                            density_mode)
             for s in selectors]

@@ -148,6 +148,23 @@ int dal_gram_rowsum_split(const uint16_t* rows, int64_t n_rows_pad, const uint16
                           int64_t n_cols_pad, int64_t d_pad, int64_t* acc, int grid_blocks,
                           dal_stream_t stream);
 double dal_density_error_bound_split(int64_t n_cols);
+/* Symmetric (SYRK-style) form of dal_gram_rowsum_split: S = U U^T is
+ * symmetric, so each unordered pair of 256-row blocks {I, J} is multiplied
+ * once and gives the row sums of S_IJ (-> acc rows of I) and its column sums
+ * (-> acc rows of J): half the MFMA work.  Row block I takes column block J
+ * iff J == I, or J > I and I+J even, or J < I and I+J odd (global block
+ * indices, so the bits do not depend on the sharding).  rows: the operand of
+ * global row blocks [row_block0, row_block0 + n_row_blocks); cols: the operand
+ * whose first block is global block col_block0; only column blocks
+ * [j_lo, j_hi) are processed (j_hi <= nb_active = pad512(N_total) / 256), so
+ * a caller can split the columns over several calls.  acc is indexed by
+ * GLOBAL row (>= nb_active * 256 entries, zeroed by the caller); on several
+ * GPUs the per-rank accs are summed (reduce-scatter).  Same rounding
+ * structure and bound as dal_gram_rowsum_split (dal_density_error_bound_split). */
+int dal_gram_rowsum_sym(const uint16_t* rows, int64_t row_block0, int64_t n_row_blocks,
+                        const uint16_t* cols, int64_t col_block0, int64_t j_lo, int64_t j_hi,
+                        int64_t nb_active, int64_t d_pad, int64_t* acc, int grid_blocks,
+                        dal_stream_t stream);
 
 /* ---- (a5-a10) forest votes + uncertainty / density-weighted score ------
  * Replaces uncertainty_sampling.py:88-98 / density_weighting.py:136-167:

@@ -37,7 +37,11 @@ for n, d in [(int(a), int(b)) for a, b in shapes]:
         e0.record()
         os.environ["DAL_GRAM_SCHED"] = "0" if kind.endswith("s0") else "1"
         os.environ["DAL_GRAM_MT"] = "32" if "32" in kind else "16"
-        if kind == "f32":
+        if kind == "sym":
+            nb = st.n_pad // 256
+            _lib.call("dal_gram_rowsum_sym", _ptr(sp), 0, nb, _ptr(sp), 0, 0, nb, nb, st.d_pad,
+                      _ptr(acc), grid, _stream(dev))
+        elif kind == "f32":
             _lib.call("dal_gram_rowsum", _ptr(u), st.n_pad, _ptr(u), st.n_pad, st.d_pad, st.d_pad,
                       _ptr(acc), grid, _stream(dev))
         else:
@@ -64,6 +68,11 @@ for n, d in [(int(a), int(b)) for a, b in shapes]:
               f"max rel {float((err / canon.abs()).max()):.3e}  bound {bound:.3e}  "
               f"within={bool(float(err.max()) <= bound)}", flush=True)
     sk = [k for k in kinds if k.startswith("split")]
+    if "sym" in kinds:
+        a2, _ = run("sym", grid=37)
+        a3, _ = run("sym", grid=1000)
+        print(f"   sym grid-invariant: {torch.equal(a2, accs['sym']) and torch.equal(a3, accs['sym'])}",
+              flush=True)
     if len(sk) > 1:
         print(f"   all split variants same bits: {all(torch.equal(accs[sk[0]], accs[k]) for k in sk)}",
               flush=True)

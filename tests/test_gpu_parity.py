@@ -75,7 +75,7 @@ def test_canonical_colsum_bit_exact(cuda, n, d):
     assert np.array_equal(_np(st.colsum()), ref)
 
 
-@pytest.mark.parametrize("gram", ["split", "f32"])
+@pytest.mark.parametrize("gram", ["sym", "split", "f32"])
 @pytest.mark.parametrize("n,d,dist", [(4096, 256, "uniform"), (5000, 64, "uniform"),
                                       (3000, 30, "normal"), (2100, 128, "uniform"),
                                       (1200, 500, "uniform")])
@@ -93,6 +93,9 @@ def test_gram_density_within_bound(cuda, n, d, dist, gram):
     err = np.abs(got[ok] - ref[ok])
     lib = _lib.load()
     bound = (lib.dal_density_error_bound if gram == "f32" else lib.dal_density_error_bound_split)(n - len(E))
+    if gram == "sym":  # symmetric pairs: same kernel arithmetic as "split", within the same bound
+        sp = _np(PoolState(X, excluded=E, device=cuda, gram="split").density())
+        assert np.abs(sp[ok] - got[ok]).max() <= 2 * bound
     assert err.max() <= bound
     # accuracy bar of the north star: 1e-5 relative (signed data: relative to sum |S_ij|)
     scale = np.abs(O.l2_normalize(X) @ O.l2_normalize(X)[ok].T).sum(axis=1)[ok]
@@ -123,7 +126,7 @@ def test_split_operand_bit_exact(cuda, d):
     assert (np.abs(rec - u) <= 2.0**-22 * np.abs(u) + 2.0**-37).all()
 
 
-@pytest.mark.parametrize("gram", ["split", "f32"])
+@pytest.mark.parametrize("gram", ["sym", "split", "f32"])
 @pytest.mark.parametrize("d", [32, 64, 256])
 def test_gram_kernels_deterministic_across_grids_and_column_splits(cuda, gram, d):
     """int64 fixed-point accumulation: identical bits for any grid/unit split
@@ -143,7 +146,7 @@ def test_gram_kernels_deterministic_across_grids_and_column_splits(cuda, gram, d
         assert np.array_equal(o, outs[0])
     part = torch.zeros(st.n_pad, dtype=torch.int64, device=cuda)
     for c0, c1 in ((2048, 4096), (0, 1024), (4096, st.n_pad), (1024, 2048)):
-        st.gram_accumulate(part, op[c0:], c1 - c0)
+        st.gram_accumulate(part, op[c0:], c1 - c0, col_row0=c0)
     assert np.array_equal(_np(part), outs[0])
 
 
@@ -421,7 +424,7 @@ def test_cosine_entries_and_column_similarities(cuda):
 
 
 # ------------------------------------------- config-2 scale properties ----
-@pytest.mark.parametrize("gram", ["split", "f32"])
+@pytest.mark.parametrize("gram", ["sym", "split", "f32"])
 def test_config2_scale_selection_bit_exact(cuda, gram):
     """100k x 64, T=10, k=100 (BASELINE config 2) against the oracle, with
     either density GEMM kernel."""
@@ -453,7 +456,7 @@ def test_config2_scale_selection_bit_exact(cuda, gram):
 
 # ------------------------------------------------ multi-shard (1 GPU) -----
 @pytest.mark.parametrize("world", [2, 3, 4])
-@pytest.mark.parametrize("mode", ["dw", "us", "dw-separable", "dw-f32"])
+@pytest.mark.parametrize("mode", ["dw", "us", "dw-separable", "dw-f32", "dw-split"])
 def test_sharded_emulation_bit_identical(cuda, world, mode):
     """P row shards (emulated in one process, all-gathers as concatenation)
     give the same density bits and the same selection as P = 1 and the oracle."""
@@ -468,7 +471,7 @@ def test_sharded_emulation_bit_identical(cuda, world, mode):
     F = Forest.synthetic(10, 4, d, seed=1)
     E = np.arange(10)
     unl = np.arange(10, n)
-    gram = "f32" if mode == "dw-f32" else "split"
+    gram = {"dw-f32": "f32", "dw-split": "split"}.get(mode, "sym")
     sels = []
     for r in range(world):
         lo, hi, _ = parallel.shard_range(n, world, r)
@@ -483,7 +486,7 @@ def test_sharded_emulation_bit_identical(cuda, world, mode):
     elif mode == "dw":
         ref = density_step(st, unl, F, 50)
         _, o_idx, o_sc = O.density_select(X, unl, of, 50, 1.0, E)
-        dens = torch.cat([s.state.density_fixed()[: s.state.n] for s in sels])
+        dens = torch.cat([s._density[: s.state.n] for s in sels])
         assert torch.equal(dens, st.density_fixed()[:n])
     else:
         ref = uncertainty_step(st, unl, F, 50)
