@@ -39,6 +39,10 @@
 
 #include <stdlib.h>
 
+#ifndef DAL_ABL
+#define DAL_ABL 0  // timing ablations (scripts/gram_ablate.py): 1 no column sums, 2 no stage DMA
+#endif
+
 #include <type_traits>
 
 #include "common.hpp"
@@ -328,7 +332,7 @@ struct SymCfg {
   static_assert(NKS >= 1 && PIECES >= 1, "bad slice");
 };
 
-template <int KS, int MT>
+template <int KS, int MT, bool ONE>
 __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
     const uint16_t* __restrict__ urows, int row_block0, int n_rb,
     const uint16_t* __restrict__ ucols, int col_block0, int j_lo, int j_hi,
@@ -408,7 +412,10 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
     }
   };
 
-  f16x8 ah[C::RT][C::NKS], al[C::RT][C::NKS];
+  // ONE: a single accumulator per tile carries 2^12 h_i.h_j + h_i.l_j + l_i.h_j
+  // (the hi rows pre-scaled by 2^12 -- exact in fp16 since |h| <= 1), so the
+  // epilogue needs no combine step; sums are in units of 2^-12.
+  f16x8 ah[C::RT][C::NKS], al[C::RT][C::NKS], aH[ONE ? C::RT : 1][C::NKS];
   auto load_a = [&](int I) {
 #pragma unroll
     for (int rt = 0; rt < C::RT; ++rt) {
@@ -421,7 +428,15 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
       }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);
+    if constexpr (ONE) {
+      const f16x8 k4096 = {4096, 4096, 4096, 4096, 4096, 4096, 4096, 4096};
+#pragma unroll
+      for (int rt = 0; rt < C::RT; ++rt)
+#pragma unroll
+        for (int c = 0; c < C::NKS; ++c) aH[rt][c] = ah[rt][c] * k4096;
+    }
   };
+  constexpr float kFold = ONE ? 0x1p20f : 0x1p32f;  // tile sums -> multiples of 2^-32
 
   int boh[C::NKS], bol[C::NKS];
 #pragma unroll
@@ -442,38 +457,59 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
 
   // one 128-column stage: per column tile, fresh accumulators -> row and column sums
   auto compute = [&](const float4* B, bool cols_too, double* cacc) {
+    // software-pipelined: tile ct's MFMAs are issued before tile ct-1's
+    // epilogue (two accumulator sets), so the epilogue's VALU runs under them
+    acc_t m[2][C::RT], x[2][C::RT];
 #pragma unroll
-    for (int ct = 0; ct < C::NCT; ++ct) {
-      acc_t m[C::RT], x[C::RT];
+    for (int ct = 0; ct <= C::NCT; ++ct) {
+      if (ct < C::NCT) {
+        const int st = ct & 1;
 #pragma unroll
-      for (int c = 0; c < C::NKS; ++c) {
-        const f16x8 bh = __builtin_bit_cast(f16x8, B[ct * MT * C::SLOTS + boh[c]]);
-        const f16x8 bl = __builtin_bit_cast(f16x8, B[ct * MT * C::SLOTS + bol[c]]);
-        const acc_t zero = {};
+        for (int c = 0; c < C::NKS; ++c) {
+          const f16x8 bh = __builtin_bit_cast(f16x8, B[ct * MT * C::SLOTS + boh[c]]);
+          const f16x8 bl = __builtin_bit_cast(f16x8, B[ct * MT * C::SLOTS + bol[c]]);
+          const acc_t zero = {};
+          if constexpr (ONE) {
 #pragma unroll
-        for (int rt = 0; rt < C::RT; ++rt) m[rt] = A::mfma(ah[rt][c], bh, c == 0 ? zero : m[rt]);
+            for (int rt = 0; rt < C::RT; ++rt) m[st][rt] = A::mfma(aH[rt][c], bh, c == 0 ? zero : m[st][rt]);
 #pragma unroll
-        for (int rt = 0; rt < C::RT; ++rt) x[rt] = A::mfma(ah[rt][c], bl, c == 0 ? zero : x[rt]);
+            for (int rt = 0; rt < C::RT; ++rt) m[st][rt] = A::mfma(ah[rt][c], bl, m[st][rt]);
 #pragma unroll
-        for (int rt = 0; rt < C::RT; ++rt) x[rt] = A::mfma(al[rt][c], bh, x[rt]);
-      }
-      float cp = 0.0f;
+            for (int rt = 0; rt < C::RT; ++rt) m[st][rt] = A::mfma(al[rt][c], bh, m[st][rt]);
+          } else {
 #pragma unroll
-      for (int rt = 0; rt < C::RT; ++rt) {
+            for (int rt = 0; rt < C::RT; ++rt) m[st][rt] = A::mfma(ah[rt][c], bh, c == 0 ? zero : m[st][rt]);
 #pragma unroll
-        for (int r = 0; r < C::NV; ++r) {
-          const float t = __builtin_fmaf(x[rt][r], 0x1p-12f, m[rt][r]);
-          racc[rt][r] += t;
-          cp += t;
+            for (int rt = 0; rt < C::RT; ++rt) x[st][rt] = A::mfma(ah[rt][c], bl, c == 0 ? zero : x[st][rt]);
+#pragma unroll
+            for (int rt = 0; rt < C::RT; ++rt) x[st][rt] = A::mfma(al[rt][c], bh, x[st][rt]);
+          }
         }
       }
-      if (cols_too) atomicAdd(cacc + ct * MT + li, fold_fixed(cp));
-      // pin the row accumulators here: otherwise LLVM sinks the adds to the
-      // fold and keeps every tile's values live (hundreds of spilled VGPRs)
+      if (ct > 0) {
+        const int pt = (ct - 1) & 1;
+        float cp = 0.0f;
 #pragma unroll
-      for (int rt = 0; rt < C::RT; ++rt)
+        for (int rt = 0; rt < C::RT; ++rt) {
 #pragma unroll
-        for (int r = 0; r < C::NV; ++r) asm volatile("" : "+v"(racc[rt][r]));
+          for (int r = 0; r < C::NV; ++r) {
+            const float t = ONE ? m[pt][rt][r] : __builtin_fmaf(x[pt][rt][r], 0x1p-12f, m[pt][rt][r]);
+            racc[rt][r] += t;
+            cp += t;
+          }
+        }
+#if DAL_ABL == 1
+        (void)cp; (void)cols_too; (void)cacc;
+#else
+        if (cols_too) atomicAdd(cacc + (ct - 1) * MT + li, static_cast<double>(__builtin_rintf(cp * kFold)));
+#endif
+        // pin the row accumulators here: otherwise LLVM sinks the adds to the
+        // fold and keeps every tile's values live (hundreds of spilled VGPRs)
+#pragma unroll
+        for (int rt = 0; rt < C::RT; ++rt)
+#pragma unroll
+          for (int r = 0; r < C::NV; ++r) asm volatile("" : "+v"(racc[rt][r]));
+      }
     }
   };
   auto fold_rows = [&]() {
@@ -481,7 +517,7 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
     for (int rt = 0; rt < C::RT; ++rt)
 #pragma unroll
       for (int r = 0; r < C::NV; ++r) {
-        facc[rt][r] += fold_fixed(racc[rt][r]);
+        facc[rt][r] += static_cast<double>(__builtin_rintf(racc[rt][r] * kFold));
         racc[rt][r] = 0.0f;
       }
   };
@@ -538,12 +574,16 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (flushJ >= 0) flush_cols(cb ^ 1, flushJ);
+#if DAL_ABL != 2
     issue(1, J, 1);
+#endif
     compute(B0, cols_too, &colacc[cb][0]);
 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+#if DAL_ABL != 2
     if (has_next) issue(0, nJ, 0);
+#endif
     compute(B1, cols_too, &colacc[cb][C::SC]);
     fold_rows();
     flushJ = cols_too ? J : -1;
@@ -659,7 +699,7 @@ int launch_split(const uint16_t* rows, int64_t n_rows_pad, const uint16_t* cols,
   return DAL_OK;
 }
 
-template <int KS, int MT>
+template <int KS, int MT, bool ONE>
 int launch_sym(const uint16_t* rows, int64_t row_block0, int64_t n_rb, const uint16_t* cols,
                int64_t col_block0, int64_t j_lo, int64_t j_hi, int64_t nb_active, int64_t ldh,
                int slice_off, int64_t* acc, int grid_blocks, hipStream_t stream) {
@@ -667,13 +707,28 @@ int launch_sym(const uint16_t* rows, int64_t row_block0, int64_t n_rb, const uin
   const int64_t nj = j_hi - j_lo;
   // chunks of column blocks: enough units for a balanced round-robin (each
   // unit does ~half its chunk's blocks), few enough to limit A reloads
+  // column-block chunks: >= 4 units per block, then the count whose last
+  // round-robin round is fullest (units cost ~equal: half a chunk each)
   int64_t nc = 1;
-  while (nc < nj && n_rb * nc < 8LL * G0) ++nc;
+  while (nc < nj && n_rb * nc < 4LL * G0) ++nc;
+  {
+    double best = -1.0;
+    int64_t best_nc = nc;
+    for (int64_t c = nc; c <= nc + 32 && c <= nj; ++c) {
+      const int64_t cb = ceil_div(nj, c), ncc = ceil_div(nj, cb), u = n_rb * ncc;
+      const double eff = static_cast<double>(u) / (static_cast<double>(G0) * ceil_div(u, G0));
+      if (eff > best + 0.01) {
+        best = eff;
+        best_nc = c;
+      }
+    }
+    nc = best_nc;
+  }
   const int64_t cbk = ceil_div(nj, nc);
   const int64_t n_chunks = ceil_div(nj, cbk);
   const int64_t n_units = n_rb * n_chunks;
   const int64_t G = n_units < G0 ? n_units : G0;
-  hipLaunchKernelGGL((gram_sym_kernel<KS, MT>), dim3(static_cast<unsigned>(G)), dim3(kSpThreads), 0, stream,
+  hipLaunchKernelGGL((gram_sym_kernel<KS, MT, ONE>), dim3(static_cast<unsigned>(G)), dim3(kSpThreads), 0, stream,
                      rows, static_cast<int>(row_block0), static_cast<int>(n_rb), cols,
                      static_cast<int>(col_block0), static_cast<int>(j_lo), static_cast<int>(j_hi),
                      static_cast<int>(nb_active), ldh, slice_off, static_cast<int>(cbk),
@@ -761,10 +816,19 @@ extern "C" int dal_gram_rowsum_sym(const uint16_t* rows, int64_t row_block0, int
   const int64_t ldh = 2 * d_pad;
   for (int64_t off = 0; off < d_pad; off += ks) {
     const int so = static_cast<int>(2 * off);
-    const int rc = ks == 32 ? launch_sym<32, 16>(rows, row_block0, n_row_blocks, cols, col_block0, j_lo,
-                                                 j_hi, nb_active, ldh, so, acc, grid_blocks, st)
-                            : launch_sym<64, 16>(rows, row_block0, n_row_blocks, cols, col_block0, j_lo,
-                                                 j_hi, nb_active, ldh, so, acc, grid_blocks, st);
+    const char* env = getenv("DAL_GRAM_ONE");
+    const bool one = env ? atoi(env) != 0 : true;
+    int rc;
+    if (one)
+      rc = ks == 32 ? launch_sym<32, 16, true>(rows, row_block0, n_row_blocks, cols, col_block0, j_lo, j_hi,
+                                               nb_active, ldh, so, acc, grid_blocks, st)
+                    : launch_sym<64, 16, true>(rows, row_block0, n_row_blocks, cols, col_block0, j_lo, j_hi,
+                                               nb_active, ldh, so, acc, grid_blocks, st);
+    else
+      rc = ks == 32 ? launch_sym<32, 16, false>(rows, row_block0, n_row_blocks, cols, col_block0, j_lo, j_hi,
+                                                nb_active, ldh, so, acc, grid_blocks, st)
+                    : launch_sym<64, 16, false>(rows, row_block0, n_row_blocks, cols, col_block0, j_lo, j_hi,
+                                                nb_active, ldh, so, acc, grid_blocks, st);
     if (rc != DAL_OK) return rc;
   }
   return DAL_OK;

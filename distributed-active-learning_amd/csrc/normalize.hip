@@ -78,38 +78,34 @@ __global__ __launch_bounds__(kNormThreads) void normalize_rows_kernel(
 // (lanes = features, coalesced loads) into an fp64 LDS tile; wave 0 then adds
 // the 256 rows in order -- the canonical sequence, but with the divisions and
 // loads in parallel.
-constexpr int kColFeat = 64;
+constexpr int kColFeat = 16;
 __global__ __launch_bounds__(256) void canon_colsum_partials_kernel(
     const float* __restrict__ x, int64_t n, int d, int64_t ldx, const double* __restrict__ norm64,
     const uint8_t* __restrict__ flags, double* __restrict__ partials) {
+  // block = (256-row chunk, kColFeat features): all 256 threads compute the
+  // fp64 unit values (the divisions) into LDS, then kColFeat lanes add the 256
+  // rows in order.  Small blocks -> many chunks in flight per CU: the
+  // sequential add chains overlap instead of running one chunk per CU.
   __shared__ double u[DAL_CANON_CHUNK][kColFeat];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x;
+  const int fl = tid % kColFeat, rs = tid / kColFeat;
   const int64_t c = blockIdx.x;
-  const int f = blockIdx.y * kColFeat + lane;
-  const int64_t r0 = c * DAL_CANON_CHUNK + wave * 64;
+  const int f = blockIdx.y * kColFeat + fl;
   // Excluded / padding rows contribute +0.0: the running sum starts at +0.0
   // and can never become -0.0, so adding +0.0 is bit-identical to skipping.
+  constexpr int kRowsPerPass = 256 / kColFeat;
 #pragma unroll
-  for (int i0 = 0; i0 < 64; i0 += 16) {
-    float xv[16];
-    double nv[16];
-    bool lv[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int64_t r = r0 + i0 + i;
-      lv[i] = r < n && f < d && !(flags && (flags[r] & DAL_ROW_EXCLUDED));
-      xv[i] = lv[i] ? x[r * ldx + f] : 0.0f;
-      nv[i] = lv[i] ? norm64[r] : 1.0;
-    }
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-      u[wave * 64 + i0 + i][lane] = lv[i] ? static_cast<double>(xv[i]) / nv[i] : 0.0;
+  for (int k = 0; k < DAL_CANON_CHUNK / kRowsPerPass; ++k) {
+    const int rl = rs + k * kRowsPerPass;
+    const int64_t r = c * DAL_CANON_CHUNK + rl;
+    const bool live = r < n && f < d && !(flags && (flags[r] & DAL_ROW_EXCLUDED));
+    u[rl][fl] = live ? static_cast<double>(x[r * ldx + f]) / norm64[r] : 0.0;
   }
   __syncthreads();
-  if (wave != 0 || f >= d) return;
+  if (tid >= kColFeat || f >= d) return;
   double acc = 0.0;
 #pragma unroll 32
-  for (int rl = 0; rl < DAL_CANON_CHUNK; ++rl) acc = acc + u[rl][lane];
+  for (int rl = 0; rl < DAL_CANON_CHUNK; ++rl) acc = acc + u[rl][tid];
   partials[c * d + f] = acc;
 }
 
@@ -148,23 +144,35 @@ __global__ __launch_bounds__(256) void density_separable_kernel(
 }
 
 // s[f] = sum_c partials[c][f], sequential over c; loads batched 32 deep.
-__global__ __launch_bounds__(64) void canon_colsum_reduce_kernel(const double* __restrict__ partials,
-                                                                 int64_t n_chunks, int d,
-                                                                 double* __restrict__ s) {
-  const int f = blockIdx.x * 64 + threadIdx.x;
-  if (f >= d) return;
-  constexpr int kBatch = 32;
+constexpr int kRedFeat = 32;     // features per reduce block
+constexpr int kRedTile = 512;    // chunks staged in LDS per pass (128 KiB)
+__global__ __launch_bounds__(256) void canon_colsum_reduce_kernel(const double* __restrict__ partials,
+                                                                  int64_t n_chunks, int d,
+                                                                  double* __restrict__ s) {
+  // all 256 threads stage a tile of partials in LDS (many loads in flight),
+  // then kRedFeat lanes add the chunks in order
+  __shared__ double t[kRedTile][kRedFeat];
+  const int tid = threadIdx.x;
+  const int f0 = blockIdx.x * kRedFeat;
   double acc = 0.0;
-  int64_t c = 0;
-  for (; c + kBatch <= n_chunks; c += kBatch) {
-    double v[kBatch];
+  for (int64_t c0 = 0; c0 < n_chunks; c0 += kRedTile) {
+    const int m = static_cast<int>(n_chunks - c0 < kRedTile ? n_chunks - c0 : kRedTile);
+    for (int e = tid; e < m * kRedFeat; e += 256) {
+      const int ci = e / kRedFeat, fl = e % kRedFeat;
+      t[ci][fl] = f0 + fl < d ? partials[(c0 + ci) * d + f0 + fl] : 0.0;
+    }
+    __syncthreads();
+    if (tid < kRedFeat) {
+      int ci = 0;
+      for (; ci + 8 <= m; ci += 8) {
 #pragma unroll
-    for (int i = 0; i < kBatch; ++i) v[i] = partials[(c + i) * d + f];
-#pragma unroll
-    for (int i = 0; i < kBatch; ++i) acc = acc + v[i];
+        for (int i = 0; i < 8; ++i) acc = acc + t[ci + i][tid];
+      }
+      for (; ci < m; ++ci) acc = acc + t[ci][tid];
+    }
+    __syncthreads();
   }
-  for (; c < n_chunks; ++c) acc = acc + partials[c * d + f];
-  s[f] = acc;
+  if (tid < kRedFeat && f0 + tid < d) s[f0 + tid] = acc;
 }
 
 __global__ __launch_bounds__(256) void mark_rows_kernel(const int64_t* __restrict__ idx, int64_t count,
@@ -244,8 +252,8 @@ extern "C" int dal_canon_colsum_reduce(const double* partials, int64_t n_chunks,
                                        double* colsum, dal_stream_t stream) {
   if (!partials || !colsum) return DAL_ERR_ARG;
   if (n_chunks < 1 || d < 1) return DAL_ERR_SHAPE;
-  hipLaunchKernelGGL(canon_colsum_reduce_kernel, dim3(static_cast<unsigned>(ceil_div(d, 64))),
-                     dim3(64), 0, as_stream(stream), partials, n_chunks, static_cast<int>(d),
+  hipLaunchKernelGGL(canon_colsum_reduce_kernel, dim3(static_cast<unsigned>(ceil_div(d, kRedFeat))),
+                     dim3(256), 0, as_stream(stream), partials, n_chunks, static_cast<int>(d),
                      colsum);
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;

@@ -647,6 +647,14 @@ static int select_with_rerank(const uint64_t* keys_lo, const uint64_t* keys_hi, 
   rc = run_compact<true>(keys_lo, IntervalArgs{keys_hi}, n, idx_base, k, ws, L1, dev_status, st);
   if (rc) return rc;
   rerank(h1, ckey, cidx, cpay, cap);  // canonical keys for every slot (NONE past the count)
+  if (cap <= DAL_SORT_CAP_PAYLOAD) {
+    // level 2 fits one block: sort the cand_count candidates (row order, so
+    // ties resolve by index) by canonical key with their scores, take k
+    hipLaunchKernelGGL(sort_kernel<true>, dim3(1), dim3(kSortThreads), 0, st, ckey, cidx, cpay, h1, int64_t{0},
+                       k, out_keys, out_idx, out_scores);
+    DAL_RETURN_IF_LAUNCH_FAILED();
+    return DAL_OK;
+  }
   rc = run_radix(ckey, cap, k, h2, st);
   if (rc) return rc;
   rc = run_compact<false>(ckey, IntervalArgs{nullptr}, cap, 0, k, base2, L2, nullptr, st);

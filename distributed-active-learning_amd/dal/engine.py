@@ -398,8 +398,9 @@ def density_error(state: PoolState) -> float:
 
 
 def candidate_cap(n: int, k: int) -> int:
-    """Initial re-rank candidate capacity (k plus a band; grown on overflow)."""
-    return int(min(n, max(4 * k, k + 8192)))
+    """Initial re-rank candidate capacity (grown on overflow).  Up to
+    DAL_SORT_CAP_PAYLOAD the exact second level is a single one-block sort."""
+    return int(min(n, max(4 * k, _lib.DAL_SORT_CAP_PAYLOAD)))
 
 
 def workspace(nbytes: int, device):

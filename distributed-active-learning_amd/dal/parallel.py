@@ -228,6 +228,14 @@ def hip_sort_positions(keys, pos, k):
     return out_pos
 
 
+def _gloo_needs_bytes(dtype) -> bool:
+    """gloo gathers none of torch's 16-bit integer or unsigned 16/32/64-bit
+    types: such tensors travel as their bytes."""
+    torch = __import__("torch")
+    names = ("int16", "uint16", "uint32", "uint64")
+    return any(getattr(torch, n, None) == dtype for n in names)
+
+
 class TorchComm:
     """all-gather over torch.distributed (RCCL on ROCm GPUs, gloo on CPU)."""
 
@@ -247,6 +255,9 @@ class TorchComm:
         """Start an all-gather; returns (output, work handle or None).  With
         RCCL it runs asynchronously on the communicator's stream."""
         torch = __import__("torch")
+        if self.dist.get_backend(self.group) == "gloo" and t.dim() and _gloo_needs_bytes(t.dtype):
+            # the fp16-split Gram operand is uint16 bit patterns: gather the bytes
+            return self.all_gather(t.contiguous().view(torch.uint8)).view(t.dtype), None
         if t.is_cuda and self.dist.get_backend(self.group) == "gloo":
             # rehearsal path (several ranks sharing one GPU): stage through the host
             return self.all_gather(t.cpu()).to(t.device), None

@@ -37,7 +37,8 @@ for n, d in [(int(a), int(b)) for a, b in shapes]:
         e0.record()
         os.environ["DAL_GRAM_SCHED"] = "0" if kind.endswith("s0") else "1"
         os.environ["DAL_GRAM_MT"] = "32" if "32" in kind else "16"
-        if kind == "sym":
+        os.environ["DAL_GRAM_ONE"] = "0" if kind == "sym0" else "1"
+        if kind.startswith("sym"):
             nb = st.n_pad // 256
             _lib.call("dal_gram_rowsum_sym", _ptr(sp), 0, nb, _ptr(sp), 0, 0, nb, nb, st.d_pad,
                       _ptr(acc), grid, _stream(dev))
@@ -68,6 +69,9 @@ for n, d in [(int(a), int(b)) for a, b in shapes]:
               f"max rel {float((err / canon.abs()).max()):.3e}  bound {bound:.3e}  "
               f"within={bool(float(err.max()) <= bound)}", flush=True)
     sk = [k for k in kinds if k.startswith("split")]
+    if "sym0" in kinds and "sym" in kinds:
+        print(f"   sym one-acc vs two-acc max |diff| (2^-32 units): "
+              f"{int((accs['sym'] - accs['sym0']).abs().max())}", flush=True)
     if "sym" in kinds:
         a2, _ = run("sym", grid=37)
         a3, _ = run("sym", grid=1000)

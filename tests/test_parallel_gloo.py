@@ -168,3 +168,43 @@ def test_other_column_ranges_cover_the_rest():
                 cols.update(range(c0, c1))
             own = set(range(rank * shard, (rank + 1) * shard))
             assert cols.isdisjoint(own) and cols | own == set(range(world * shard))
+
+
+def _comm_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        comm = parallel.TorchComm()
+        # fp16-split Gram operands travel as uint16 bit patterns (no gloo type)
+        u = (torch.arange(6, dtype=torch.int32) + 1000 * rank + 60000).to(torch.uint16).view(3, 2)
+        g = comm.all_gather(u)
+        # the symmetric Gram's global-length accumulator is reduce-scattered
+        acc = torch.arange(world * 4, dtype=torch.int64) * (rank + 1)
+        rs = comm.reduce_scatter_sum(acc)
+        q.put((rank, g.dtype == torch.uint16, g.to(torch.int32).numpy(), rs.numpy()))
+    except Exception as e:
+        q.put((rank, repr(e), None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_comm_unsigned_gather_and_reduce_scatter():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want_g = np.concatenate([np.arange(6).reshape(3, 2) + 1000 * r + 60000 for r in range(world)])
+    full = np.arange(world * 4) * sum(r + 1 for r in range(world))
+    for rank, is_u16, g, rs in res:
+        assert is_u16 is True, is_u16
+        assert np.array_equal(g, want_g)
+        assert np.array_equal(rs, full[rank * 4:(rank + 1) * 4])
