@@ -218,7 +218,7 @@ __global__ __launch_bounds__(kGramThreads, 1) void gram_rowsum_kernel(
     }
     const bool has_next = n_unit < u_end;
 
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA for `buf` landed
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // this wave's DMA for `buf` landed
     __syncthreads();  // ... for every wave; everyone finished reading buf^1
     stage(buf, has_next, stage_base(n_s));
     if (last_of_unit) finish_unit();

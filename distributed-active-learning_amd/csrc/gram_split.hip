@@ -39,10 +39,6 @@
 
 #include <stdlib.h>
 
-#ifndef DAL_ABL
-#define DAL_ABL 0  // timing ablations (scripts/gram_ablate.py): 1 no column sums, 2 no stage DMA
-#endif
-
 #include <type_traits>
 
 #include "common.hpp"
@@ -52,6 +48,7 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 #define AS3 __attribute__((address_space(3)))
 
 constexpr int kSpThreads = 256;    // 4 waves
@@ -267,14 +264,14 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_split_kernel(
     const bool has_next = n_unit < u_end;
 
     // stage 2*pr on buffer 0 (its DMA was issued one stage ago)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
     issue(1, 2 * pr + 1);
     compute(std::integral_constant<bool, true>{}, B0);
     if constexpr (C::FS == 1) fold();
 
     // stage 2*pr+1 on buffer 1
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
     if (has_next) issue(0, 2 * n_pr);
     compute(std::integral_constant<bool, C::FS == 1>{}, B1);
@@ -332,7 +329,7 @@ struct SymCfg {
   static_assert(NKS >= 1 && PIECES >= 1, "bad slice");
 };
 
-template <int KS, int MT, bool ONE>
+template <int KS, int MT, int SG>
 __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
     const uint16_t* __restrict__ urows, int row_block0, int n_rb,
     const uint16_t* __restrict__ ucols, int col_block0, int j_lo, int j_hi,
@@ -412,10 +409,10 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
     }
   };
 
-  // ONE: a single accumulator per tile carries 2^12 h_i.h_j + h_i.l_j + l_i.h_j
+  // A single accumulator per tile carries 2^12 h_i.h_j + h_i.l_j + l_i.h_j
   // (the hi rows pre-scaled by 2^12 -- exact in fp16 since |h| <= 1), so the
   // epilogue needs no combine step; sums are in units of 2^-12.
-  f16x8 ah[C::RT][C::NKS], al[C::RT][C::NKS], aH[ONE ? C::RT : 1][C::NKS];
+  f16x8 ah[C::RT][C::NKS], al[C::RT][C::NKS], aH[C::RT][C::NKS];
   auto load_a = [&](int I) {
 #pragma unroll
     for (int rt = 0; rt < C::RT; ++rt) {
@@ -428,15 +425,13 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
       }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);
-    if constexpr (ONE) {
-      const f16x8 k4096 = {4096, 4096, 4096, 4096, 4096, 4096, 4096, 4096};
+    const f16x8 k4096 = {4096, 4096, 4096, 4096, 4096, 4096, 4096, 4096};
 #pragma unroll
-      for (int rt = 0; rt < C::RT; ++rt)
+    for (int rt = 0; rt < C::RT; ++rt)
 #pragma unroll
-        for (int c = 0; c < C::NKS; ++c) aH[rt][c] = ah[rt][c] * k4096;
-    }
+      for (int c = 0; c < C::NKS; ++c) aH[rt][c] = ah[rt][c] * k4096;
   };
-  constexpr float kFold = ONE ? 0x1p20f : 0x1p32f;  // tile sums -> multiples of 2^-32
+  constexpr float kFold = 0x1p20f;  // tile sums (units of 2^-12) -> multiples of 2^-32
 
   int boh[C::NKS], bol[C::NKS];
 #pragma unroll
@@ -445,80 +440,163 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
     bol[c] = li * C::SLOTS + ((C::HI + c * C::LG + lq) ^ (li & C::SWZ));
   }
 
-  float racc[C::RT][C::NV];
+  // row accumulators as float pairs: the epilogue adds run as v_pk_add_f32
+  // (two lanes' worth per issue), half the VALU issue under the MFMAs
+  f32x2 racc[C::RT][C::NV / 2];
   double facc[C::RT][C::NV];
 #pragma unroll
-  for (int rt = 0; rt < C::RT; ++rt)
+  for (int rt = 0; rt < C::RT; ++rt) {
 #pragma unroll
-    for (int r = 0; r < C::NV; ++r) {
-      racc[rt][r] = 0.0f;
-      facc[rt][r] = 0.0;
-    }
+    for (int r = 0; r < C::NV / 2; ++r) racc[rt][r] = f32x2{0.0f, 0.0f};
+#pragma unroll
+    for (int r = 0; r < C::NV; ++r) facc[rt][r] = 0.0;
+  }
 
-  // one 128-column stage: per column tile, fresh accumulators -> row and column sums
-  auto compute = [&](const float4* B, bool cols_too, double* cacc) {
-    // software-pipelined: tile ct's MFMAs are issued before tile ct-1's
-    // epilogue (two accumulator sets), so the epilogue's VALU runs under them
-    acc_t m[2][C::RT], x[2][C::RT];
+  // one 128-column stage: per 16-column tile, a fresh accumulator per row tile
+  // -> row sums (racc) and the tile's column sums (-> LDS fp64, exact).
+  // Software-pipelined: tile ct's MFMAs are issued beside tile ct-1's epilogue
+  // (two accumulator sets) and tile ct+1's B fragments are read from LDS during
+  // tile ct.  The column-sum add is branch-free (scaled by 0 on the diagonal
+  // pair), so each tile is one scheduling region; SG interleaves it explicitly
+  // (one MFMA, then a B read or one epilogue VALU op, ...) instead of leaving
+  // the epilogue as a VALU burst between MFMA bursts.
+  auto compute = [&](const float4* B, float cmul, double* cacc) {
+    acc_t m[2][C::RT];
+    f16x8 bh[2][C::NKS], bl[2][C::NKS];
+    auto load_b = [&](int sb, int ct) {
+#pragma unroll
+      for (int c = 0; c < C::NKS; ++c) {
+        bh[sb][c] = __builtin_bit_cast(f16x8, B[ct * MT * C::SLOTS + boh[c]]);
+        bl[sb][c] = __builtin_bit_cast(f16x8, B[ct * MT * C::SLOTS + bol[c]]);
+      }
+    };
+    load_b(0, 0);
 #pragma unroll
     for (int ct = 0; ct <= C::NCT; ++ct) {
+      if (ct + 1 < C::NCT) load_b((ct + 1) & 1, ct + 1);
       if (ct < C::NCT) {
         const int st = ct & 1;
+        const acc_t zero = {};
 #pragma unroll
         for (int c = 0; c < C::NKS; ++c) {
-          const f16x8 bh = __builtin_bit_cast(f16x8, B[ct * MT * C::SLOTS + boh[c]]);
-          const f16x8 bl = __builtin_bit_cast(f16x8, B[ct * MT * C::SLOTS + bol[c]]);
-          const acc_t zero = {};
-          if constexpr (ONE) {
 #pragma unroll
-            for (int rt = 0; rt < C::RT; ++rt) m[st][rt] = A::mfma(aH[rt][c], bh, c == 0 ? zero : m[st][rt]);
+          for (int rt = 0; rt < C::RT; ++rt) m[st][rt] = A::mfma(aH[rt][c], bh[st][c], c == 0 ? zero : m[st][rt]);
 #pragma unroll
-            for (int rt = 0; rt < C::RT; ++rt) m[st][rt] = A::mfma(ah[rt][c], bl, m[st][rt]);
+          for (int rt = 0; rt < C::RT; ++rt) m[st][rt] = A::mfma(ah[rt][c], bl[st][c], m[st][rt]);
 #pragma unroll
-            for (int rt = 0; rt < C::RT; ++rt) m[st][rt] = A::mfma(al[rt][c], bh, m[st][rt]);
-          } else {
-#pragma unroll
-            for (int rt = 0; rt < C::RT; ++rt) m[st][rt] = A::mfma(ah[rt][c], bh, c == 0 ? zero : m[st][rt]);
-#pragma unroll
-            for (int rt = 0; rt < C::RT; ++rt) x[st][rt] = A::mfma(ah[rt][c], bl, c == 0 ? zero : x[st][rt]);
-#pragma unroll
-            for (int rt = 0; rt < C::RT; ++rt) x[st][rt] = A::mfma(al[rt][c], bh, x[st][rt]);
-          }
+          for (int rt = 0; rt < C::RT; ++rt) m[st][rt] = A::mfma(al[rt][c], bh[st][c], m[st][rt]);
         }
       }
       if (ct > 0) {
         const int pt = (ct - 1) & 1;
-        float cp = 0.0f;
+        f32x2 cp2 = {0.0f, 0.0f};
 #pragma unroll
         for (int rt = 0; rt < C::RT; ++rt) {
 #pragma unroll
-          for (int r = 0; r < C::NV; ++r) {
-            const float t = ONE ? m[pt][rt][r] : __builtin_fmaf(x[pt][rt][r], 0x1p-12f, m[pt][rt][r]);
+          for (int r = 0; r < C::NV / 2; ++r) {
+            const f32x2 t = {m[pt][rt][2 * r], m[pt][rt][2 * r + 1]};
             racc[rt][r] += t;
-            cp += t;
+            cp2 += t;
           }
         }
-#if DAL_ABL == 1
-        (void)cp; (void)cols_too; (void)cacc;
-#else
-        if (cols_too) atomicAdd(cacc + (ct - 1) * MT + li, static_cast<double>(__builtin_rintf(cp * kFold)));
-#endif
-        // pin the row accumulators here: otherwise LLVM sinks the adds to the
-        // fold and keeps every tile's values live (hundreds of spilled VGPRs)
+        const float cp = cp2.x + cp2.y;
+        atomicAdd(cacc + (ct - 1) * MT + li, static_cast<double>(__builtin_rintf(cp * cmul)));
+      }
+      {
+        constexpr int NM = 3 * C::NKS * C::RT;
 #pragma unroll
-        for (int rt = 0; rt < C::RT; ++rt)
+        for (int i = 0; i < NM; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+          if (i < 2 * C::NKS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read (next tile's B)
+          else __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);                   // VALU (epilogue)
+        }
+      }
+      // pin the row accumulators here: otherwise LLVM sinks the adds to the
+      // fold and keeps every tile's values live (hundreds of spilled VGPRs)
 #pragma unroll
-          for (int r = 0; r < C::NV; ++r) asm volatile("" : "+v"(racc[rt][r]));
+      for (int rt = 0; rt < C::RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < C::NV / 2; ++r) asm volatile("" : "+v"(racc[rt][r]));
+    }
+  };
+  // SG 2 ("chained"): the row sums ride in the MFMA accumulators.  Two
+  // accumulator chains per row tile (even / odd column tiles) run through the
+  // whole 256-column pair, so the MFMAs themselves add each tile into the row
+  // sums (no per-element VALU add).  A tile's column sums are the growth of its
+  // chain's lane total: T = sum of the lane's 16 values after the tile, minus T
+  // before it (same column lane, the previous tile of that chain) -- one add
+  // per element instead of two.  The epilogue of tile ct-1 (other chain) runs
+  // beside tile ct's MFMAs and the B reads of tile ct+1.
+  acc_t mc[2][C::RT];
+  float tprev[2];
+  auto compute_chained = [&](const float4* B, float cmul, double* cacc, bool first_stage) {
+    f16x8 bh[2][C::NKS], bl[2][C::NKS];
+    auto load_b = [&](int sb, int ct) {
+#pragma unroll
+      for (int c = 0; c < C::NKS; ++c) {
+        bh[sb][c] = __builtin_bit_cast(f16x8, B[ct * MT * C::SLOTS + boh[c]]);
+        bl[sb][c] = __builtin_bit_cast(f16x8, B[ct * MT * C::SLOTS + bol[c]]);
+      }
+    };
+    load_b(0, 0);
+#pragma unroll
+    for (int ct = 0; ct <= C::NCT; ++ct) {
+      if (ct + 1 < C::NCT) load_b((ct + 1) & 1, ct + 1);
+      if (ct < C::NCT) {
+        const int ch = ct & 1;
+        const bool fresh = first_stage && ct < 2;  // first tile of the chain in this pair
+#pragma unroll
+        for (int c = 0; c < C::NKS; ++c) {
+          const acc_t zero = {};
+#pragma unroll
+          for (int rt = 0; rt < C::RT; ++rt)
+            mc[ch][rt] = A::mfma(aH[rt][c], bh[ch][c], (c == 0 && fresh) ? zero : mc[ch][rt]);
+#pragma unroll
+          for (int rt = 0; rt < C::RT; ++rt) mc[ch][rt] = A::mfma(ah[rt][c], bl[ch][c], mc[ch][rt]);
+#pragma unroll
+          for (int rt = 0; rt < C::RT; ++rt) mc[ch][rt] = A::mfma(al[rt][c], bh[ch][c], mc[ch][rt]);
+        }
+      }
+      if (ct > 0) {
+        const int ch = (ct - 1) & 1;
+        float t0 = 0.0f, t1 = 0.0f;  // two short chains (latency), fixed order
+#pragma unroll
+        for (int rt = 0; rt < C::RT; ++rt) {
+#pragma unroll
+          for (int r = 0; r < C::NV; r += 2) {
+            t0 += mc[ch][rt][r];
+            t1 += mc[ch][rt][r + 1];
+          }
+        }
+        const float T = t0 + t1;
+        const float cp = (first_stage && ct - 1 < 2) ? T : T - tprev[ch];
+        tprev[ch] = T;
+        atomicAdd(cacc + (ct - 1) * MT + li, static_cast<double>(__builtin_rintf(cp * cmul)));
+      }
+      constexpr int NM = 3 * C::NKS * C::RT;
+#pragma unroll
+      for (int i = 0; i < NM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        if (i < 2 * C::NKS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read (next tile's B)
+        else __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);                   // VALU (epilogue)
       }
     }
   };
+  auto fold_chains = [&]() {
+#pragma unroll
+    for (int rt = 0; rt < C::RT; ++rt)
+#pragma unroll
+      for (int r = 0; r < C::NV; ++r)
+        facc[rt][r] += static_cast<double>(__builtin_rintf((mc[0][rt][r] + mc[1][rt][r]) * kFold));
+  };
+
   auto fold_rows = [&]() {
 #pragma unroll
     for (int rt = 0; rt < C::RT; ++rt)
 #pragma unroll
       for (int r = 0; r < C::NV; ++r) {
-        facc[rt][r] += static_cast<double>(__builtin_rintf(racc[rt][r] * kFold));
-        racc[rt][r] = 0.0f;
+        facc[rt][r] += static_cast<double>(__builtin_rintf(racc[rt][r / 2][r % 2] * kFold));
+        racc[rt][r / 2][r % 2] = 0.0f;
       }
   };
   auto finish_unit = [&](int I) {
@@ -571,21 +649,28 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
     const bool last_of_unit = n_unit != unit;
     const bool cols_too = J != I;
 
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const float cmul = cols_too ? kFold : 0.0f;  // diagonal pair: row sums only
+
+    // lgkmcnt(0): the previous pair's LDS column adds (no-return ds_add_f64)
+    // must land before another wave's flush reads them.  hipcc emits no LDS
+    // wait at this loop-top barrier (measured: a lost tile partial, rarely)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
     if (flushJ >= 0) flush_cols(cb ^ 1, flushJ);
-#if DAL_ABL != 2
     issue(1, J, 1);
-#endif
-    compute(B0, cols_too, &colacc[cb][0]);
+    if constexpr (SG == 2) compute_chained(B0, cmul, &colacc[cb][0], true);
+    else compute(B0, cmul, &colacc[cb][0]);
 
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
-#if DAL_ABL != 2
     if (has_next) issue(0, nJ, 0);
-#endif
-    compute(B1, cols_too, &colacc[cb][C::SC]);
-    fold_rows();
+    if constexpr (SG == 2) {
+      compute_chained(B1, cmul, &colacc[cb][C::SC], false);
+      fold_chains();
+    } else {
+      compute(B1, cmul, &colacc[cb][C::SC]);
+      fold_rows();
+    }
     flushJ = cols_too ? J : -1;
     cb ^= 1;
     if (last_of_unit) finish_unit(I);
@@ -699,7 +784,7 @@ int launch_split(const uint16_t* rows, int64_t n_rows_pad, const uint16_t* cols,
   return DAL_OK;
 }
 
-template <int KS, int MT, bool ONE>
+template <int KS, int MT, int SG>
 int launch_sym(const uint16_t* rows, int64_t row_block0, int64_t n_rb, const uint16_t* cols,
                int64_t col_block0, int64_t j_lo, int64_t j_hi, int64_t nb_active, int64_t ldh,
                int slice_off, int64_t* acc, int grid_blocks, hipStream_t stream) {
@@ -728,7 +813,7 @@ int launch_sym(const uint16_t* rows, int64_t row_block0, int64_t n_rb, const uin
   const int64_t n_chunks = ceil_div(nj, cbk);
   const int64_t n_units = n_rb * n_chunks;
   const int64_t G = n_units < G0 ? n_units : G0;
-  hipLaunchKernelGGL((gram_sym_kernel<KS, MT, ONE>), dim3(static_cast<unsigned>(G)), dim3(kSpThreads), 0, stream,
+  hipLaunchKernelGGL((gram_sym_kernel<KS, MT, SG>), dim3(static_cast<unsigned>(G)), dim3(kSpThreads), 0, stream,
                      rows, static_cast<int>(row_block0), static_cast<int>(n_rb), cols,
                      static_cast<int>(col_block0), static_cast<int>(j_lo), static_cast<int>(j_hi),
                      static_cast<int>(nb_active), ldh, slice_off, static_cast<int>(cbk),
@@ -757,6 +842,27 @@ extern "C" double dal_density_error_bound_split(int64_t n_cols) {
   const double gamma = 1088.0 * u / (1.0 - 1088.0 * u);
   const double s = 1.0 / 4194304.0;  // 2^-22
   return (gamma * (1.0 + 1.0 / 512.0) + 5.0 * s + 1e-10) * static_cast<double>(n_cols) + 1e-9;
+}
+
+extern "C" double dal_density_error_bound_sym(int64_t n_cols) {
+  // dal_gram_rowsum_sym (chained epilogue; also covers the per-tile one).  With
+  // u = 2^-23 (conservative for the MFMA's internal fp32 adds), products exact
+  // (f16 x f16), and c = 1 + 2^-8 >= sum_d |h_i h_j| + |h_i l_j| + |l_i h_j| over
+  // sum_d |u_i u_j| <= 1 (Cauchy-Schwarz on unit rows), per density entry:
+  //   row side   two chains of <= 8 tiles x 192 products, joined by one add:
+  //              gamma_1537 * c per column
+  //   column side  a tile's column partial is T_k - T_{k-1}, T = sum of the
+  //              lane's 16 chain values (k <= 8 tiles into the chain):
+  //              (8 gamma_192 + 15 gamma_15 + u) * c per row
+  //   split + fp32 unit rows  5 * 2^-22;  fixed-point roundings <= 2^-33 each
+  // Every column j of a row's density lies on exactly one side of its pair.
+  const double u = 1.0 / 8388608.0;  // 2^-23
+  auto gamma = [u](double n) { return n * u / (1.0 - n * u); };
+  const double row = gamma(1537.0);
+  const double col = 8.0 * gamma(192.0) + 15.0 * gamma(15.0) + u;
+  const double c = 1.0 + 1.0 / 256.0;
+  const double s = 1.0 / 4194304.0;  // 2^-22
+  return ((row > col ? row : col) * c + 5.0 * s + 1e-10) * static_cast<double>(n_cols) + 1e-9;
 }
 
 extern "C" int64_t dal_split_f16_halves(int64_t n_pad, int64_t d_pad) { return n_pad * 2 * d_pad; }
@@ -816,19 +922,20 @@ extern "C" int dal_gram_rowsum_sym(const uint16_t* rows, int64_t row_block0, int
   const int64_t ldh = 2 * d_pad;
   for (int64_t off = 0; off < d_pad; off += ks) {
     const int so = static_cast<int>(2 * off);
-    const char* env = getenv("DAL_GRAM_ONE");
-    const bool one = env ? atoi(env) != 0 : true;
+    // epilogue variant (A/B knob): 2 = chained accumulators (default), 1 = per-tile
+    const char* env = getenv("DAL_GRAM_SG");
+    const int sg = env ? atoi(env) : 2;
     int rc;
-    if (one)
-      rc = ks == 32 ? launch_sym<32, 16, true>(rows, row_block0, n_row_blocks, cols, col_block0, j_lo, j_hi,
-                                               nb_active, ldh, so, acc, grid_blocks, st)
-                    : launch_sym<64, 16, true>(rows, row_block0, n_row_blocks, cols, col_block0, j_lo, j_hi,
-                                               nb_active, ldh, so, acc, grid_blocks, st);
+    if (sg == 1)
+      rc = ks == 32 ? launch_sym<32, 16, 1>(rows, row_block0, n_row_blocks, cols, col_block0, j_lo, j_hi,
+                                            nb_active, ldh, so, acc, grid_blocks, st)
+                    : launch_sym<64, 16, 1>(rows, row_block0, n_row_blocks, cols, col_block0, j_lo, j_hi,
+                                            nb_active, ldh, so, acc, grid_blocks, st);
     else
-      rc = ks == 32 ? launch_sym<32, 16, false>(rows, row_block0, n_row_blocks, cols, col_block0, j_lo, j_hi,
-                                                nb_active, ldh, so, acc, grid_blocks, st)
-                    : launch_sym<64, 16, false>(rows, row_block0, n_row_blocks, cols, col_block0, j_lo, j_hi,
-                                                nb_active, ldh, so, acc, grid_blocks, st);
+      rc = ks == 32 ? launch_sym<32, 16, 2>(rows, row_block0, n_row_blocks, cols, col_block0, j_lo, j_hi,
+                                            nb_active, ldh, so, acc, grid_blocks, st)
+                    : launch_sym<64, 16, 2>(rows, row_block0, n_row_blocks, cols, col_block0, j_lo, j_hi,
+                                            nb_active, ldh, so, acc, grid_blocks, st);
     if (rc != DAL_OK) return rc;
   }
   return DAL_OK;

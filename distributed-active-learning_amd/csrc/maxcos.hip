@@ -149,7 +149,7 @@ __global__ __launch_bounds__(kMcThreads, OCC) void maxcos2_kernel(
 
   auto stage_body = [&](auto bufc, int st) {
     constexpr int buf = decltype(bufc)::value;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
     if (st + 1 < n_stages) issue(buf ^ 1, st + 1);
     const float4* B = lds + buf * C::F4;
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(kMcThreads, OCC) void maxcos2_kernel(
   };
   auto stage_body_rt = [&](int st) {
     const int buf = st & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
     if (st + 1 < n_stages) issue(buf ^ 1, st + 1);
     const float4* B = lds + buf * C::F4;

@@ -53,6 +53,7 @@ SIGNATURES = {
     "dal_gram_rowsum_split": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_void_p, c_int,
                                       c_void_p]),
     "dal_density_error_bound_split": (c_double, [c_int64]),
+    "dal_density_error_bound_sym": (c_double, [c_int64]),
     "dal_gram_rowsum_sym": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64, c_int64,
                                     c_int64, c_int64, c_void_p, c_int, c_void_p]),
     "dal_forest_score": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32,

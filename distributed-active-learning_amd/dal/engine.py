@@ -387,13 +387,14 @@ def topk_keys(keys, k: int, idx_base: int = 0):
 
 
 def density_error(state: PoolState) -> float:
-    """Bound on |d_gemm - d_canonical| (rigorous; dal_density_error_bound or
-    dal_density_error_bound_split, by the pool's Gram kernel)."""
+    """Bound on |d_gemm - d_canonical| (rigorous; dal_density_error_bound,
+    _split or _sym, by the pool's Gram kernel)."""
     n_cols = max(state.n_total - state.n_excluded_global(), 1)
     lib = _lib.load()
     if state.gram == "f32":
         return float(lib.dal_density_error_bound(n_cols))
-    # "split" and "sym": same per-entry arithmetic and fold structure
+    if state.gram == "sym":
+        return float(lib.dal_density_error_bound_sym(n_cols))
     return float(lib.dal_density_error_bound_split(n_cols))
 
 

@@ -159,12 +159,18 @@ double dal_density_error_bound_split(int64_t n_cols);
  * [j_lo, j_hi) are processed (j_hi <= nb_active = pad512(N_total) / 256), so
  * a caller can split the columns over several calls.  acc is indexed by
  * GLOBAL row (>= nb_active * 256 entries, zeroed by the caller); on several
- * GPUs the per-rank accs are summed (reduce-scatter).  Same rounding
- * structure and bound as dal_gram_rowsum_split (dal_density_error_bound_split). */
+ * GPUs the per-rank accs are summed (reduce-scatter).  Per 16x16 tile the
+ * three products share one fp32 accumulator; the row sums ride in two MFMA
+ * accumulator chains per pair (even / odd column tiles) and a tile's column
+ * sums are the growth of its chain's lane total.  Each pair's sums are rounded
+ * to multiples of 2^-32 and added exactly (int64), so the bits do not depend on
+ * the grid, the column split or the GPU count.  Rigorous bound on
+ * |d - d_canonical|: dal_density_error_bound_sym. */
 int dal_gram_rowsum_sym(const uint16_t* rows, int64_t row_block0, int64_t n_row_blocks,
                         const uint16_t* cols, int64_t col_block0, int64_t j_lo, int64_t j_hi,
                         int64_t nb_active, int64_t d_pad, int64_t* acc, int grid_blocks,
                         dal_stream_t stream);
+double dal_density_error_bound_sym(int64_t n_cols);
 
 /* ---- (a5-a10) forest votes + uncertainty / density-weighted score ------
  * Replaces uncertainty_sampling.py:88-98 / density_weighting.py:136-167:

@@ -37,7 +37,10 @@ for n, d in [(int(a), int(b)) for a, b in shapes]:
         e0.record()
         os.environ["DAL_GRAM_SCHED"] = "0" if kind.endswith("s0") else "1"
         os.environ["DAL_GRAM_MT"] = "32" if "32" in kind else "16"
-        os.environ["DAL_GRAM_ONE"] = "0" if kind == "sym0" else "1"
+        if kind.startswith("symsg"):
+            os.environ["DAL_GRAM_SG"] = kind[5:]
+        else:
+            os.environ.pop("DAL_GRAM_SG", None)
         if kind.startswith("sym"):
             nb = st.n_pad // 256
             _lib.call("dal_gram_rowsum_sym", _ptr(sp), 0, nb, _ptr(sp), 0, 0, nb, nb, st.d_pad,
@@ -62,20 +65,22 @@ for n, d in [(int(a), int(b)) for a, b in shapes]:
     for kind in kinds:
         dk = accs[kind][10:n].to(torch.float64) / 2.0**32
         err = (dk - canon).abs()
-        bound = (lib.dal_density_error_bound if kind.startswith("f32") else lib.dal_density_error_bound_split)(n - 10)
+        bound = (lib.dal_density_error_bound if kind.startswith("f32") else
+                 lib.dal_density_error_bound_sym if kind.startswith("sym") else lib.dal_density_error_bound_split)(n - 10)
         ms = float(np.median(t[kind]))
         print(f"n={n} d={d} {kind:6s} median {ms:8.3f} ms  {flops / ms / 1e9:7.1f} TF/s "
               f"({100 * flops / ms / 1e9 / 157.3:5.1f}% of fp32 peak)  max|err| {float(err.max()):.3e} "
               f"max rel {float((err / canon.abs()).max()):.3e}  bound {bound:.3e}  "
               f"within={bool(float(err.max()) <= bound)}", flush=True)
     sk = [k for k in kinds if k.startswith("split")]
-    if "sym0" in kinds and "sym" in kinds:
-        print(f"   sym one-acc vs two-acc max |diff| (2^-32 units): "
-              f"{int((accs['sym'] - accs['sym0']).abs().max())}", flush=True)
-    if "sym" in kinds:
-        a2, _ = run("sym", grid=37)
-        a3, _ = run("sym", grid=1000)
-        print(f"   sym grid-invariant: {torch.equal(a2, accs['sym']) and torch.equal(a3, accs['sym'])}",
+    for kk in [k for k in kinds if k.startswith("symsg")]:
+        if "sym" in kinds:
+            print(f"   sym vs {kk}: same bits {torch.equal(accs['sym'], accs[kk])}, max |diff| "
+                  f"{int((accs['sym'] - accs[kk]).abs().max())} (2^-32 units)", flush=True)
+    for kk in [k for k in kinds if k.startswith("sym")]:
+        a2, _ = run(kk, grid=37)
+        a3, _ = run(kk, grid=1000)
+        print(f"   {kk} grid-invariant: {torch.equal(a2, accs[kk]) and torch.equal(a3, accs[kk])}",
               flush=True)
     if len(sk) > 1:
         print(f"   all split variants same bits: {all(torch.equal(accs[sk[0]], accs[k]) for k in sk)}",

@@ -45,6 +45,8 @@ def test_host_helpers():
     assert 1.0 < b < 10.0  # ~3.1e-5 * N
     bs = lib.dal_density_error_bound_split(100000)
     assert b < bs < 20.0  # ~1.25e-4 * N (conservative MFMA accumulation model)
+    bsym = lib.dal_density_error_bound_sym(100000)
+    assert bs < bsym < 30.0  # ~2.1e-4 * N (chained accumulators: longer fp32 chains)
     assert lib.dal_split_f16_halves(512, 64) == 512 * 128
     assert lib.dal_topk_workspace_bytes(1 << 21, 1000) > 0
 
