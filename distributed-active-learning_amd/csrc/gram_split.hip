@@ -541,7 +541,11 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
     load_b(0, 0);
 #pragma unroll
     for (int ct = 0; ct <= C::NCT; ++ct) {
+      // the next tile's B reads go out first and are fenced there, so their
+      // latency hides under this tile's MFMAs (left alone, the scheduler
+      // sinks them to their use and each tile starts with an LDS wait)
       if (ct + 1 < C::NCT) load_b((ct + 1) & 1, ct + 1);
+      __builtin_amdgcn_sched_barrier(0);
       if (ct < C::NCT) {
         const int ch = ct & 1;
         const bool fresh = first_stage && ct < 2;  // first tile of the chain in this pair
@@ -559,11 +563,11 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
       }
       if (ct > 0) {
         const int ch = (ct - 1) & 1;
-        float t0 = 0.0f, t1 = 0.0f;  // two short chains (latency), fixed order
+        float t0 = mc[ch][0][0], t1 = mc[ch][0][1];  // two short chains (latency), fixed order
 #pragma unroll
         for (int rt = 0; rt < C::RT; ++rt) {
 #pragma unroll
-          for (int r = 0; r < C::NV; r += 2) {
+          for (int r = rt == 0 ? 2 : 0; r < C::NV; r += 2) {
             t0 += mc[ch][rt][r];
             t1 += mc[ch][rt][r + 1];
           }
@@ -577,9 +581,9 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
 #pragma unroll
       for (int i = 0; i < NM; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        if (i < 2 * C::NKS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read (next tile's B)
-        else __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);                   // VALU (epilogue)
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // VALU (previous tile's epilogue)
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
   auto fold_chains = [&]() {
