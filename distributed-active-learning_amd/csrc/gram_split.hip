@@ -6,20 +6,21 @@
 // IndexedRowMatrix/BlockMatrix), :95-100 (drop i,j in L0) and :157-161
 // (groupByKey + sum per row); cosine_similarity.py:29-45 is the same product.
 //
-// Split.  Every normalised fp32 component u (|u| <= 1) is written as
-//   h = fp16_rn(u),   l = fp16_rn((u - h) * 2^12)     (u - h is exact in fp32)
-// so u = h + l*2^-12 + e with |e| <= 2^-22 |u| (+2^-37 absolute when h or l
-// is subnormal).  Then
-//   u_i.u_j = h_i.h_j + 2^-12 (h_i.l_j + l_i.h_j) + O(3 * 2^-22 |u_i||u_j|)
-// and fp16 x fp16 products are exact in fp32.  Three v_mfma_f32_32x32x16_f16
-// per 16 features replace eight v_mfma_f32_32x32x2_f32 per 16 features:
-// 96 vs 512 SIMD cycles, 5.3x the fp32-MFMA rate at equal accuracy class.
-// Two accumulators per row tile: M (h.h, the large term) and X (the cross
-// terms, scaled by 2^12, ~2^-10 of M), so M's fp32 chain carries 512
-// products per fold exactly like the fp32 kernel's.
+// Split.  Every normalised fp32 component u (|u| <= 1) is scaled by 2^12
+// (exact) and written as two fp16 terms at that same scale:
+//   H = fp16_rn(2^12 u),   L = fp16_rn(2^12 u - H)   (the difference is exact in fp32)
+// so 2^12 u = H + L + e with |e| <= 2^-22 |2^12 u| (+2^-25 absolute when L is
+// subnormal).  Then
+//   2^24 u_i.u_j = H_i.H_j + H_i.L_j + L_i.H_j + O(3 * 2^-22 |2^12 u_i||2^12 u_j|)
+// with every fp16 x fp16 product exact in fp32 and all three products in the
+// SAME units (2^-24), so they can share one fp32 accumulator.  Three
+// v_mfma_f32_16x16x32_f16 per 32 features replace sixteen
+// v_mfma_f32_16x16x4_f32: 48 vs 512 SIMD cycles, ~10x the fp32-MFMA rate at
+// equal accuracy class.  This kernel keeps two accumulators per row tile: M
+// (H.H, the large term) and X (the cross terms, ~2^-11 of M).
 //
 // Exactness of the row sums is kept from gram.hip: per 256-column fold group
-// each lane's partial v = fma(X, 2^-12, M) is rounded to a multiple of 2^-32
+// each lane's partial v = M + X (units 2^-24) is rounded to a multiple of 2^-32
 // and added into an fp64 register (integer arithmetic below 2^53); units end
 // in int64 atomics.  Fold groups sit at fixed column positions (multiples of
 // 256), so the density is bit-identical for any grid, unit split, column
@@ -40,6 +41,7 @@
 #include <stdlib.h>
 
 #include <type_traits>
+#include <vector>
 
 #include "common.hpp"
 
@@ -98,8 +100,9 @@ struct SpAcc<16> {
   static __device__ __forceinline__ int row(int r, int q) { return 4 * q + r; }
 };
 
-__device__ __forceinline__ double fold_fixed(float v) {
-  return static_cast<double>(__builtin_rintf(v * 4294967296.0f));
+// a partial in units of 2^-24 -> exact fp64 integer in units of 2^-32
+__device__ __forceinline__ double fold_fixed24(float v) {
+  return static_cast<double>(__builtin_rintf(v * 256.0f));
 }
 
 template <int KS, int MT>
@@ -219,7 +222,7 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_split_kernel(
 #pragma unroll
     for (int rt = 0; rt < C::RT; ++rt)
 #pragma unroll
-      for (int r = 0; r < C::NV; ++r) facc[rt][r] += fold_fixed(__builtin_fmaf(x[rt][r], 0x1p-12f, m[rt][r]));
+      for (int r = 0; r < C::NV; ++r) facc[rt][r] += fold_fixed24(m[rt][r] + x[rt][r]);
   };
 
   auto finish_unit = [&]() {
@@ -302,7 +305,7 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_split_kernel(
 // Every row block then takes ~nb/2 column blocks, so work is balanced across
 // row blocks, units and row-sharded GPUs.  Column block = fold group = one
 // pair of 128-column stages.  Per 16x16 (or 32x32) output tile the per-tile
-// accumulators are combined on the VALU: t = fma(X, 2^-12, M) is added into
+// accumulators are combined on the VALU: t = M + X is added into
 // the fp32 row accumulator (the same 16-tile chain per fold as the asymmetric
 // kernel) and summed over the lane's rows into a column partial, which is
 // rounded to a multiple of 2^-32 and added into an LDS fp64 column
@@ -409,10 +412,9 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
     }
   };
 
-  // A single accumulator per tile carries 2^12 h_i.h_j + h_i.l_j + l_i.h_j
-  // (the hi rows pre-scaled by 2^12 -- exact in fp16 since |h| <= 1), so the
-  // epilogue needs no combine step; sums are in units of 2^-12.
-  f16x8 ah[C::RT][C::NKS], al[C::RT][C::NKS], aH[C::RT][C::NKS];
+  // A single accumulator per tile carries H_i.H_j + H_i.L_j + L_i.H_j (all in
+  // units of 2^-24), so the epilogue needs no combine step.
+  f16x8 ah[C::RT][C::NKS], al[C::RT][C::NKS];
   auto load_a = [&](int I) {
 #pragma unroll
     for (int rt = 0; rt < C::RT; ++rt) {
@@ -425,13 +427,8 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
       }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);
-    const f16x8 k4096 = {4096, 4096, 4096, 4096, 4096, 4096, 4096, 4096};
-#pragma unroll
-    for (int rt = 0; rt < C::RT; ++rt)
-#pragma unroll
-      for (int c = 0; c < C::NKS; ++c) aH[rt][c] = ah[rt][c] * k4096;
   };
-  constexpr float kFold = 0x1p20f;  // tile sums (units of 2^-12) -> multiples of 2^-32
+  constexpr float kFold = 0x1p8f;  // tile sums (units of 2^-24) -> multiples of 2^-32
 
   int boh[C::NKS], bol[C::NKS];
 #pragma unroll
@@ -480,7 +477,7 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
 #pragma unroll
         for (int c = 0; c < C::NKS; ++c) {
 #pragma unroll
-          for (int rt = 0; rt < C::RT; ++rt) m[st][rt] = A::mfma(aH[rt][c], bh[st][c], c == 0 ? zero : m[st][rt]);
+          for (int rt = 0; rt < C::RT; ++rt) m[st][rt] = A::mfma(ah[rt][c], bh[st][c], c == 0 ? zero : m[st][rt]);
 #pragma unroll
           for (int rt = 0; rt < C::RT; ++rt) m[st][rt] = A::mfma(ah[rt][c], bl[st][c], m[st][rt]);
 #pragma unroll
@@ -554,7 +551,7 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
           const acc_t zero = {};
 #pragma unroll
           for (int rt = 0; rt < C::RT; ++rt)
-            mc[ch][rt] = A::mfma(aH[rt][c], bh[ch][c], (c == 0 && fresh) ? zero : mc[ch][rt]);
+            mc[ch][rt] = A::mfma(ah[rt][c], bh[ch][c], (c == 0 && fresh) ? zero : mc[ch][rt]);
 #pragma unroll
           for (int rt = 0; rt < C::RT; ++rt) mc[ch][rt] = A::mfma(ah[rt][c], bl[ch][c], mc[ch][rt]);
 #pragma unroll
@@ -692,6 +689,314 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
   if (flushJ >= 0) flush_cols(cb ^ 1, flushJ);
 }
 
+// ---------------------------------------------------------------------------
+// Symmetric kernel on 512-row super blocks (SYM2, the default).  Same per-tile
+// arithmetic as gram_sym_kernel (three products in one accumulator, row sums
+// chained in the MFMA accumulators, column sums from the growth of the chain's
+// lane total), but each wave owns 128 rows (8 row tiles): every B fragment
+// read from LDS feeds twice the MFMAs, every LDS-DMA'd stage serves 512 rows,
+// and the per-pair column flush is spread over twice the rows.  Orientation on
+// super blocks (512 rows = the row granule, so shard-independent): super block
+// P takes super block Q when Q == P (diagonal: row sums only, all columns),
+// Q > P and P+Q even, Q < P and P+Q odd.  A pair is 512 x 512 = four
+// 128-column stages; the chains are folded every two stages (256 columns: the
+// chain lengths, and so the error bound, of gram_sym_kernel) into an LDS fp64
+// row accumulator of exact integers, flushed to the int64 output per unit.
+template <int KS>
+struct Sym2Cfg {
+  static constexpr int MT = 16;
+  static constexpr int ROWB = KS * 4;                 // bytes per column row (H + L)
+  static constexpr int SLOTS = ROWB / 16;
+  static constexpr int HI = KS / 8;
+  static constexpr int SC = 128;                      // columns per stage
+  static constexpr int STAGE = SC * ROWB;             // 32 KiB (KS 64) or 16 KiB (KS 32)
+  static constexpr int F4 = STAGE / 16;
+  static constexpr int SWZ = (SLOTS < 16 ? SLOTS : 16) - 1;
+  static constexpr int PIECES = STAGE / (4 * 1024);   // 1-KiB DMA pieces per wave per stage
+  static constexpr int RT = 8;                        // 16-row tiles per wave (128 rows)
+  static constexpr int LG = 4;
+  static constexpr int NKS = KS / 32;                 // k-steps of v_mfma_f32_16x16x32_f16
+  static constexpr int NCT = SC / MT;                 // column tiles per stage
+  static constexpr int NV = 4;                        // accumulator values per lane
+  static constexpr int SB = 512;                      // super block
+  static_assert(NKS >= 1 && PIECES >= 1, "bad slice");
+};
+
+template <int KS>
+__global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
+    const uint16_t* __restrict__ urows, int srow0, int n_srb,
+    const uint16_t* __restrict__ ucols, int scol0, int q_lo, int q_hi,
+    int ns_active, int64_t ldh, int slice_off, int chunk_sb, int n_chunks,
+    unsigned long long* __restrict__ acc_out) {
+  using C = Sym2Cfg<KS>;
+  using A = SpAcc<16>;
+  using acc_t = A::type;
+  __shared__ __attribute__((aligned(16))) float4 lds[2 * C::F4];
+  __shared__ double colacc[2][C::SB];
+  __shared__ double rowacc[C::SB];
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int li = lane & 15, lq = lane >> 4;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int n_units = n_srb * n_chunks;
+
+  colacc[0][tid] = 0.0;
+  colacc[0][tid + 256] = 0.0;
+  colacc[1][tid] = 0.0;
+  colacc[1][tid + 256] = 0.0;
+  rowacc[tid] = 0.0;
+  rowacc[tid + 256] = 0.0;
+
+  // unit u (chunk-major, dealt round-robin): super block P, column super blocks [lo, hi)
+  auto unit_P = [&](int u) { return srow0 + u % n_srb; };
+  auto unit_qlo = [&](int u) { return q_lo + (u / n_srb) * chunk_sb; };
+  auto unit_qhi = [&](int u) {
+    const int e = q_lo + (u / n_srb + 1) * chunk_sb;
+    return e < q_hi ? e : q_hi;
+  };
+  auto first_Q = [&](int P, int lo, int hi) -> int {
+    if (P >= ns_active) return -1;
+    int Q = lo;
+    if (Q < P) {
+      if (((P + Q) & 1) == 0) ++Q;  // Q < P needs P+Q odd (Q may become P)
+    } else if (Q > P) {
+      if ((P + Q) & 1) ++Q;         // Q > P needs P+Q even
+    }
+    return Q < hi ? Q : -1;
+  };
+  auto next_Q = [&](int P, int Q, int hi) -> int {
+    const int n = (Q == P - 1) ? P : Q + 2;
+    return n < hi ? n : -1;
+  };
+  auto seek = [&](int u, int& Q) {
+    while (u < n_units) {
+      Q = first_Q(unit_P(u), unit_qlo(u), unit_qhi(u));
+      if (Q >= 0) break;
+      u += G;
+    }
+    return u;
+  };
+
+  // per-piece source offsets are recomputed at each issue (registers are the
+  // scarce resource here, VALU issue is not)
+  auto voff = [&](int q) {
+    const int p = (wave * C::PIECES + q) * 64 + lane;
+    const int row = p / C::SLOTS;
+    const int slot = (p % C::SLOTS) ^ (row & C::SWZ);
+    return static_cast<unsigned>(row * ldh * 2 + slot * 16);
+  };
+  const unsigned dst0 = __builtin_amdgcn_readfirstlane(
+      static_cast<unsigned>(reinterpret_cast<uintptr_t>((AS3 float4*)(lds + wave * C::PIECES * 64))));
+  // stage h (0..3) of column super block Q into buffer buf
+  auto issue = [&](int buf, int Q, int h) {
+    const uint16_t* sbase =
+        ucols + (static_cast<int64_t>(Q - scol0) * C::SB + h * C::SC) * ldh + slice_off;
+#pragma unroll
+    for (int q = 0; q < C::PIECES; ++q) {
+      const unsigned dst = dst0 + static_cast<unsigned>(buf * C::STAGE + q * 1024);
+      unsigned keep;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+          "global_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "v"(voff(q)), "s"(dst), "s"(sbase)
+          : "memory");
+    }
+  };
+
+  f16x8 ah[C::RT][C::NKS], al[C::RT][C::NKS];
+  auto load_a = [&](int P) {
+    // uniform 64-bit base + 32-bit per-lane offsets (no per-tile 64-bit addresses)
+    const uint16_t* pb = urows + static_cast<int64_t>(P - srow0) * C::SB * ldh + slice_off;
+    const unsigned lrow = static_cast<unsigned>((wave * 128 + li) * ldh + lq * 8);
+    const unsigned tstep = static_cast<unsigned>(16 * ldh);
+#pragma unroll
+    for (int rt = 0; rt < C::RT; ++rt) {
+#pragma unroll
+      for (int c = 0; c < C::NKS; ++c) {
+        const unsigned o = lrow + rt * tstep + c * C::LG * 8;
+        ah[rt][c] = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(pb + o));
+        al[rt][c] = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(pb + o + KS));
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+  };
+  constexpr float kFold = 0x1p8f;  // units of 2^-24 -> multiples of 2^-32
+
+  int boh[C::NKS], bol[C::NKS];
+#pragma unroll
+  for (int c = 0; c < C::NKS; ++c) {
+    boh[c] = li * C::SLOTS + ((c * C::LG + lq) ^ (li & C::SWZ));
+    bol[c] = li * C::SLOTS + ((C::HI + c * C::LG + lq) ^ (li & C::SWZ));
+  }
+
+  acc_t mc[2][C::RT];
+  float tprev[2];
+  // one 128-column stage; fresh = first stage after a fold (chains restart)
+  // (LDS operands are addressed by index, never through generic pointers:
+  // 64-bit flat addresses would cost registers this kernel does not have)
+  auto compute = [&](int buf, float cmul, int cbuf, int col0, bool fresh_stage) {
+    // one register set of B fragments: k-step c of tile ct+1 is read as soon as
+    // tile ct's MFMAs of k-step c are issued (24 MFMAs of latency cover)
+    f16x8 bh[C::NKS], bl[C::NKS];
+    auto load_b = [&](int c, int ct) {
+      bh[c] = __builtin_bit_cast(f16x8, lds[buf * C::F4 + ct * 16 * C::SLOTS + boh[c]]);
+      bl[c] = __builtin_bit_cast(f16x8, lds[buf * C::F4 + ct * 16 * C::SLOTS + bol[c]]);
+    };
+#pragma unroll
+    for (int c = 0; c < C::NKS; ++c) load_b(c, 0);
+#pragma unroll
+    for (int ct = 0; ct <= C::NCT; ++ct) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (ct < C::NCT) {
+        const int ch = ct & 1;
+        const bool fresh = fresh_stage && ct < 2;
+#pragma unroll
+        for (int c = 0; c < C::NKS; ++c) {
+          const acc_t zero = {};
+#pragma unroll
+          for (int rt = 0; rt < C::RT; ++rt)
+            mc[ch][rt] = A::mfma(ah[rt][c], bh[c], (c == 0 && fresh) ? zero : mc[ch][rt]);
+#pragma unroll
+          for (int rt = 0; rt < C::RT; ++rt) mc[ch][rt] = A::mfma(ah[rt][c], bl[c], mc[ch][rt]);
+#pragma unroll
+          for (int rt = 0; rt < C::RT; ++rt) mc[ch][rt] = A::mfma(al[rt][c], bh[c], mc[ch][rt]);
+          if (ct + 1 < C::NCT) load_b(c, ct + 1);
+        }
+      }
+      if (ct > 0) {
+        const int ch = (ct - 1) & 1;
+        float t0 = mc[ch][0][0], t1 = mc[ch][0][1];
+#pragma unroll
+        for (int rt = 0; rt < C::RT; ++rt) {
+#pragma unroll
+          for (int r = rt == 0 ? 2 : 0; r < C::NV; r += 2) {
+            t0 += mc[ch][rt][r];
+            t1 += mc[ch][rt][r + 1];
+          }
+        }
+        const float T = t0 + t1;
+        const float cp = (fresh_stage && ct - 1 < 2) ? T : T - tprev[ch];
+        tprev[ch] = T;
+        atomicAdd(&colacc[cbuf][col0 + (ct - 1) * 16 + li], static_cast<double>(__builtin_rintf(cp * cmul)));
+      }
+      {
+        constexpr int NM = 3 * C::RT;  // MFMAs per k-step
+#pragma unroll
+        for (int c = 0; c < C::NKS; ++c) {
+#pragma unroll
+          for (int i = 0; i < NM; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // VALU (previous tile's epilogue)
+          }
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);    // next tile's B, k-step c
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // chains -> LDS row accumulator (exact integer fp64 adds; 16 column lanes per row)
+  // Row fold: the 16 column lanes of a DPP row hold partials of the same row;
+  // they are summed across the row (rotations 8, 4, 2, 1: fixed order, lane 0's
+  // result is used) before ONE exact fp64 LDS add per row -- 16 lanes adding
+  // to one LDS address serialise, and cost more than the whole tile stream.
+  auto row16_sum = [](float v) {
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x122, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x121, 0xF, 0xF, false));
+    return v;
+  };
+  auto fold_rows = [&]() {
+#pragma unroll
+    for (int rt = 0; rt < C::RT; ++rt) {
+#pragma unroll
+      for (int r = 0; r < C::NV; ++r) {
+        const float v = row16_sum(mc[0][rt][r] + mc[1][rt][r]);
+        if (li == 0)
+          atomicAdd(&rowacc[wave * 128 + rt * 16 + 4 * lq + r], static_cast<double>(__builtin_rintf(v * kFold)));
+      }
+      // one row tile at a time: converting all 32 values first would need 64
+      // more VGPRs while the A fragments are live
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  auto flush_one = [&](double& slot, int64_t out_row) {
+    const double v = slot;
+    if (v != 0.0) atomicAdd(acc_out + out_row, static_cast<unsigned long long>(static_cast<long long>(v)));
+    slot = 0.0;
+  };
+  auto flush_cols = [&](int cbuf, int Qf) {
+    flush_one(colacc[cbuf][tid], static_cast<int64_t>(Qf) * C::SB + tid);
+    flush_one(colacc[cbuf][tid + 256], static_cast<int64_t>(Qf) * C::SB + tid + 256);
+  };
+  auto flush_rows = [&](int Pf) {
+    flush_one(rowacc[tid], static_cast<int64_t>(Pf) * C::SB + tid);
+    flush_one(rowacc[tid + 256], static_cast<int64_t>(Pf) * C::SB + tid + 256);
+  };
+  // lgkmcnt(0) with every barrier: LDS adds (no-return) must land before
+  // another wave's flush reads them (hipcc may omit this wait at a loop barrier)
+  auto block_sync = [&]() {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+
+  int Q = -1;
+  int unit = seek(g, Q);
+  if (unit >= n_units) return;
+  int P = unit_P(unit), qhi_u = unit_qhi(unit);
+  issue(0, Q, 0);
+  load_a(P);
+  int cb = 0;        // colacc buffer of the current pair
+  int flushQ = -1;   // column super block whose sums wait in colacc[cb ^ 1]
+  int flushP = -1;   // row super block whose sums wait in rowacc
+
+  while (true) {
+    int nQ = next_Q(P, Q, qhi_u), n_unit = unit;
+    if (nQ < 0) n_unit = seek(unit + G, nQ);
+    const bool has_next = n_unit < n_units;
+    const bool last_of_unit = n_unit != unit;
+    const float cmul = Q != P ? kFold : 0.0f;  // diagonal pair: row sums only
+
+    block_sync();
+    if (flushQ >= 0) flush_cols(cb ^ 1, flushQ);
+    if (flushP >= 0) flush_rows(flushP);
+    flushP = -1;
+    issue(1, Q, 1);
+    compute(0, cmul, cb, 0, true);
+
+    block_sync();
+    issue(0, Q, 2);
+    compute(1, cmul, cb, 128, false);
+    fold_rows();
+
+    block_sync();
+    issue(1, Q, 3);
+    compute(0, cmul, cb, 256, true);
+
+    block_sync();
+    if (has_next) issue(0, nQ, 0);
+    compute(1, cmul, cb, 384, false);
+    fold_rows();
+
+    flushQ = Q != P ? Q : -1;
+    cb ^= 1;
+    if (last_of_unit) flushP = P;
+    if (!has_next) break;
+    if (last_of_unit) {
+      unit = n_unit;
+      P = unit_P(unit);
+      qhi_u = unit_qhi(unit);
+      load_a(P);
+    }
+    Q = nQ;
+  }
+  block_sync();
+  if (flushQ >= 0) flush_cols(cb ^ 1, flushQ);
+  if (flushP >= 0) flush_rows(flushP);
+}
+
 // fp32 unit rows -> two-term fp16 split, layout [n_pad][d_pad/KS][hi KS | lo KS].
 // One thread per 8 features (one 16-B slot of hi and of lo).
 __global__ __launch_bounds__(256) void split_f16_kernel(const float* __restrict__ u, int64_t n_pad,
@@ -708,10 +1013,11 @@ __global__ __launch_bounds__(256) void split_f16_kernel(const float* __restrict_
   f16x8 h, l;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const _Float16 he = static_cast<_Float16>(v[e]);
-    const float r = v[e] - static_cast<float>(he);  // exact
+    const float sv = v[e] * 4096.0f;                 // exact
+    const _Float16 he = static_cast<_Float16>(sv);
+    const float r = sv - static_cast<float>(he);     // exact
     h[e] = he;
-    l[e] = static_cast<_Float16>(r * 4096.0f);
+    l[e] = static_cast<_Float16>(r);
   }
   uint16_t* dst = out + row * (2 * static_cast<int64_t>(d_pad)) + (f0 / ks) * (2 * ks) + (f0 % ks);
   *reinterpret_cast<uint4*>(dst) = __builtin_bit_cast(uint4, h);
@@ -788,31 +1094,76 @@ int launch_split(const uint16_t* rows, int64_t n_rows_pad, const uint16_t* cols,
   return DAL_OK;
 }
 
+// Number of column blocks J in [lo, hi) that row block I takes under the
+// symmetric orientation rule (J == I; J > I with I+J even; J < I with I+J odd).
+inline int64_t sym_pairs(int64_t I, int64_t lo, int64_t hi) {
+  auto same_parity = [](int64_t a, int64_t b, int64_t p) -> int64_t {  // #J in [a, b) with J % 2 == p
+    if (b <= a) return 0;
+    return (b - p + 1) / 2 - (a - p + 1) / 2;
+  };
+  int64_t n = (lo <= I && I < hi) ? 1 : 0;
+  n += same_parity(lo > I + 1 ? lo : I + 1, hi, I & 1);
+  n += same_parity(lo, hi < I ? hi : I, (I & 1) ^ 1);
+  return n;
+}
+
+// Column-chunk count for the symmetric kernels' round-robin units: unit u =
+// (row block row0 + u % n_rb, chunk u / n_rb), dealt to block u % G.  Picks,
+// among chunk counts giving >= min_units_per_block units per block, the one
+// whose most loaded block has the fewest pairs (exact count; cached per shape).
+inline int64_t sym_chunks(int64_t row0, int64_t n_rb, int64_t lo, int64_t hi, int64_t n_active, int64_t G0,
+                          int min_units_per_block) {
+  struct Entry {
+    int64_t k[7];
+    int64_t nc;
+  };
+  static thread_local Entry cache[8] = {};
+  static thread_local int cache_next = 0;
+  const int64_t key[7] = {row0, n_rb, lo, hi, n_active, G0, min_units_per_block};
+  for (const Entry& e : cache) {
+    bool hit = e.nc > 0;
+    for (int i = 0; i < 7 && hit; ++i) hit = e.k[i] == key[i];
+    if (hit) return e.nc;
+  }
+  const int64_t nj = hi - lo;
+  int64_t nc0 = 1;
+  while (nc0 < nj && n_rb * nc0 < static_cast<int64_t>(min_units_per_block) * G0) ++nc0;
+  int64_t best_nc = nc0, best_max = -1;
+  std::vector<int64_t> load;
+  int64_t tried = 0;
+  for (int64_t c = nc0; c <= nj && tried < 24; ++c) {
+    const int64_t cb = ceil_div(nj, c), ncc = ceil_div(nj, cb);
+    if (c > nc0 && cb == ceil_div(nj, c - 1)) continue;  // same partition as c - 1
+    ++tried;
+    const int64_t units = n_rb * ncc, G = units < G0 ? units : G0;
+    load.assign(static_cast<size_t>(G), 0);
+    for (int64_t u = 0; u < units; ++u) {
+      const int64_t I = row0 + u % n_rb;
+      if (I >= n_active) continue;
+      const int64_t clo = lo + (u / n_rb) * cb, chi = clo + cb < hi ? clo + cb : hi;
+      load[static_cast<size_t>(u % G)] += sym_pairs(I, clo, chi);
+    }
+    int64_t mx = 0;
+    for (int64_t v : load) mx = v > mx ? v : mx;
+    if (best_max < 0 || mx < best_max) {
+      best_max = mx;
+      best_nc = ncc;
+    }
+  }
+  Entry& e = cache[cache_next];
+  cache_next = (cache_next + 1) % 8;
+  for (int i = 0; i < 7; ++i) e.k[i] = key[i];
+  e.nc = best_nc;
+  return best_nc;
+}
+
 template <int KS, int MT, int SG>
 int launch_sym(const uint16_t* rows, int64_t row_block0, int64_t n_rb, const uint16_t* cols,
                int64_t col_block0, int64_t j_lo, int64_t j_hi, int64_t nb_active, int64_t ldh,
                int slice_off, int64_t* acc, int grid_blocks, hipStream_t stream) {
   const int G0 = grid_blocks > 0 ? grid_blocks : 2 * device_cus_split();
   const int64_t nj = j_hi - j_lo;
-  // chunks of column blocks: enough units for a balanced round-robin (each
-  // unit does ~half its chunk's blocks), few enough to limit A reloads
-  // column-block chunks: >= 4 units per block, then the count whose last
-  // round-robin round is fullest (units cost ~equal: half a chunk each)
-  int64_t nc = 1;
-  while (nc < nj && n_rb * nc < 4LL * G0) ++nc;
-  {
-    double best = -1.0;
-    int64_t best_nc = nc;
-    for (int64_t c = nc; c <= nc + 32 && c <= nj; ++c) {
-      const int64_t cb = ceil_div(nj, c), ncc = ceil_div(nj, cb), u = n_rb * ncc;
-      const double eff = static_cast<double>(u) / (static_cast<double>(G0) * ceil_div(u, G0));
-      if (eff > best + 0.01) {
-        best = eff;
-        best_nc = c;
-      }
-    }
-    nc = best_nc;
-  }
+  const int64_t nc = sym_chunks(row_block0, n_rb, j_lo, j_hi, nb_active, G0, 4);
   const int64_t cbk = ceil_div(nj, nc);
   const int64_t n_chunks = ceil_div(nj, cbk);
   const int64_t n_units = n_rb * n_chunks;
@@ -822,6 +1173,26 @@ int launch_sym(const uint16_t* rows, int64_t row_block0, int64_t n_rb, const uin
                      static_cast<int>(col_block0), static_cast<int>(j_lo), static_cast<int>(j_hi),
                      static_cast<int>(nb_active), ldh, slice_off, static_cast<int>(cbk),
                      static_cast<int>(n_chunks), reinterpret_cast<unsigned long long*>(acc));
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}
+
+template <int KS>
+int launch_sym2(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint16_t* cols, int64_t scol0,
+                int64_t q_lo, int64_t q_hi, int64_t ns_active, int64_t ldh, int slice_off, int64_t* acc,
+                int grid_blocks, hipStream_t stream) {
+  const int G0 = grid_blocks > 0 ? grid_blocks : 2 * device_cus_split();
+  const int64_t nq = q_hi - q_lo;
+  const int64_t nc = sym_chunks(srow0, n_srb, q_lo, q_hi, ns_active, G0, 2);
+  const int64_t cbk = ceil_div(nq, nc);
+  const int64_t n_chunks = ceil_div(nq, cbk);
+  const int64_t n_units = n_srb * n_chunks;
+  const int64_t G = n_units < G0 ? n_units : G0;
+  hipLaunchKernelGGL((gram_sym2_kernel<KS>), dim3(static_cast<unsigned>(G)), dim3(kSpThreads), 0, stream,
+                     rows, static_cast<int>(srow0), static_cast<int>(n_srb), cols, static_cast<int>(scol0),
+                     static_cast<int>(q_lo), static_cast<int>(q_hi), static_cast<int>(ns_active), ldh,
+                     slice_off, static_cast<int>(cbk), static_cast<int>(n_chunks),
+                     reinterpret_cast<unsigned long long*>(acc));
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
 }
@@ -853,8 +1224,9 @@ extern "C" double dal_density_error_bound_sym(int64_t n_cols) {
   // u = 2^-23 (conservative for the MFMA's internal fp32 adds), products exact
   // (f16 x f16), and c = 1 + 2^-8 >= sum_d |h_i h_j| + |h_i l_j| + |l_i h_j| over
   // sum_d |u_i u_j| <= 1 (Cauchy-Schwarz on unit rows), per density entry:
-  //   row side   two chains of <= 8 tiles x 192 products, joined by one add:
-  //              gamma_1537 * c per column
+  //   row side   two chains of <= 8 tiles x 192 products, joined by one add
+  //              (+4 adds of the cross-lane row sum in the 512-row kernel):
+  //              gamma_1541 * c per column
   //   column side  a tile's column partial is T_k - T_{k-1}, T = sum of the
   //              lane's 16 chain values (k <= 8 tiles into the chain):
   //              (8 gamma_192 + 15 gamma_15 + u) * c per row
@@ -862,7 +1234,7 @@ extern "C" double dal_density_error_bound_sym(int64_t n_cols) {
   // Every column j of a row's density lies on exactly one side of its pair.
   const double u = 1.0 / 8388608.0;  // 2^-23
   auto gamma = [u](double n) { return n * u / (1.0 - n * u); };
-  const double row = gamma(1537.0);
+  const double row = gamma(1541.0);
   const double col = 8.0 * gamma(192.0) + 15.0 * gamma(15.0) + u;
   const double c = 1.0 + 1.0 / 256.0;
   const double s = 1.0 / 4194304.0;  // 2^-22
@@ -924,6 +1296,25 @@ extern "C" int dal_gram_rowsum_sym(const uint16_t* rows, int64_t row_block0, int
   hipStream_t st = as_stream(stream);
   const int ks = split_ks(d_pad);
   const int64_t ldh = 2 * d_pad;
+  // kernel: 512-row super blocks (default; half the LDS bytes, DMA and
+  // column flushes per MFMA -- measured 0-4 % faster from 100k to 500k rows) or
+  // the 256-row-block kernel (A/B knob DAL_GRAM_SYM=1).  Fixed per build, so
+  // every GPU count runs the same kernel and produces the same bits.
+  const char* kenv = getenv("DAL_GRAM_SYM");
+  const int kind = kenv && atoi(kenv) == 1 ? 1 : 2;
+  if (kind == 2) {
+    // super-block form: every block index must be even (shards are 512-row multiples)
+    if ((row_block0 | n_row_blocks | col_block0 | j_lo | j_hi | nb_active) & 1) return DAL_ERR_SHAPE;
+    for (int64_t off = 0; off < d_pad; off += ks) {
+      const int so = static_cast<int>(2 * off);
+      const int rc = ks == 32 ? launch_sym2<32>(rows, row_block0 / 2, n_row_blocks / 2, cols, col_block0 / 2,
+                                                j_lo / 2, j_hi / 2, nb_active / 2, ldh, so, acc, grid_blocks, st)
+                              : launch_sym2<64>(rows, row_block0 / 2, n_row_blocks / 2, cols, col_block0 / 2,
+                                                j_lo / 2, j_hi / 2, nb_active / 2, ldh, so, acc, grid_blocks, st);
+      if (rc != DAL_OK) return rc;
+    }
+    return DAL_OK;
+  }
   for (int64_t off = 0; off < d_pad; off += ks) {
     const int so = static_cast<int>(2 * off);
     // epilogue variant (A/B knob): 2 = chained accumulators (default), 1 = per-tile

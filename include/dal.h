@@ -132,12 +132,13 @@ int dal_gram_rowsum(const float* u_rows, int64_t n_rows_pad, const float* u_cols
 /* ---- (a2-a4) the same row-sum on fp16 MFMA with a two-term split ------
  * Same contract and replaced reference lines as dal_gram_rowsum, at the fp16
  * matrix-core rate.  dal_split_f16 writes each normalised fp32 row u (from
- * dal_normalize_rows, ld >= d_pad) as h = fp16(u), l = fp16((u - h) * 2^12)
- * in the layout [n_pad][d_pad / KS][KS hi halves | KS lo halves], KS = 32 if
- * d_pad == 32 else 64 (dal_split_f16_halves(n_pad, d_pad) halves in all);
- * dal_gram_rowsum_split then accumulates acc[i] += round(sum_j <u_i,u_j> * 2^32)
- * from three v_mfma_f32_32x32x16_f16 products (h.h, h.l, l.h) per 16
- * features, folded exactly per 256-column group (bit-identical for any grid,
+ * dal_normalize_rows, ld >= d_pad) at scale 2^12 as H = fp16(2^12 u),
+ * L = fp16(2^12 u - H) (RNE) in the layout [n_pad][d_pad / KS][KS H halves |
+ * KS L halves], KS = 32 if d_pad == 32 else 64 (dal_split_f16_halves(n_pad,
+ * d_pad) halves in all); dal_gram_rowsum_split then accumulates
+ * acc[i] += round(sum_j <u_i,u_j> * 2^32) from three v_mfma_f32_16x16x32_f16
+ * products (H.H, H.L, L.H, all in units of 2^-24) per 32 features, folded
+ * exactly per 256-column group (bit-identical for any grid,
  * column split or GPU count).  Rigorous bound: dal_density_error_bound_split.
  * n_rows_pad % 256 == 0, n_cols_pad % 512 == 0; grid_blocks <= 0 selects
  * two blocks per CU. */

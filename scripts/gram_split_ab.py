@@ -37,10 +37,14 @@ for n, d in [(int(a), int(b)) for a, b in shapes]:
         e0.record()
         os.environ["DAL_GRAM_SCHED"] = "0" if kind.endswith("s0") else "1"
         os.environ["DAL_GRAM_MT"] = "32" if "32" in kind else "16"
+        # sym: default kernel; symk1: 256-row-block kernel; symsgN: its epilogue variant N
+        os.environ.pop("DAL_GRAM_SG", None)
+        os.environ.pop("DAL_GRAM_SYM", None)
         if kind.startswith("symsg"):
+            os.environ["DAL_GRAM_SYM"] = "1"
             os.environ["DAL_GRAM_SG"] = kind[5:]
-        else:
-            os.environ.pop("DAL_GRAM_SG", None)
+        elif kind in ("symk1", "symk2"):
+            os.environ["DAL_GRAM_SYM"] = kind[-1]
         if kind.startswith("sym"):
             nb = st.n_pad // 256
             _lib.call("dal_gram_rowsum_sym", _ptr(sp), 0, nb, _ptr(sp), 0, 0, nb, nb, st.d_pad,

@@ -105,8 +105,8 @@ def test_gram_density_within_bound(cuda, n, d, dist, gram):
 
 @pytest.mark.parametrize("d", [30, 64, 200])
 def test_split_operand_bit_exact(cuda, d):
-    """dal_split_f16: h = fp16(u), l = fp16((u - h) * 2^12) (RNE), layout
-    [n_pad][d_pad/KS][KS hi | KS lo]."""
+    """dal_split_f16: H = fp16(2^12 u), L = fp16(2^12 u - H) (RNE), layout
+    [n_pad][d_pad/KS][KS H | KS L]."""
     from dal.engine import PoolState
 
     X = O.synthetic_pool(1000, d, seed=d, dist="normal")
@@ -115,15 +115,16 @@ def test_split_operand_bit_exact(cuda, d):
     sp = _np(st.gram_operand()).view(np.float16)
     d_pad = st.d_pad
     ks = 32 if d_pad == 32 else 64
-    h = u.astype(np.float16)
-    l = ((u - h.astype(np.float32)) * np.float32(4096)).astype(np.float16)
+    v = u * np.float32(4096)  # exact
+    h = v.astype(np.float16)
+    l = (v - h.astype(np.float32)).astype(np.float16)
     ref = np.empty((st.n_pad, 2 * d_pad), dtype=np.float16)
     for s0 in range(0, d_pad, ks):
         ref[:, 2 * s0:2 * s0 + ks] = h[:, s0:s0 + ks]
         ref[:, 2 * s0 + ks:2 * s0 + 2 * ks] = l[:, s0:s0 + ks]
     assert np.array_equal(sp.view(np.uint16), ref.view(np.uint16))
-    # reconstruction error of the split: |u - h - l 2^-12| <= 2^-22 |u| + 2^-37
-    rec = h.astype(np.float64) + l.astype(np.float64) * 2.0**-12
+    # reconstruction error of the split: |u - (H + L) 2^-12| <= 2^-22 |u| + 2^-37
+    rec = (h.astype(np.float64) + l.astype(np.float64)) * 2.0**-12
     assert (np.abs(rec - u) <= 2.0**-22 * np.abs(u) + 2.0**-37).all()
 
 
@@ -151,17 +152,20 @@ def test_gram_kernels_deterministic_across_grids_and_column_splits(cuda, gram, d
     assert np.array_equal(_np(part), outs[0])
 
 
-@pytest.mark.parametrize("sg", ["1", "2"])
-def test_sym_gram_repeatable_at_scale(cuda, sg, monkeypatch):
-    """The symmetric kernel's LDS column accumulator is flushed by other waves
-    one barrier later: repeated launches over many pairs (here 120k rows x
-    d 256, four K slices, ~27k block pairs each) must give identical bits and
-    stay within the rigorous bound (both epilogue variants)."""
+@pytest.mark.parametrize("knobs", [{"DAL_GRAM_SYM": "2"}, {"DAL_GRAM_SYM": "1"},
+                                   {"DAL_GRAM_SYM": "1", "DAL_GRAM_SG": "1"}])
+def test_sym_gram_repeatable_at_scale(cuda, knobs, monkeypatch):
+    """The symmetric kernels' LDS row/column accumulators are flushed by other
+    waves one barrier later: repeated launches over many pairs (here 120k rows
+    x d 256, four K slices, ~27k block pairs each) must give identical bits and
+    stay within the rigorous bound (512-row kernel, 256-row kernel and its
+    per-tile epilogue variant)."""
     import torch
     from dal import _lib
     from dal.engine import PoolState
 
-    monkeypatch.setenv("DAL_GRAM_SG", sg)
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
     g = torch.Generator(device=cuda)
     g.manual_seed(11)
     x = torch.rand((120_000, 256), generator=g, device=cuda).clamp_(min=1e-7)
