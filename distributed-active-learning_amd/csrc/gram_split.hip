@@ -296,23 +296,23 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_split_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Symmetric (SYRK-style) variant: S = U U^T is symmetric, so each unordered
-// pair of 256-row blocks {I, J} is multiplied ONCE and yields both the row sums
-// of S_IJ (-> rows of I) and its column sums (-> rows of J): half the MFMAs.
-// Orientation rule, a function of the global block indices only (so the bits
-// do not depend on the GPU count): row block I takes column block J when
-//   J == I (diagonal: row sums only),  J > I and I+J even,  J < I and I+J odd.
-// Every row block then takes ~nb/2 column blocks, so work is balanced across
-// row blocks, units and row-sharded GPUs.  Column block = fold group = one
-// pair of 128-column stages.  Per 16x16 (or 32x32) output tile the per-tile
-// accumulators are combined on the VALU: t = M + X is added into
-// the fp32 row accumulator (the same 16-tile chain per fold as the asymmetric
-// kernel) and summed over the lane's rows into a column partial, which is
-// rounded to a multiple of 2^-32 and added into an LDS fp64 column
-// accumulator (integer-valued: exact, order-free); after the pair the 256
-// column sums go to global int64 atomics.  The LDS column accumulator is
-// double-buffered so its flush (at the next pair's first barrier) never races
-// the next pair's adds.
+// Symmetric (SYRK-style) variant on 256-row blocks (DAL_GRAM_SYM=1; the
+// default is the 512-row gram_sym2_kernel below): S = U U^T is symmetric, so
+// each unordered pair of 256-row blocks {I, J} is multiplied ONCE and yields
+// both the row sums of S_IJ (-> rows of I) and its column sums (-> rows of J):
+// half the MFMAs.  Orientation rule, a function of the global block indices
+// only (so the bits do not depend on the GPU count): row block I takes column
+// block J when J == I (diagonal: row sums only), J > I and I+J even, J < I and
+// I+J odd.  Every row block then takes ~nb/2 column blocks, so work is
+// balanced across row blocks, units and row-sharded GPUs.  Column block = fold
+// group = one pair of 128-column stages.  Epilogue SG 2 (default): the row
+// sums ride in two MFMA accumulator chains (even / odd column tiles) and a
+// tile's column sums are the growth of its chain's lane total; SG 1: per-tile
+// fresh accumulators, row sums added on the VALU.  Column partials are rounded
+// to multiples of 2^-32 and added into an LDS fp64 column accumulator (exact,
+// order-free); after the pair the 256 column sums go to global int64 atomics.
+// The LDS column accumulator is double-buffered so its flush (at the next
+// pair's first barrier) never races the next pair's adds.
 template <int KS, int MT>
 struct SymCfg {
   static constexpr int ROWB = KS * 4;
