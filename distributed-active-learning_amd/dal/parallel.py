@@ -228,9 +228,10 @@ def hip_sort_positions(keys, pos, k):
     return out_pos
 
 
-def _gloo_needs_bytes(dtype) -> bool:
-    """gloo gathers none of torch's 16-bit integer or unsigned 16/32/64-bit
-    types: such tensors travel as their bytes."""
+def _needs_bytes(dtype) -> bool:
+    """Neither RCCL/NCCL nor gloo has torch's 16-bit integer or unsigned
+    16/32/64-bit types (the split Gram operand is int16 bit patterns): such
+    tensors are gathered as their bytes (a gather only moves bits)."""
     torch = __import__("torch")
     names = ("int16", "uint16", "uint32", "uint64")
     return any(getattr(torch, n, None) == dtype for n in names)
@@ -255,9 +256,9 @@ class TorchComm:
         """Start an all-gather; returns (output, work handle or None).  With
         RCCL it runs asynchronously on the communicator's stream."""
         torch = __import__("torch")
-        if self.dist.get_backend(self.group) == "gloo" and t.dim() and _gloo_needs_bytes(t.dtype):
-            # the fp16-split Gram operand is uint16 bit patterns: gather the bytes
-            return self.all_gather(t.contiguous().view(torch.uint8)).view(t.dtype), None
+        if t.dim() and _needs_bytes(t.dtype):
+            out, work = self.all_gather_start(t.contiguous().view(torch.uint8))
+            return out.view(t.dtype), work
         if t.is_cuda and self.dist.get_backend(self.group) == "gloo":
             # rehearsal path (several ranks sharing one GPU): stage through the host
             return self.all_gather(t.cpu()).to(t.device), None
@@ -298,10 +299,19 @@ def select(sel: ShardedSelector, comm, unlabeled_idx, forest, k: int, mode: str 
     parts_full = comm.all_gather(parts) if mode == "dw" else None
     top = sel.local_select(u_full, parts_full, unlabeled_idx, forest, k, mode, strategy, beta,
                            density_mode)
-    keys_all = comm.all_gather(top.keys)
-    idx_all = comm.all_gather(top.idx)
-    sc_all = comm.all_gather(top.scores)
-    return merge_topk(keys_all, idx_all, sc_all, k, sort_fn)
+    return merge_topk(*gather_topk(comm, top), k, sort_fn)
+
+
+def gather_topk(comm, top: LocalTopk):
+    """ONE all-gather of every rank's (key, index, score) triples, packed as
+    int64 [3, k] (scores by bit pattern): a collective's latency, not its
+    bytes, dominates at k = 100-1000."""
+    torch = __import__("torch")
+    k = int(top.keys.shape[0])
+    packed = torch.stack([top.keys, top.idx, top.scores.view(torch.int64)])  # [3, k]
+    g = comm.all_gather(packed.reshape(1, 3 * k)).reshape(-1, 3, k)       # [P, 3, k]
+    return (g[:, 0].reshape(-1), g[:, 1].reshape(-1),
+            g[:, 2].reshape(-1).contiguous().view(torch.float64))
 
 
 def emulate(selectors, unlabeled_idx, forest, k: int, mode: str = "dw",
@@ -351,7 +361,7 @@ def diversity_select_sharded(x_local, row_base: int, labeled_rows, k: int, comm,
         idx[:kk] = sel.indices
         sc[:kk] = sel.selected_scores
         keys[:kk] = _score_keys_asc(sel.selected_scores)
-    return merge_topk(comm.all_gather(keys), comm.all_gather(idx), comm.all_gather(sc), k, sort_fn)
+    return merge_topk(*gather_topk(comm, LocalTopk(keys, idx, sc)), k, sort_fn)
 
 
 def _score_keys_asc(s):
