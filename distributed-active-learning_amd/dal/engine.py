@@ -135,6 +135,13 @@ class PoolState:
     def n_excluded_global(self) -> int:
         return int(self.excluded.size)
 
+    def norms(self):
+        """Canonical fp64 row norms [n]: those of the fused normalise+split
+        pass once the Gram operand exists, else from dal_normalize_rows."""
+        if self._norm64 is None:
+            self.normalized()
+        return self._norm64
+
     def normalized(self):
         """(u [n_pad, d_pad] fp32 with E rows zeroed, norm64 [n] fp64)."""
         if self._u is None:
@@ -154,21 +161,29 @@ class PoolState:
         """The density GEMM's operand for this shard's rows: the fp32 unit rows
         (gram "f32") or their two-term fp16 split [n_pad, 2*d_pad] (gram
         "split", dal_split_f16).  All-gathered as is in the multi-GPU path."""
-        u, _ = self.normalized()
         if self.gram == "f32":
+            u, _ = self.normalized()
             return u
         if self._split is None:  # "split" and "sym" share the operand
             torch = _torch()
             self._split = torch.empty((self.n_pad, 2 * self.d_pad), dtype=torch.int16, device=self.device)
-            call("dal_split_f16", _ptr(u), self.n_pad, self.d_pad, self.d_pad, _ptr(self._split),
-                 _stream(self.device))
+            if self._u is not None:
+                call("dal_split_f16", _ptr(self._u), self.n_pad, self.d_pad, self.d_pad, _ptr(self._split),
+                     _stream(self.device))
+            else:  # fused: the fp32 unit rows never reach HBM
+                norm64 = torch.empty(self.n, dtype=torch.float64, device=self.device)
+                call("dal_normalize_split", _ptr(self.x), self.n, self.d, self.d, _ptr(self.flags),
+                     self.n_pad, self.d_pad, _ptr(self._split), _ptr(norm64), _ptr(self.status),
+                     _stream(self.device))
+                if self._norm64 is None:
+                    self._norm64 = norm64
         return self._split
 
     def colsum_partials(self):
         """Canonical fp64 column-sum partials of this shard ([chunks, d])."""
         if self._colsum_partials is None:
             torch = _torch()
-            _, norm64 = self.normalized()
+            norm64 = self.norms()
             chunks = (self.n + DAL_CANON_CHUNK - 1) // DAL_CANON_CHUNK
             self._colsum_partials = torch.empty((chunks, self.d), dtype=torch.float64, device=self.device)
             call("dal_canon_colsum_partials", _ptr(self.x), self.n, self.d, self.d, _ptr(norm64),
@@ -253,7 +268,7 @@ class PoolState:
         the oracle.  ``colsum`` = the global s (multi-GPU); default this pool's."""
         if self._density_exact is None or colsum is not None:
             torch = _torch()
-            _, norm64 = self.normalized()
+            norm64 = self.norms()
             s = self.colsum() if colsum is None else colsum
             d = torch.empty(self.n, dtype=torch.float64, device=self.device)
             call("dal_density_separable", _ptr(self.x), self.n, self.d, self.d, _ptr(norm64), _ptr(s),
@@ -418,7 +433,7 @@ def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k
     torch = _torch()
     lib = _lib.load()
     n = state.n
-    _, norm64 = state.normalized()
+    norm64 = state.norms()
     cap = candidate_cap(n, k)
     while True:
         wsb = int(lib.dal_dw_select_workspace_bytes(n, k, cap))
@@ -482,20 +497,23 @@ def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: 
         return _density_step_separable(state, unlabeled_idx, forest, k, beta)
     if mode != "gram":
         raise ValueError(f"density mode must be 'gram' or 'separable', not {mode!r}")
-    flags, unl, n_cand = state.row_flags(unlabeled_idx)
-    if n_cand == 0:
+    unl = _as_index(unlabeled_idx, state.device)
+    if int(unl.shape[0]) == 0:
         raise ValueError("unlabeled set is empty (the reference loop breaks here)")
+    # the density GEMM goes to the GPU first; the host prepares the rest while it runs
+    dens = state.density_fixed() if density_fixed is None else density_fixed
+    flags, unl, n_cand = state.row_flags(unl)
     kk = min(int(k), n_cand)
     loc = state.local_positions(unl)
-    dens = state.density_fixed() if density_fixed is None else density_fixed
     lut_dev = device_lut("entropy", forest.n_trees, state.device)
     votes, scores, keys_lo, keys_hi = forest_score(
         state, forest, lut_dev, flags, DAL_DESCENDING, density=dens,
         density_err=density_error(state), beta=beta, want_hi=True)
+    out_scores, out_votes = scores[loc], votes[loc]  # queued before the selection's sync
     idx, sel_scores, _ = dw_select_local(state, flags, votes, keys_lo, keys_hi, lut_dev, kk, beta,
                                          state.colsum())
     state.check_status()  # already synchronised by dw_select_local
-    return Selection(scores=scores[loc], indices=idx, selected_scores=sel_scores, votes=votes[loc])
+    return Selection(scores=out_scores, indices=idx, selected_scores=sel_scores, votes=out_votes)
 
 
 def _density_step_separable(state: PoolState, unlabeled_idx, forest: Forest, k: int,

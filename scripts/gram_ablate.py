@@ -23,7 +23,9 @@ for a in os.environ.get("AB_LIBS", "abl1,abl2").split(","):
 knobs = [k.split("=") for k in os.environ.get("AB_KNOBS", "").split(",") if k]
 for name, kv in knobs:
     libs[name] = (libs["full"], kv)
-for n, d in [(100_000, 64), (200_000, 30)]:
+SHAPES = [tuple(int(v) for v in t.split("x")) for t in os.environ.get("AB_SHAPES", "100000x64,200000x30").split(",")]
+ROUNDS = int(os.environ.get("AB_ROUNDS", "4"))
+for n, d in SHAPES:
     g = torch.Generator(device=dev)
     g.manual_seed(n)
     x = torch.rand((n, d), generator=g, device=dev).clamp_(min=1e-7)
@@ -31,7 +33,7 @@ for n, d in [(100_000, 64), (200_000, 30)]:
     sp = st.gram_operand()
     nb = st.n_pad // 256
     res = {k: [] for k in libs}
-    for r in range(4):
+    for r in range(ROUNDS):
         for k, L in libs.items():
             if isinstance(L, tuple):
                 L, kv = L

@@ -103,6 +103,25 @@ def test_gram_density_within_bound(cuda, n, d, dist, gram):
     assert (err / scale).max() <= DENSITY_RTOL
 
 
+@pytest.mark.parametrize("d", [7, 30, 64, 65, 200, 500])
+def test_fused_normalize_split_matches_two_pass(cuda, d):
+    """dal_normalize_split == dal_normalize_rows + dal_split_f16, bit for bit
+    (operand and canonical norms), incl. excluded rows and row padding."""
+    import torch
+    from dal.engine import PoolState
+
+    X = O.synthetic_pool(1300, d, seed=d + 1, dist="normal")
+    E = [0, 5, 1299]
+    fused = PoolState(X, excluded=E, device=cuda, gram="sym")
+    op_f = fused.gram_operand()  # fused path: no fp32 unit rows yet
+    assert fused._u is None
+    two = PoolState(X, excluded=E, device=cuda, gram="sym")
+    u, n64 = two.normalized()
+    op_t = two.gram_operand()    # two-pass path
+    assert torch.equal(op_f, op_t)
+    assert torch.equal(fused.norms(), n64)
+
+
 @pytest.mark.parametrize("d", [30, 64, 200])
 def test_split_operand_bit_exact(cuda, d):
     """dal_split_f16: H = fp16(2^12 u), L = fp16(2^12 u - H) (RNE), layout
