@@ -170,13 +170,23 @@ class PoolState:
             if self._u is not None:
                 call("dal_split_f16", _ptr(self._u), self.n_pad, self.d_pad, self.d_pad, _ptr(self._split),
                      _stream(self.device))
-            else:  # fused: the fp32 unit rows never reach HBM
+            elif self.n == 0:  # an empty shard (more GPUs than row granules)
+                self._split.zero_()
+                if self._norm64 is None:
+                    self._norm64 = torch.zeros(0, dtype=torch.float64, device=self.device)
+            else:  # fused: the fp32 unit rows never reach HBM; canonical partials on the way
                 norm64 = torch.empty(self.n, dtype=torch.float64, device=self.device)
-                call("dal_normalize_split", _ptr(self.x), self.n, self.d, self.d, _ptr(self.flags),
-                     self.n_pad, self.d_pad, _ptr(self._split), _ptr(norm64), _ptr(self.status),
-                     _stream(self.device))
+                chunks = (self.n + DAL_CANON_CHUNK - 1) // DAL_CANON_CHUNK
+                parts = None
+                if self._colsum_partials is None:
+                    parts = torch.empty((chunks, self.d), dtype=torch.float64, device=self.device)
+                call("dal_prep_split", _ptr(self.x), self.n, self.d, self.d, _ptr(self.flags),
+                     self.n_pad, self.d_pad, _ptr(self._split), _ptr(norm64),
+                     0 if parts is None else _ptr(parts), _ptr(self.status), _stream(self.device))
                 if self._norm64 is None:
                     self._norm64 = norm64
+                if parts is not None:
+                    self._colsum_partials = parts
         return self._split
 
     def colsum_partials(self):

@@ -104,9 +104,10 @@ def test_gram_density_within_bound(cuda, n, d, dist, gram):
 
 
 @pytest.mark.parametrize("d", [7, 30, 64, 65, 200, 500])
-def test_fused_normalize_split_matches_two_pass(cuda, d):
-    """dal_normalize_split == dal_normalize_rows + dal_split_f16, bit for bit
-    (operand and canonical norms), incl. excluded rows and row padding."""
+def test_fused_prep_matches_separate_kernels(cuda, d):
+    """dal_prep_split == dal_normalize_rows + dal_split_f16 +
+    dal_canon_colsum_partials, bit for bit (operand, canonical norms and
+    column-sum partials), incl. excluded rows and row padding."""
     import torch
     from dal.engine import PoolState
 
@@ -120,6 +121,9 @@ def test_fused_normalize_split_matches_two_pass(cuda, d):
     op_t = two.gram_operand()    # two-pass path
     assert torch.equal(op_f, op_t)
     assert torch.equal(fused.norms(), n64)
+    assert two._colsum_partials is None  # computed below by its own kernel
+    assert torch.equal(fused.colsum_partials(), two.colsum_partials())
+    assert torch.equal(fused.colsum(), two.colsum())
 
 
 @pytest.mark.parametrize("d", [30, 64, 200])
@@ -546,6 +550,54 @@ def test_sharded_emulation_bit_identical(cuda, world, mode):
     assert np.array_equal(_np(idx), _np(ref.indices))
     assert np.array_equal(_np(idx), o_idx)
     assert np.array_equal(_np(sc), o_sc)
+
+
+class _RecordingComm:
+    """Single-process stand-in for TorchComm: the all-gather returns the
+    precomputed gathered operand (asynchronously: a work handle), the
+    reduce-scatter returns this rank's full contribution (summed by the test)."""
+
+    def __init__(self, u_full):
+        self.u_full = u_full
+        self.waited = False
+
+    def all_gather_start(self, t):
+        return self.u_full, "work"
+
+    def wait(self, work):
+        assert work == "work"
+        self.waited = True
+
+    def reduce_scatter_sum(self, t):
+        return t
+
+
+@pytest.mark.parametrize("world,n", [(2, 5000), (3, 7000), (4, 2500), (8, 9000)])
+def test_exchange_density_column_split_bit_identical(cuda, world, n):
+    """ShardedSelector.exchange_density (the RCCL path: own-shard launch with
+    CUs left to the collective, then the other column ranges, then the
+    reduce-scatter of the global accumulator) sums to the single-GPU density
+    bits exactly."""
+    import torch
+    from dal import parallel
+    from dal.engine import PoolState
+
+    d = 64
+    X = O.synthetic_pool(n, d, seed=world)
+    E = np.arange(10)
+    sels = []
+    for r in range(world):
+        lo, hi, _ = parallel.shard_range(n, world, r)
+        sels.append(parallel.ShardedSelector(X[lo:hi], n, r, world, excluded=E, device=cuda, gram="sym"))
+    u_full = torch.cat([s.prep()[0] for s in sels])
+    total = None
+    for s in sels:
+        comm = _RecordingComm(u_full)
+        s.exchange_density(comm, s.prep()[0])
+        assert comm.waited
+        total = s._density.clone() if total is None else total + s._density
+    st = PoolState(X, excluded=E, device=cuda, gram="sym")
+    assert torch.equal(total[:n], st.density_fixed()[:n])
 
 
 # ------------------------------------------------ separable density -------
