@@ -698,10 +698,14 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
 // and the per-pair column flush is spread over twice the rows.  Orientation on
 // super blocks (512 rows = the row granule, so shard-independent): super block
 // P takes super block Q when Q == P (diagonal: row sums only, all columns),
-// Q > P and P+Q even, Q < P and P+Q odd.  A pair is 512 x 512 = four
-// 128-column stages; the chains are folded every two stages (256 columns: the
-// chain lengths, and so the error bound, of gram_sym_kernel) into an LDS fp64
-// row accumulator of exact integers, flushed to the int64 output per unit.
+// Q > P and P+Q even, Q < P and P+Q odd.  Work is scheduled in 512 x 256 pairs
+// (P, J), J a 256-column block of super block Q = J/2: two 128-column stages,
+// then the chains are folded (256 columns: the chain lengths, and so the error
+// bound, of gram_sym_kernel) into an LDS fp64 row accumulator of exact
+// integers, flushed to the int64 output per unit; the pair's 256 column sums
+// are flushed per pair.  The half-super-block granularity keeps small launches
+// (a GPU's own shard) balanced; a skip range [skip_lo, skip_hi) of J lets one
+// launch cover every column but an already processed shard.
 template <int KS>
 struct Sym2Cfg {
   static constexpr int MT = 16;
@@ -725,14 +729,14 @@ struct Sym2Cfg {
 template <int KS>
 __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
     const uint16_t* __restrict__ urows, int srow0, int n_srb,
-    const uint16_t* __restrict__ ucols, int scol0, int q_lo, int q_hi,
-    int ns_active, int64_t ldh, int slice_off, int chunk_sb, int n_chunks,
+    const uint16_t* __restrict__ ucols, int jcol0, int j_lo, int j_hi, int skip_lo, int skip_hi,
+    int ns_active, int64_t ldh, int slice_off, int chunk_j, int n_chunks,
     unsigned long long* __restrict__ acc_out) {
   using C = Sym2Cfg<KS>;
   using A = SpAcc<16>;
   using acc_t = A::type;
   __shared__ __attribute__((aligned(16))) float4 lds[2 * C::F4];
-  __shared__ double colacc[2][C::SB];
+  __shared__ double colacc[2][256];
   __shared__ double rowacc[C::SB];
 
   const int tid = threadIdx.x;
@@ -742,37 +746,31 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
   const int n_units = n_srb * n_chunks;
 
   colacc[0][tid] = 0.0;
-  colacc[0][tid + 256] = 0.0;
   colacc[1][tid] = 0.0;
-  colacc[1][tid + 256] = 0.0;
   rowacc[tid] = 0.0;
   rowacc[tid + 256] = 0.0;
 
-  // unit u (chunk-major, dealt round-robin): super block P, column super blocks [lo, hi)
+  // unit u (chunk-major, dealt round-robin): super block P, 256-column blocks [lo, hi)
   auto unit_P = [&](int u) { return srow0 + u % n_srb; };
-  auto unit_qlo = [&](int u) { return q_lo + (u / n_srb) * chunk_sb; };
-  auto unit_qhi = [&](int u) {
-    const int e = q_lo + (u / n_srb + 1) * chunk_sb;
-    return e < q_hi ? e : q_hi;
+  auto unit_jlo = [&](int u) { return j_lo + (u / n_srb) * chunk_j; };
+  auto unit_jhi = [&](int u) {
+    const int e = j_lo + (u / n_srb + 1) * chunk_j;
+    return e < j_hi ? e : j_hi;
   };
-  auto first_Q = [&](int P, int lo, int hi) -> int {
+  auto takes = [&](int P, int J) -> bool {  // orientation on super blocks, minus the skip range
+    const int Q = J >> 1;
+    if (J >= skip_lo && J < skip_hi) return false;
+    return Q == P || (Q > P && ((P + Q) & 1) == 0) || (Q < P && ((P + Q) & 1));
+  };
+  auto first_J = [&](int P, int J, int hi) -> int {
     if (P >= ns_active) return -1;
-    int Q = lo;
-    if (Q < P) {
-      if (((P + Q) & 1) == 0) ++Q;  // Q < P needs P+Q odd (Q may become P)
-    } else if (Q > P) {
-      if ((P + Q) & 1) ++Q;         // Q > P needs P+Q even
-    }
-    return Q < hi ? Q : -1;
+    while (J < hi && !takes(P, J)) ++J;
+    return J < hi ? J : -1;
   };
-  auto next_Q = [&](int P, int Q, int hi) -> int {
-    const int n = (Q == P - 1) ? P : Q + 2;
-    return n < hi ? n : -1;
-  };
-  auto seek = [&](int u, int& Q) {
+  auto seek = [&](int u, int& J) {
     while (u < n_units) {
-      Q = first_Q(unit_P(u), unit_qlo(u), unit_qhi(u));
-      if (Q >= 0) break;
+      J = first_J(unit_P(u), unit_jlo(u), unit_jhi(u));
+      if (J >= 0) break;
       u += G;
     }
     return u;
@@ -788,10 +786,10 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
   };
   const unsigned dst0 = __builtin_amdgcn_readfirstlane(
       static_cast<unsigned>(reinterpret_cast<uintptr_t>((AS3 float4*)(lds + wave * C::PIECES * 64))));
-  // stage h (0..3) of column super block Q into buffer buf
-  auto issue = [&](int buf, int Q, int h) {
+  // stage h (0/1) of 256-column block J into buffer buf
+  auto issue = [&](int buf, int J, int h) {
     const uint16_t* sbase =
-        ucols + (static_cast<int64_t>(Q - scol0) * C::SB + h * C::SC) * ldh + slice_off;
+        ucols + (static_cast<int64_t>(J - jcol0) * 256 + h * C::SC) * ldh + slice_off;
 #pragma unroll
     for (int q = 0; q < C::PIECES; ++q) {
       const unsigned dst = dst0 + static_cast<unsigned>(buf * C::STAGE + q * 1024);
@@ -927,9 +925,8 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
     if (v != 0.0) atomicAdd(acc_out + out_row, static_cast<unsigned long long>(static_cast<long long>(v)));
     slot = 0.0;
   };
-  auto flush_cols = [&](int cbuf, int Qf) {
-    flush_one(colacc[cbuf][tid], static_cast<int64_t>(Qf) * C::SB + tid);
-    flush_one(colacc[cbuf][tid + 256], static_cast<int64_t>(Qf) * C::SB + tid + 256);
+  auto flush_cols = [&](int cbuf, int Jf) {
+    flush_one(colacc[cbuf][tid], static_cast<int64_t>(Jf) * 256 + tid);
   };
   auto flush_rows = [&](int Pf) {
     flush_one(rowacc[tid], static_cast<int64_t>(Pf) * C::SB + tid);
@@ -942,58 +939,50 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
     __syncthreads();
   };
 
-  int Q = -1;
-  int unit = seek(g, Q);
+  int J = -1;
+  int unit = seek(g, J);
   if (unit >= n_units) return;
-  int P = unit_P(unit), qhi_u = unit_qhi(unit);
-  issue(0, Q, 0);
+  int P = unit_P(unit), jhi_u = unit_jhi(unit);
+  issue(0, J, 0);
   load_a(P);
   int cb = 0;        // colacc buffer of the current pair
-  int flushQ = -1;   // column super block whose sums wait in colacc[cb ^ 1]
+  int flushJ = -1;   // column block whose sums wait in colacc[cb ^ 1]
   int flushP = -1;   // row super block whose sums wait in rowacc
 
   while (true) {
-    int nQ = next_Q(P, Q, qhi_u), n_unit = unit;
-    if (nQ < 0) n_unit = seek(unit + G, nQ);
+    int nJ = first_J(P, J + 1, jhi_u), n_unit = unit;
+    if (nJ < 0) n_unit = seek(unit + G, nJ);
     const bool has_next = n_unit < n_units;
     const bool last_of_unit = n_unit != unit;
-    const float cmul = Q != P ? kFold : 0.0f;  // diagonal pair: row sums only
+    const bool diag = (J >> 1) == P;
+    const float cmul = diag ? 0.0f : kFold;  // diagonal super block: row sums only
 
     block_sync();
-    if (flushQ >= 0) flush_cols(cb ^ 1, flushQ);
+    if (flushJ >= 0) flush_cols(cb ^ 1, flushJ);
     if (flushP >= 0) flush_rows(flushP);
     flushP = -1;
-    issue(1, Q, 1);
+    issue(1, J, 1);
     compute(0, cmul, cb, 0, true);
 
     block_sync();
-    issue(0, Q, 2);
+    if (has_next) issue(0, nJ, 0);
     compute(1, cmul, cb, 128, false);
     fold_rows();
 
-    block_sync();
-    issue(1, Q, 3);
-    compute(0, cmul, cb, 256, true);
-
-    block_sync();
-    if (has_next) issue(0, nQ, 0);
-    compute(1, cmul, cb, 384, false);
-    fold_rows();
-
-    flushQ = Q != P ? Q : -1;
+    flushJ = diag ? -1 : J;
     cb ^= 1;
     if (last_of_unit) flushP = P;
     if (!has_next) break;
     if (last_of_unit) {
       unit = n_unit;
       P = unit_P(unit);
-      qhi_u = unit_qhi(unit);
+      jhi_u = unit_jhi(unit);
       load_a(P);
     }
-    Q = nQ;
+    J = nJ;
   }
   block_sync();
-  if (flushQ >= 0) flush_cols(cb ^ 1, flushQ);
+  if (flushJ >= 0) flush_cols(cb ^ 1, flushJ);
   if (flushP >= 0) flush_rows(flushP);
 }
 
@@ -1250,22 +1239,92 @@ int launch_sym(const uint16_t* rows, int64_t row_block0, int64_t n_rb, const uin
   return DAL_OK;
 }
 
+// Pairs (P, J) the super-block kernel processes for row super block P over
+// 256-column blocks [a, b) minus [skip_lo, skip_hi): J is taken when its super
+// block Q = J / 2 is (Q == P, Q > P with P+Q even, Q < P with P+Q odd).  O(1).
+inline int64_t sym2_pairs_range(int64_t P, int64_t a, int64_t b) {
+  if (b <= a) return 0;
+  auto takes = [P](int64_t Q) { return Q == P || (Q > P && ((P + Q) & 1) == 0) || (Q < P && ((P + Q) & 1)); };
+  const int64_t qa = a >> 1, qb = (b - 1) >> 1;  // super blocks touched (inclusive)
+  int64_t n = 2 * sym_pairs(P, qa, qb + 1);
+  if ((a & 1) && takes(qa)) --n;        // only the upper half of qa lies in [a, b)
+  if (!((b - 1) & 1) && takes(qb)) --n; // only the lower half of qb lies in [a, b)
+  return n;
+}
+inline int64_t sym2_pairs(int64_t P, int64_t a, int64_t b, int64_t skip_lo, int64_t skip_hi) {
+  const int64_t sa = a > skip_lo ? a : skip_lo, sb = b < skip_hi ? b : skip_hi;
+  return sym2_pairs_range(P, a, b) - sym2_pairs_range(P, sa, sb);
+}
+
+// Column-chunk count for the super-block kernel's units (P, chunk of J),
+// dealt round-robin: among counts giving >= 2 units per block, the one whose
+// most loaded block has the fewest pairs (exact; cached per shape).
+inline int64_t sym2_chunks(int64_t srow0, int64_t n_srb, int64_t lo, int64_t hi, int64_t skip_lo, int64_t skip_hi,
+                           int64_t ns_active, int64_t G0) {
+  if (const char* e = getenv("DAL_GRAM_NC")) {  // timing knob: force the chunk count
+    const int64_t f = atoll(e);
+    if (f > 0) return f < hi - lo ? f : hi - lo;
+  }
+  struct Entry {
+    int64_t k[8];
+    int64_t nc;
+  };
+  static thread_local Entry cache[8] = {};
+  static thread_local int cache_next = 0;
+  const int64_t key[8] = {srow0, n_srb, lo, hi, skip_lo, skip_hi, ns_active, G0};
+  for (const Entry& e : cache) {
+    bool hit = e.nc > 0;
+    for (int i = 0; i < 8 && hit; ++i) hit = e.k[i] == key[i];
+    if (hit) return e.nc;
+  }
+  const int64_t nj = hi - lo;
+  int64_t nc0 = 1;
+  while (nc0 < nj && n_srb * nc0 < 2 * G0) ++nc0;
+  int64_t best_nc = nc0, best_max = -1;
+  std::vector<int64_t> load;
+  int tried = 0;
+  for (int64_t c = nc0; c <= nj && tried < 24; ++c) {
+    const int64_t cb = ceil_div(nj, c), ncc = ceil_div(nj, cb);
+    if (c > nc0 && cb == ceil_div(nj, c - 1)) continue;  // same partition as c - 1
+    ++tried;
+    const int64_t units = n_srb * ncc, G = units < G0 ? units : G0;
+    load.assign(static_cast<size_t>(G), 0);
+    for (int64_t u = 0; u < units; ++u) {
+      const int64_t P = srow0 + u % n_srb;
+      if (P >= ns_active) continue;
+      const int64_t clo = lo + (u / n_srb) * cb, chi = clo + cb < hi ? clo + cb : hi;
+      load[static_cast<size_t>(u % G)] += sym2_pairs(P, clo, chi, skip_lo, skip_hi);
+    }
+    int64_t mx = 0;
+    for (int64_t v : load) mx = v > mx ? v : mx;
+    if (best_max < 0 || mx < best_max) {
+      best_max = mx;
+      best_nc = ncc;
+    }
+  }
+  Entry& e = cache[cache_next];
+  cache_next = (cache_next + 1) % 8;
+  for (int i = 0; i < 8; ++i) e.k[i] = key[i];
+  e.nc = best_nc;
+  return best_nc;
+}
+
 template <int KS>
-int launch_sym2(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint16_t* cols, int64_t scol0,
-                int64_t q_lo, int64_t q_hi, int64_t ns_active, int64_t ldh, int slice_off, int64_t* acc,
-                int grid_blocks, hipStream_t stream) {
+int launch_sym2(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint16_t* cols, int64_t jcol0,
+                int64_t j_lo, int64_t j_hi, int64_t skip_lo, int64_t skip_hi, int64_t ns_active, int64_t ldh,
+                int slice_off, int64_t* acc, int grid_blocks, hipStream_t stream) {
   const int G0 = grid_blocks > 0 ? grid_blocks : 2 * device_cus_split();
-  const int64_t nq = q_hi - q_lo;
-  const int64_t nc = sym_chunks(srow0, n_srb, q_lo, q_hi, ns_active, G0, 2);
-  const int64_t cbk = ceil_div(nq, nc);
-  const int64_t n_chunks = ceil_div(nq, cbk);
+  const int64_t nj = j_hi - j_lo;
+  const int64_t nc = sym2_chunks(srow0, n_srb, j_lo, j_hi, skip_lo, skip_hi, ns_active, G0);
+  const int64_t cbk = ceil_div(nj, nc);
+  const int64_t n_chunks = ceil_div(nj, cbk);
   const int64_t n_units = n_srb * n_chunks;
   const int64_t G = n_units < G0 ? n_units : G0;
   hipLaunchKernelGGL((gram_sym2_kernel<KS>), dim3(static_cast<unsigned>(G)), dim3(kSpThreads), 0, stream,
-                     rows, static_cast<int>(srow0), static_cast<int>(n_srb), cols, static_cast<int>(scol0),
-                     static_cast<int>(q_lo), static_cast<int>(q_hi), static_cast<int>(ns_active), ldh,
-                     slice_off, static_cast<int>(cbk), static_cast<int>(n_chunks),
-                     reinterpret_cast<unsigned long long*>(acc));
+                     rows, static_cast<int>(srow0), static_cast<int>(n_srb), cols, static_cast<int>(jcol0),
+                     static_cast<int>(j_lo), static_cast<int>(j_hi), static_cast<int>(skip_lo),
+                     static_cast<int>(skip_hi), static_cast<int>(ns_active), ldh, slice_off,
+                     static_cast<int>(cbk), static_cast<int>(n_chunks), reinterpret_cast<unsigned long long*>(acc));
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
 }
@@ -1376,13 +1435,13 @@ extern "C" int dal_gram_rowsum_split(const uint16_t* rows, int64_t n_rows_pad, c
   return DAL_OK;
 }
 
-extern "C" int dal_gram_rowsum_sym(const uint16_t* rows, int64_t row_block0, int64_t n_row_blocks,
-                                   const uint16_t* cols, int64_t col_block0, int64_t j_lo, int64_t j_hi,
-                                   int64_t nb_active, int64_t d_pad, int64_t* acc, int grid_blocks,
-                                   dal_stream_t stream) {
+extern "C" int dal_gram_rowsum_sym_skip(const uint16_t* rows, int64_t row_block0, int64_t n_row_blocks,
+                                        const uint16_t* cols, int64_t col_block0, int64_t j_lo, int64_t j_hi,
+                                        int64_t skip_lo, int64_t skip_hi, int64_t nb_active, int64_t d_pad,
+                                        int64_t* acc, int grid_blocks, dal_stream_t stream) {
   if (!rows || !cols || !acc) return DAL_ERR_ARG;
   if (row_block0 < 0 || n_row_blocks <= 0 || col_block0 < 0 || nb_active <= 0) return DAL_ERR_SHAPE;
-  if (j_lo < col_block0 || j_hi < j_lo || j_hi > nb_active) return DAL_ERR_SHAPE;
+  if (j_lo < col_block0 || j_hi < j_lo || j_hi > nb_active || skip_hi < skip_lo) return DAL_ERR_SHAPE;
   if (d_pad != dal_pad_features(d_pad)) return DAL_ERR_SHAPE;
   if ((reinterpret_cast<uintptr_t>(rows) | reinterpret_cast<uintptr_t>(cols)) & 15) return DAL_ERR_SHAPE;
   if (j_hi == j_lo || row_block0 >= nb_active) return DAL_OK;
@@ -1396,17 +1455,27 @@ extern "C" int dal_gram_rowsum_sym(const uint16_t* rows, int64_t row_block0, int
   const char* kenv = getenv("DAL_GRAM_SYM");
   const int kind = kenv && atoi(kenv) == 1 ? 1 : 2;
   if (kind == 2) {
-    // super-block form: every block index must be even (shards are 512-row multiples)
-    if ((row_block0 | n_row_blocks | col_block0 | j_lo | j_hi | nb_active) & 1) return DAL_ERR_SHAPE;
+    // super-block rows: the row blocks (and nb_active) must be even (shards are 512-row multiples)
+    if ((row_block0 | n_row_blocks | nb_active) & 1) return DAL_ERR_SHAPE;
     for (int64_t off = 0; off < d_pad; off += ks) {
       const int so = static_cast<int>(2 * off);
-      const int rc = ks == 32 ? launch_sym2<32>(rows, row_block0 / 2, n_row_blocks / 2, cols, col_block0 / 2,
-                                                j_lo / 2, j_hi / 2, nb_active / 2, ldh, so, acc, grid_blocks, st)
-                              : launch_sym2<64>(rows, row_block0 / 2, n_row_blocks / 2, cols, col_block0 / 2,
-                                                j_lo / 2, j_hi / 2, nb_active / 2, ldh, so, acc, grid_blocks, st);
+      const int rc = ks == 32 ? launch_sym2<32>(rows, row_block0 / 2, n_row_blocks / 2, cols, col_block0, j_lo, j_hi,
+                                                skip_lo, skip_hi, nb_active / 2, ldh, so, acc, grid_blocks, st)
+                              : launch_sym2<64>(rows, row_block0 / 2, n_row_blocks / 2, cols, col_block0, j_lo, j_hi,
+                                                skip_lo, skip_hi, nb_active / 2, ldh, so, acc, grid_blocks, st);
       if (rc != DAL_OK) return rc;
     }
     return DAL_OK;
+  }
+  if (skip_hi > skip_lo && skip_hi > j_lo && skip_lo < j_hi) {  // 256-row kernel: the two sides separately
+    int rc = DAL_OK;
+    if (skip_lo > j_lo)
+      rc = dal_gram_rowsum_sym_skip(rows, row_block0, n_row_blocks, cols, col_block0, j_lo, skip_lo, 0, 0,
+                                    nb_active, d_pad, acc, grid_blocks, stream);
+    if (rc == DAL_OK && skip_hi < j_hi)
+      rc = dal_gram_rowsum_sym_skip(rows, row_block0, n_row_blocks, cols, col_block0, skip_hi, j_hi, 0, 0,
+                                    nb_active, d_pad, acc, grid_blocks, stream);
+    return rc;
   }
   for (int64_t off = 0; off < d_pad; off += ks) {
     const int so = static_cast<int>(2 * off);
@@ -1427,4 +1496,12 @@ extern "C" int dal_gram_rowsum_sym(const uint16_t* rows, int64_t row_block0, int
     if (rc != DAL_OK) return rc;
   }
   return DAL_OK;
+}
+
+extern "C" int dal_gram_rowsum_sym(const uint16_t* rows, int64_t row_block0, int64_t n_row_blocks,
+                                   const uint16_t* cols, int64_t col_block0, int64_t j_lo, int64_t j_hi,
+                                   int64_t nb_active, int64_t d_pad, int64_t* acc, int grid_blocks,
+                                   dal_stream_t stream) {
+  return dal_gram_rowsum_sym_skip(rows, row_block0, n_row_blocks, cols, col_block0, j_lo, j_hi, 0, 0, nb_active,
+                                  d_pad, acc, grid_blocks, stream);
 }

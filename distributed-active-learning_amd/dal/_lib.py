@@ -58,6 +58,8 @@ SIGNATURES = {
     "dal_density_error_bound_sym": (c_double, [c_int64]),
     "dal_gram_rowsum_sym": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64, c_int64,
                                     c_int64, c_int64, c_void_p, c_int, c_void_p]),
+    "dal_gram_rowsum_sym_skip": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64, c_int64,
+                                         c_int64, c_int64, c_int64, c_int64, c_void_p, c_int, c_void_p]),
     "dal_forest_score": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32,
                                  c_int32, c_void_p, c_void_p, c_int, c_double, c_void_p, c_double,
                                  c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

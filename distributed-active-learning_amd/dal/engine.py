@@ -235,7 +235,8 @@ class PoolState:
         """Global count of 256-row blocks (pad512(N_total) / 256)."""
         return (self.n_total + 511) // 512 * 2
 
-    def gram_accumulate(self, acc, cols, n_cols_pad: int, grid_blocks: int = 0, col_row0: int = 0):
+    def gram_accumulate(self, acc, cols, n_cols_pad: int, grid_blocks: int = 0, col_row0: int = 0,
+                        skip=None):
         """acc += fixed-point row sums of this shard's rows against the first
         ``n_cols_pad`` (a multiple of 512) rows of ``cols`` (a Gram operand of
         the pool's kind), whose first row is global row ``col_row0``.  Exact:
@@ -243,7 +244,9 @@ class PoolState:
 
         gram "sym": acc is indexed by GLOBAL row (length >= nb_active * 256)
         and also receives the column sums of the pairs this shard owns (the
-        other ranks' rows included); the ranks' accs are summed afterwards."""
+        other ranks' rows included); the ranks' accs are summed afterwards.
+        ``skip`` = (row0, row1), global column rows (multiples of 256) left
+        out (gram "sym" only: already accumulated)."""
         torch = _torch()
         op = self.gram_operand()
         ev = None
@@ -254,10 +257,13 @@ class PoolState:
             nb = self.nb_active()
             j_lo = col_row0 // 256
             j_hi = min(j_lo + int(n_cols_pad) // 256, nb)
+            s_lo, s_hi = (0, 0) if skip is None else (skip[0] // 256, skip[1] // 256)
             if j_hi > j_lo and self.row_base // 256 < nb:
-                call("dal_gram_rowsum_sym", _ptr(op), self.row_base // 256, self.n_pad // 256,
-                     _ptr(cols), j_lo, j_lo, j_hi, nb, self.d_pad, _ptr(acc), int(grid_blocks),
+                call("dal_gram_rowsum_sym_skip", _ptr(op), self.row_base // 256, self.n_pad // 256,
+                     _ptr(cols), j_lo, j_lo, j_hi, s_lo, s_hi, nb, self.d_pad, _ptr(acc), int(grid_blocks),
                      _stream(self.device))
+        elif skip is not None:
+            raise ValueError("a skipped column range needs gram 'sym'")
         elif self.gram == "f32":
             call("dal_gram_rowsum", _ptr(op), self.n_pad, _ptr(cols), int(n_cols_pad), self.d_pad,
                  self.d_pad, _ptr(acc), int(grid_blocks), _stream(self.device))

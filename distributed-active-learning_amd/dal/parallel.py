@@ -128,9 +128,13 @@ class ShardedSelector:
             grid = max(1, 2 * (_device_cus(st.device) - reserve_cus)) if work is not None else 0
             st.gram_accumulate(acc, u_local, self.shard, grid_blocks=grid, col_row0=self.lo)
         comm.wait(work)
-        if st.n:
-            for c0, c1 in other_column_ranges(self.rank, self.world, self.shard):
-                st.gram_accumulate(acc, u_full[c0:c1], c1 - c0, col_row0=c0)
+        if st.n and self.world > 1:
+            if st.gram == "sym":  # one launch over every other column
+                st.gram_accumulate(acc, u_full, self.world * self.shard, col_row0=0,
+                                   skip=(self.lo, self.lo + self.shard))
+            else:
+                for c0, c1 in other_column_ranges(self.rank, self.world, self.shard):
+                    st.gram_accumulate(acc, u_full[c0:c1], c1 - c0, col_row0=c0)
         if st.gram == "sym":
             acc = comm.reduce_scatter_sum(acc)
         self.set_density(acc)
@@ -294,9 +298,12 @@ def select(sel: ShardedSelector, comm, unlabeled_idx, forest, k: int, mode: str 
     """One selection step across all ranks; returns (indices [k], scores [k]),
     identical on every rank."""
     u_local, parts = sel.prep()
+    # the (small) canonical partials travel first, asynchronously: on RCCL's
+    # stream they finish while the Gram runs, off the step's critical path
+    parts_full, pwork = comm.all_gather_start(parts) if mode == "dw" else (None, None)
     need_u = mode == "dw" and density_mode == "gram" and sel._density is None
     u_full = sel.exchange_density(comm, u_local) if need_u else None
-    parts_full = comm.all_gather(parts) if mode == "dw" else None
+    comm.wait(pwork)
     top = sel.local_select(u_full, parts_full, unlabeled_idx, forest, k, mode, strategy, beta,
                            density_mode)
     return merge_topk(*gather_topk(comm, top), k, sort_fn)

@@ -179,6 +179,13 @@ int dal_gram_rowsum_sym(const uint16_t* rows, int64_t row_block0, int64_t n_row_
                         const uint16_t* cols, int64_t col_block0, int64_t j_lo, int64_t j_hi,
                         int64_t nb_active, int64_t d_pad, int64_t* acc, int grid_blocks,
                         dal_stream_t stream);
+/* The same, skipping column blocks [skip_lo, skip_hi) (already processed, e.g.
+ * a GPU's own shard run beside the operand all-gather): one launch for all
+ * the other columns.  Row blocks must be even (512-row super blocks). */
+int dal_gram_rowsum_sym_skip(const uint16_t* rows, int64_t row_block0, int64_t n_row_blocks,
+                             const uint16_t* cols, int64_t col_block0, int64_t j_lo, int64_t j_hi,
+                             int64_t skip_lo, int64_t skip_hi, int64_t nb_active, int64_t d_pad,
+                             int64_t* acc, int grid_blocks, dal_stream_t stream);
 double dal_density_error_bound_sym(int64_t n_cols);
 
 /* ---- (a5-a10) forest votes + uncertainty / density-weighted score ------

@@ -572,8 +572,9 @@ class _RecordingComm:
         return t
 
 
+@pytest.mark.parametrize("kernel", ["2", "1"])
 @pytest.mark.parametrize("world,n", [(2, 5000), (3, 7000), (4, 2500), (8, 9000)])
-def test_exchange_density_column_split_bit_identical(cuda, world, n):
+def test_exchange_density_column_split_bit_identical(cuda, world, n, kernel, monkeypatch):
     """ShardedSelector.exchange_density (the RCCL path: own-shard launch with
     CUs left to the collective, then the other column ranges, then the
     reduce-scatter of the global accumulator) sums to the single-GPU density
@@ -582,6 +583,7 @@ def test_exchange_density_column_split_bit_identical(cuda, world, n):
     from dal import parallel
     from dal.engine import PoolState
 
+    monkeypatch.setenv("DAL_GRAM_SYM", kernel)
     d = 64
     X = O.synthetic_pool(n, d, seed=world)
     E = np.arange(10)
