@@ -26,6 +26,8 @@
 // 1.89 GHz the chip holds under this load).
 #include <type_traits>
 
+#include <stdlib.h>
+
 #include "common.hpp"
 
 namespace dal {
@@ -50,9 +52,9 @@ __device__ __forceinline__ float bf16_to_f32(uint16_t b) {
 // n-1, never stored); the stage-0 DMA is issued before the A fetch so both are
 // in flight together; d = 128 unrolls the stage loop twice so every B-fragment
 // address is a per-lane base plus an immediate.
-template <int DK, int OCC>
+template <int DK, int OCC, int NW = 4>
 struct Mc2Cfg {
-  static constexpr int STAGE = OCC == 2 ? 32768 : 65536;
+  static constexpr int STAGE = (OCC == 2 || NW == 8) ? 32768 : 65536;
   static constexpr int F4 = STAGE / 16;
   static constexpr int ROWB = DK * 2;
   static constexpr int SLOTS = ROWB / 16;
@@ -60,24 +62,27 @@ struct Mc2Cfg {
   static constexpr int NCT = SR / 32;
   static constexpr int NKS = DK / 16;
   static constexpr int SWZ = (SLOTS < 16 ? SLOTS : 16) - 1;
-  static constexpr int PIECES = STAGE / (4 * 1024);  // 1 KiB LDS-DMA pieces per wave per stage
+  static constexpr int PIECES = STAGE / (NW * 1024);  // 1 KiB LDS-DMA pieces per wave per stage
 };
 
-template <int DK, int OCC>
-__global__ __launch_bounds__(kMcThreads, OCC) void maxcos2_kernel(
+// NW = waves per block (64 pool rows each).  NW = 8 (one 512-thread block per
+// CU, still two waves per SIMD, half the DMA issue per MFMA) measured 12 %
+// slower than NW = 4 at 8M x 128 (barriers over 8 waves), so NW = 4 is used.
+template <int DK, int OCC, int NW>
+__global__ __launch_bounds__(64 * NW, OCC) void maxcos2_kernel(
     const uint16_t* __restrict__ pool, int64_t n, const uint16_t* __restrict__ lab, int64_t m_pad,
     const float* __restrict__ inv_lab, const float* __restrict__ inv_pool, float* __restrict__ out,
     int32_t* __restrict__ status) {
-  using C = Mc2Cfg<DK, OCC>;
+  using C = Mc2Cfg<DK, OCC, NW>;
   extern __shared__ __attribute__((aligned(16))) float4 mc_dyn[];
   float4* lds = mc_dyn;
   float* invl = reinterpret_cast<float*>(mc_dyn + 2 * C::F4);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int li = lane & 31, lh = lane >> 5;
-  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kMcRows + wave * 64;
+  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * (64 * NW) + wave * 64;
   const int n_stages = static_cast<int>(m_pad / C::SR);
 
-  for (int i = tid; i < m_pad; i += kMcThreads) invl[i] = inv_lab[i];
+  for (int i = tid; i < m_pad; i += 64 * NW) invl[i] = inv_lab[i];
 
   // per-piece source offsets (swizzled) and the wave's LDS base, computed once
   unsigned voff[C::PIECES];
@@ -207,11 +212,15 @@ __global__ __launch_bounds__(kMcThreads, OCC) void maxcos2_kernel(
       }
     }
   };
-  if constexpr (OCC == 2 && DK == 128) {
+  if constexpr (DK == 128 && (OCC == 2 || NW == 8)) {
     // the label granule (65536 / (2d) rows) is two 32 KiB stages: n_stages is even
-    for (int st = 0; st < n_stages; st += 2) {
-      stage_body(std::integral_constant<int, 0>{}, st);
-      stage_body(std::integral_constant<int, 1>{}, st + 1);
+    if ((n_stages & 1) == 0) {
+      for (int st = 0; st < n_stages; st += 2) {
+        stage_body(std::integral_constant<int, 0>{}, st);
+        stage_body(std::integral_constant<int, 1>{}, st + 1);
+      }
+    } else {
+      for (int st = 0; st < n_stages; ++st) stage_body_rt(st);
     }
   } else {
     // d = 64 unrolled twice exceeds the 256-register budget: keep one body
@@ -298,10 +307,10 @@ int launch_maxcos(const uint16_t* pool, int64_t n, const uint16_t* lab, int64_t 
   const int64_t blocks = ceil_div(n, kMcRows);
   constexpr int OCC = DK <= 128 ? 2 : 1;
   const size_t shm = 2 * Mc2Cfg<DK, OCC>::STAGE + static_cast<size_t>(m_pad) * 4;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(maxcos2_kernel<DK, OCC>),
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(maxcos2_kernel<DK, OCC, 4>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm)) != hipSuccess)
     return DAL_ERR_HIP;
-  hipLaunchKernelGGL((maxcos2_kernel<DK, OCC>), dim3(static_cast<unsigned>(blocks)), dim3(kMcThreads), shm, st,
+  hipLaunchKernelGGL((maxcos2_kernel<DK, OCC, 4>), dim3(static_cast<unsigned>(blocks)), dim3(kMcThreads), shm, st,
                      pool, n, lab, m_pad, inv_lab, inv_pool, out, status);
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;

@@ -30,6 +30,8 @@ for n, d, m in shapes:
     for r in range(rounds + 1):
         for v in variants:
             os.environ["DAL_MAXCOS_VARIANT"] = v
+            if v.startswith("nw"):
+                os.environ["DAL_MAXCOS_NW"] = v[2:]
             out = torch.empty(n, dtype=torch.float32, device=dev)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize()
