@@ -731,7 +731,7 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
     const uint16_t* __restrict__ urows, int srow0, int n_srb,
     const uint16_t* __restrict__ ucols, int jcol0, int j_lo, int j_hi, int skip_lo, int skip_hi,
     int ns_active, int64_t ldh, int slice_off, int chunk_j, int n_chunks,
-    unsigned long long* __restrict__ acc_out) {
+    unsigned long long* __restrict__ acc_out, int a_nt) {
   using C = Sym2Cfg<KS>;
   using A = SpAcc<16>;
   using acc_t = A::type;
@@ -814,8 +814,13 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
 #pragma unroll
       for (int c = 0; c < C::NKS; ++c) {
         const unsigned o = lrow + rt * tstep + c * C::LG * 8;
-        ah[rt][c] = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(pb + o));
-        al[rt][c] = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(pb + o + KS));
+        if (a_nt) {  // read once per unit: keep the column stages resident in L2
+          ah[rt][c] = __builtin_nontemporal_load(reinterpret_cast<const f16x8*>(pb + o));
+          al[rt][c] = __builtin_nontemporal_load(reinterpret_cast<const f16x8*>(pb + o + KS));
+        } else {
+          ah[rt][c] = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(pb + o));
+          al[rt][c] = __builtin_bit_cast(f16x8, *reinterpret_cast<const uint4*>(pb + o + KS));
+        }
       }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -1324,7 +1329,8 @@ int launch_sym2(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint16
                      rows, static_cast<int>(srow0), static_cast<int>(n_srb), cols, static_cast<int>(jcol0),
                      static_cast<int>(j_lo), static_cast<int>(j_hi), static_cast<int>(skip_lo),
                      static_cast<int>(skip_hi), static_cast<int>(ns_active), ldh, slice_off,
-                     static_cast<int>(cbk), static_cast<int>(n_chunks), reinterpret_cast<unsigned long long*>(acc));
+                     static_cast<int>(cbk), static_cast<int>(n_chunks), reinterpret_cast<unsigned long long*>(acc),
+                     getenv("DAL_GRAM_ANT") ? atoi(getenv("DAL_GRAM_ANT")) : 1);
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
 }
