@@ -443,14 +443,16 @@ def workspace(nbytes: int, device):
 
 
 def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k: int,
-                    beta: float, colsum):
+                    beta: float, colsum, cap_scale: int = 1, sync: bool = True):
     """dal_dw_select on this shard: exact canonical top-k of the shard.  The
-    candidate capacity grows (and the step re-runs) on DAL_FLAG_CAND_OVERFLOW."""
+    candidate capacity grows (and the step re-runs) on DAL_FLAG_CAND_OVERFLOW.
+    sync=False: no status read here -- the caller checks state.status later
+    and re-runs with a larger cap_scale on overflow (multi-GPU path)."""
     torch = _torch()
     lib = _lib.load()
     n = state.n
     norm64 = state.norms()
-    cap = candidate_cap(n, k)
+    cap = int(min(n, candidate_cap(n, k) * cap_scale))
     while True:
         wsb = int(lib.dal_dw_select_workspace_bytes(n, k, cap))
         ws, wsp = workspace(wsb, state.device)
@@ -461,6 +463,8 @@ def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k
              state.row_base, _ptr(lut_dev), float(beta), _ptr(state.x), state.d, state.d,
              _ptr(norm64), _ptr(colsum), cap, wsp, wsb, _ptr(out_idx), _ptr(out_scores),
              _ptr(out_keys), _ptr(state.status), _stream(state.device))
+        if not sync:
+            return out_idx, out_scores, out_keys
         # the step's one host sync: status word (zero-norm rows, candidate overflow)
         st = int(state.status.item())
         if cap >= n or not (st & DAL_FLAG_CAND_OVERFLOW):

@@ -63,18 +63,21 @@ class LocalTopk:
     scores: object  # fp64 [k]
 
 
-def merge_topk(keys_all, idx_all, scores_all, k: int, sort_fn):
+def merge_topk(keys_all, idx_all, scores_all, k: int, sort_fn, all_valid: bool = False):
     """Deterministic merge of P gathered local top-k lists (rank-major).
 
     Each list is sorted by (key, index) and shards are in global index order,
     so sorting by (key, position) orders ties by global index; ``sort_fn``
-    returns the positions of the k best."""
+    returns the positions of the k best.  ``all_valid``: at least k candidates
+    exist globally, so no padding key can reach the k best and the filter
+    (a host sync) is skipped."""
     torch = __import__("torch")
     n = int(keys_all.shape[0])
     pos = torch.arange(n, dtype=torch.int64, device=keys_all.device)
     best = sort_fn(keys_all, pos, k)
-    valid = keys_all[best] != _as_i64(DAL_KEY_NONE)
-    best = best[valid]
+    if not all_valid:
+        valid = keys_all[best] != _as_i64(DAL_KEY_NONE)
+        best = best[valid]
     return idx_all[best], scores_all[best]
 
 
@@ -96,6 +99,51 @@ class ShardedSelector:
         self.state = PoolState(x_local, excluded=excluded, device=device, row_base=self.lo,
                                n_total=self.n_total, n_pad=self.shard, gram=gram)
         self._density = None
+        self._ncand = None      # (pinned host count, event) of this shard's candidates
+        self.cap_scale = 1      # re-rank candidate capacity multiplier (grown on overflow)
+
+    def index_tensor(self, unlabeled_idx):
+        from .engine import _as_index
+
+        return _as_index(unlabeled_idx, self.state.device)
+
+    def status_word(self):
+        """This rank's device status word (DAL_FLAG_* bits), int32 [1]."""
+        return self.state.status
+
+    def prepare_retry(self):
+        """After a re-rank capacity overflow anywhere: clear, grow, go again."""
+        self.state.status.zero_()
+        self.cap_scale *= 4
+        self.state.clear_caches()
+        self._density = None
+
+    def count_candidates_async(self, unlabeled_idx):
+        """Queue the count of this shard's unlabeled rows; local_select reads it
+        after the Gram is in flight, so the stream never drains for it."""
+        torch = __import__("torch")
+        from .engine import _as_index
+
+        st = self.state
+        if st.n == 0:
+            self._ncand = None
+            return
+        unl = _as_index(unlabeled_idx, st.device)
+        cnt = ((unl >= st.row_base) & (unl < st.row_base + st.n)).sum()
+        host = torch.empty((), dtype=torch.int64, pin_memory=True)
+        host.copy_(cnt, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._ncand = (host, ev)
+
+    def _candidates(self, unl) -> int:
+        if self._ncand is None:
+            st = self.state
+            return int(((unl >= st.row_base) & (unl < st.row_base + st.n)).sum().item())
+        host, ev = self._ncand
+        self._ncand = None
+        ev.synchronize()
+        return int(host.item())
 
     # ---- phase A: local normalisation + canonical partials ------------
     def prep(self):
@@ -174,15 +222,18 @@ class ShardedSelector:
 
         torch = __import__("torch")
         st = self.state
-        keys = torch.full((k,), _as_i64(DAL_KEY_NONE), dtype=torch.int64, device=st.device)
-        idx = torch.full((k,), -1, dtype=torch.int64, device=st.device)
-        scores = torch.full((k,), float("nan"), dtype=torch.float64, device=st.device)
+
+        def empty():
+            return LocalTopk(torch.full((k,), _as_i64(DAL_KEY_NONE), dtype=torch.int64, device=st.device),
+                             torch.full((k,), -1, dtype=torch.int64, device=st.device),
+                             torch.full((k,), float("nan"), dtype=torch.float64, device=st.device))
+
         if st.n == 0:
-            return LocalTopk(keys, idx, scores)
+            return empty()
         flags, unl, _ = st.row_flags(unlabeled_idx)
-        n_cand = int(((unl >= st.row_base) & (unl < st.row_base + st.n)).sum().item())
+        n_cand = self._candidates(unl)
         if n_cand == 0:
-            return LocalTopk(keys, idx, scores)
+            return empty()
         kk = min(k, n_cand)
         if mode == "dw" and density_mode == "separable":
             colsum = st.colsum(partials_full)
@@ -197,16 +248,19 @@ class ShardedSelector:
             lut_dev = device_lut("entropy", forest.n_trees, st.device)
             votes, sc, klo, khi = forest_score(st, forest, lut_dev, flags, DAL_DESCENDING, density=dens,
                                                density_err=density_error(st), beta=beta, want_hi=True)
-            i, s, kk_keys = dw_select_local(st, flags, votes, klo, khi, lut_dev, kk, beta, colsum)
+            i, s, kk_keys = dw_select_local(st, flags, votes, klo, khi, lut_dev, kk, beta, colsum,
+                                            cap_scale=self.cap_scale, sync=False)
         else:
             order = DAL_ASCENDING if ASCENDING[strategy] else DAL_DESCENDING
             lut_dev = device_lut(strategy, forest.n_trees, st.device)
             votes, sc, kys, _ = forest_score(st, forest, lut_dev, flags, order)
             i, kk_keys = topk_keys(kys, kk, st.row_base)
             s = sc[i - st.row_base]
-        keys[:kk], idx[:kk], scores[:kk] = kk_keys, i, s
-        st.check_status()
-        return LocalTopk(keys, idx, scores)
+        if kk == k:  # every slot written by the selection
+            return LocalTopk(kk_keys, i, s)
+        out = empty()
+        out.keys[:kk], out.idx[:kk], out.scores[:kk] = kk_keys, i, s
+        return out
 
 
 def other_column_ranges(rank: int, world: int, shard: int):
@@ -297,28 +351,52 @@ def select(sel: ShardedSelector, comm, unlabeled_idx, forest, k: int, mode: str 
            density_mode: str = "gram"):
     """One selection step across all ranks; returns (indices [k], scores [k]),
     identical on every rank."""
+    unl = sel.index_tensor(unlabeled_idx)
     u_local, parts = sel.prep()
+    sel.count_candidates_async(unl)
     # the (small) canonical partials travel first, asynchronously: on RCCL's
     # stream they finish while the Gram runs, off the step's critical path
     parts_full, pwork = comm.all_gather_start(parts) if mode == "dw" else (None, None)
     need_u = mode == "dw" and density_mode == "gram" and sel._density is None
     u_full = sel.exchange_density(comm, u_local) if need_u else None
     comm.wait(pwork)
-    top = sel.local_select(u_full, parts_full, unlabeled_idx, forest, k, mode, strategy, beta,
-                           density_mode)
-    return merge_topk(*gather_topk(comm, top), k, sort_fn)
+    top = sel.local_select(u_full, parts_full, unl, forest, k, mode, strategy, beta, density_mode)
+    # every rank's status word (zero-norm rows, re-rank capacity overflow)
+    # rides in the top-k all-gather and is read once, after the merge is
+    # queued: the step's one host sync, and every rank sees the same bits
+    keys_all, idx_all, sc_all, st_all = gather_topk(comm, top, sel.status_word())
+    n_unl_global = int(unl.shape[0])  # single source of truth for the candidate count
+    out = merge_topk(keys_all, idx_all, sc_all, k, sort_fn, all_valid=n_unl_global >= k)
+    st = 0
+    for v in st_all.tolist():
+        st |= int(v)
+    if st & _lib.DAL_FLAG_ZERO_NORM:
+        raise ValueError("pool contains a zero-norm row: cosine similarity is undefined "
+                         "(the reference would propagate NaN into every density)")
+    if st & _lib.DAL_FLAG_CAND_OVERFLOW:  # rare: grow the re-rank capacity everywhere and redo
+        sel.prepare_retry()
+        return select(sel, comm, unlabeled_idx, forest, k, mode, strategy, beta, sort_fn, density_mode)
+    return out
 
 
-def gather_topk(comm, top: LocalTopk):
+def gather_topk(comm, top: LocalTopk, status=None):
     """ONE all-gather of every rank's (key, index, score) triples, packed as
-    int64 [3, k] (scores by bit pattern): a collective's latency, not its
-    bytes, dominates at k = 100-1000."""
+    int64 [3k] (scores by bit pattern), plus the rank's status word when
+    given: a collective's latency, not its bytes, dominates at k = 100-1000.
+    Returns (keys, idx, scores) rank-major [P*k] (+ statuses [P])."""
     torch = __import__("torch")
     k = int(top.keys.shape[0])
-    packed = torch.stack([top.keys, top.idx, top.scores.view(torch.int64)])  # [3, k]
-    g = comm.all_gather(packed.reshape(1, 3 * k)).reshape(-1, 3, k)       # [P, 3, k]
-    return (g[:, 0].reshape(-1), g[:, 1].reshape(-1),
-            g[:, 2].reshape(-1).contiguous().view(torch.float64))
+    parts = [top.keys, top.idx, top.scores.view(torch.int64)]
+    if status is not None:
+        parts.append(status.reshape(1).to(torch.int64))
+    packed = torch.cat(parts)
+    w = int(packed.shape[0])
+    g = comm.all_gather(packed.reshape(1, w)).reshape(-1, w)              # [P, 3k (+1)]
+    out = (g[:, :k].reshape(-1), g[:, k:2 * k].reshape(-1),
+           g[:, 2 * k:3 * k].reshape(-1).contiguous().view(torch.float64))
+    if status is not None:
+        out = out + (g[:, 3 * k],)
+    return out
 
 
 def emulate(selectors, unlabeled_idx, forest, k: int, mode: str = "dw",
@@ -344,7 +422,10 @@ def emulate(selectors, unlabeled_idx, forest, k: int, mode: str = "dw",
     keys_all = torch.cat([t.keys for t in tops])
     idx_all = torch.cat([t.idx for t in tops])
     sc_all = torch.cat([t.scores for t in tops])
-    return merge_topk(keys_all, idx_all, sc_all, k, sort_fn)
+    out = merge_topk(keys_all, idx_all, sc_all, k, sort_fn)
+    for s in selectors:
+        s.state.check_status()
+    return out
 
 
 def diversity_select_sharded(x_local, row_base: int, labeled_rows, k: int, comm, candidates=None,

@@ -1,0 +1,5 @@
+set -u
+R=$GRAFT_REPO_ROOT
+cd $R
+timeout -k 10 300 python -u scripts/sharded_overhead.py 20 > gpurun_out/sharded_overhead.log 2>&1; rc=$?
+echo "rc=$rc"; grep -v amdgpu.ids gpurun_out/sharded_overhead.log | tail -8

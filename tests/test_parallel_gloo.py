@@ -57,6 +57,15 @@ class OracleShard(parallel.ShardedSelector):
     def exchange_density(self, comm, u_local):
         return comm.all_gather(u_local)
 
+    def index_tensor(self, unl):
+        return torch.as_tensor(np.asarray(unl), dtype=torch.int64)
+
+    def count_candidates_async(self, unl):
+        pass
+
+    def status_word(self):
+        return torch.zeros(1, dtype=torch.int32)
+
     def local_select(self, u_full, parts_full, unl, forest, k, mode="dw", strategy="least_confidence",
                      beta=1.0, density_mode="gram"):
         keys = torch.full((k,), parallel._as_i64(0xFFFFFFFFFFFFFFFF), dtype=torch.int64)
