@@ -337,6 +337,11 @@ __global__ __launch_bounds__(256) void rerank_kernel(const TopkHdr* __restrict__
     return;
   }
   const int64_t i = cidx[c] - idx_base;
+  if (flags && !(flags[i] & DAL_ROW_CANDIDATE)) {  // filler when a shard has < k candidates
+    cpay[c] = __builtin_nan("");
+    ckey[c] = DAL_KEY_NONE;
+    return;
+  }
   const double nr = norm64[i];
   const float* xr = x + i * ldx;
   double acc = 0.0;

@@ -99,7 +99,6 @@ class ShardedSelector:
         self.state = PoolState(x_local, excluded=excluded, device=device, row_base=self.lo,
                                n_total=self.n_total, n_pad=self.shard, gram=gram)
         self._density = None
-        self._ncand = None      # (pinned host count, event) of this shard's candidates
         self.cap_scale = 1      # re-rank candidate capacity multiplier (grown on overflow)
 
     def index_tensor(self, unlabeled_idx):
@@ -117,33 +116,6 @@ class ShardedSelector:
         self.cap_scale *= 4
         self.state.clear_caches()
         self._density = None
-
-    def count_candidates_async(self, unlabeled_idx):
-        """Queue the count of this shard's unlabeled rows; local_select reads it
-        after the Gram is in flight, so the stream never drains for it."""
-        torch = __import__("torch")
-        from .engine import _as_index
-
-        st = self.state
-        if st.n == 0:
-            self._ncand = None
-            return
-        unl = _as_index(unlabeled_idx, st.device)
-        cnt = ((unl >= st.row_base) & (unl < st.row_base + st.n)).sum()
-        host = torch.empty((), dtype=torch.int64, pin_memory=True)
-        host.copy_(cnt, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        self._ncand = (host, ev)
-
-    def _candidates(self, unl) -> int:
-        if self._ncand is None:
-            st = self.state
-            return int(((unl >= st.row_base) & (unl < st.row_base + st.n)).sum().item())
-        host, ev = self._ncand
-        self._ncand = None
-        ev.synchronize()
-        return int(host.item())
 
     # ---- phase A: local normalisation + canonical partials ------------
     def prep(self):
@@ -231,10 +203,10 @@ class ShardedSelector:
         if st.n == 0:
             return empty()
         flags, unl, _ = st.row_flags(unlabeled_idx)
-        n_cand = self._candidates(unl)
-        if n_cand == 0:
-            return empty()
-        kk = min(k, n_cand)
+        # no host count of this shard's candidates (a sync): rows that are not
+        # candidates carry the padding key, so with fewer than k candidates
+        # they fill the local list last and never survive a merge that has k
+        kk = min(k, st.n)
         if mode == "dw" and density_mode == "separable":
             colsum = st.colsum(partials_full)
             lut_dev = device_lut("entropy", forest.n_trees, st.device)
@@ -353,7 +325,6 @@ def select(sel: ShardedSelector, comm, unlabeled_idx, forest, k: int, mode: str 
     identical on every rank."""
     unl = sel.index_tensor(unlabeled_idx)
     u_local, parts = sel.prep()
-    sel.count_candidates_async(unl)
     # the (small) canonical partials travel first, asynchronously: on RCCL's
     # stream they finish while the Gram runs, off the step's critical path
     parts_full, pwork = comm.all_gather_start(parts) if mode == "dw" else (None, None)
@@ -422,7 +393,9 @@ def emulate(selectors, unlabeled_idx, forest, k: int, mode: str = "dw",
     keys_all = torch.cat([t.keys for t in tops])
     idx_all = torch.cat([t.idx for t in tops])
     sc_all = torch.cat([t.scores for t in tops])
-    out = merge_topk(keys_all, idx_all, sc_all, k, sort_fn)
+    n_unl = int(np.asarray(unlabeled_idx).reshape(-1).shape[0]) if not hasattr(unlabeled_idx, "shape") \
+        else int(unlabeled_idx.shape[0])
+    out = merge_topk(keys_all, idx_all, sc_all, k, sort_fn, all_valid=n_unl >= k)
     for s in selectors:
         s.state.check_status()
     return out

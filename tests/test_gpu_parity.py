@@ -552,6 +552,33 @@ def test_sharded_emulation_bit_identical(cuda, world, mode):
     assert np.array_equal(_np(sc), o_sc)
 
 
+@pytest.mark.parametrize("case", ["sparse-shard", "fewer-than-k"])
+def test_sharded_selection_with_few_candidates(cuda, case):
+    """A shard with fewer unlabeled rows than k (and a pool with fewer than k
+    in all): non-candidate rows fill the local lists last with the padding
+    key and never reach the merged selection."""
+    from dal import parallel
+    from dal.forest import Forest
+
+    n, d, k, world = 5000, 32, 50, 3
+    X = O.synthetic_pool(n, d, seed=5)
+    of = O.synthetic_forest(10, 4, d, seed=1)
+    F = Forest.synthetic(10, 4, d, seed=1)
+    E = np.arange(10)
+    if case == "sparse-shard":
+        unl = np.concatenate([np.arange(10, 1700), np.arange(4990, 5000)])
+    else:
+        unl = np.array([12, 40, 999, 2048, 3000, 3001, 4500, 4999])
+    sels = []
+    for r in range(world):
+        lo, hi, _ = parallel.shard_range(n, world, r)
+        sels.append(parallel.ShardedSelector(X[lo:hi], n, r, world, excluded=E, device=cuda))
+    idx, sc = parallel.emulate(sels, unl, F, k, mode="dw")
+    _, o_idx, o_sc = O.density_select(X, unl, of, k, 1.0, E)
+    assert np.array_equal(_np(idx), o_idx)
+    assert np.array_equal(_np(sc), o_sc)
+
+
 class _RecordingComm:
     """Single-process stand-in for TorchComm: the all-gather returns the
     precomputed gathered operand (asynchronously: a work handle), the

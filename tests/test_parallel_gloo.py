@@ -60,9 +60,6 @@ class OracleShard(parallel.ShardedSelector):
     def index_tensor(self, unl):
         return torch.as_tensor(np.asarray(unl), dtype=torch.int64)
 
-    def count_candidates_async(self, unl):
-        pass
-
     def status_word(self):
         return torch.zeros(1, dtype=torch.int32)
 
