@@ -1034,10 +1034,18 @@ __global__ __launch_bounds__(256) void normalize_split_kernel(
   const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kNsRows;
   double n2 = 0.0;
   for (int c0 = 0; c0 < d; c0 += 64) {
-    for (int e = tid; e < kNsRows * 64; e += 256) {
-      const int r = e / 64, c = e % 64;
+    // 16 independent loads per thread, all in flight before the LDS writes
+    float v[kNsRows * 64 / 256];
+#pragma unroll
+    for (int j = 0; j < kNsRows * 64 / 256; ++j) {
+      const int e = tid + 256 * j, r = e / 64, c = e % 64;
       const int64_t row = row0 + r;
-      tile[r][c] = (row < n && c0 + c < d) ? x[row * ldx + c0 + c] : 0.0f;
+      v[j] = (row < n && c0 + c < d) ? x[row * ldx + c0 + c] : 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < kNsRows * 64 / 256; ++j) {
+      const int e = tid + 256 * j;
+      tile[e / 64][e % 64] = v[j];
     }
     __syncthreads();
     if (tid < kNsRows) {

@@ -94,13 +94,24 @@ __global__ __launch_bounds__(256) void canon_colsum_partials_kernel(
   // Excluded / padding rows contribute +0.0: the running sum starts at +0.0
   // and can never become -0.0, so adding +0.0 is bit-identical to skipping.
   constexpr int kRowsPerPass = 256 / kColFeat;
+  // all loads of the thread's 16 rows first (in flight together), then the
+  // divisions: a load-then-divide loop would serialise 16 memory latencies
+  constexpr int kPer = DAL_CANON_CHUNK / kRowsPerPass;
+  float xv[kPer];
+  double nv[kPer];
+  bool lv[kPer];
 #pragma unroll
-  for (int k = 0; k < DAL_CANON_CHUNK / kRowsPerPass; ++k) {
-    const int rl = rs + k * kRowsPerPass;
-    const int64_t r = c * DAL_CANON_CHUNK + rl;
-    const bool live = r < n && f < d && !(flags && (flags[r] & DAL_ROW_EXCLUDED));
-    u[rl][fl] = live ? static_cast<double>(x[r * ldx + f]) / norm64[r] : 0.0;
+  for (int k = 0; k < kPer; ++k) {
+    const int64_t r = c * DAL_CANON_CHUNK + rs + k * kRowsPerPass;
+    lv[k] = r < n && f < d;
+    const int64_t rr = lv[k] ? r : 0;
+    xv[k] = lv[k] ? x[rr * ldx + f] : 0.0f;
+    nv[k] = lv[k] ? norm64[rr] : 1.0;
+    if (lv[k] && flags && (flags[rr] & DAL_ROW_EXCLUDED)) lv[k] = false;
   }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k)
+    u[rs + k * kRowsPerPass][fl] = lv[k] ? static_cast<double>(xv[k]) / nv[k] : 0.0;
   __syncthreads();
   if (tid >= kColFeat || f >= d) return;
   double acc = 0.0;
@@ -157,9 +168,20 @@ __global__ __launch_bounds__(256) void canon_colsum_reduce_kernel(const double* 
   double acc = 0.0;
   for (int64_t c0 = 0; c0 < n_chunks; c0 += kRedTile) {
     const int m = static_cast<int>(n_chunks - c0 < kRedTile ? n_chunks - c0 : kRedTile);
-    for (int e = tid; e < m * kRedFeat; e += 256) {
-      const int ci = e / kRedFeat, fl = e % kRedFeat;
-      t[ci][fl] = f0 + fl < d ? partials[(c0 + ci) * d + f0 + fl] : 0.0;
+    // staging: batches of 16 independent loads per thread (latency overlapped)
+    for (int e0 = 0; e0 < m * kRedFeat; e0 += 256 * 16) {
+      double v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int e = e0 + j * 256 + tid;
+        const int ci = e / kRedFeat, fl = e % kRedFeat;
+        v[j] = (e < m * kRedFeat && f0 + fl < d) ? partials[(c0 + ci) * d + f0 + fl] : 0.0;
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int e = e0 + j * 256 + tid;
+        if (e < m * kRedFeat) t[e / kRedFeat][e % kRedFeat] = v[j];
+      }
     }
     __syncthreads();
     if (tid < kRedFeat) {
