@@ -132,22 +132,46 @@ class ShardedSelector:
         return u, parts
 
     # ---- exchange 1 overlapped with the own-shard columns ---------------
-    def exchange_density(self, comm, u_local, reserve_cus: int = RCCL_RESERVED_CUS):
-        """All-gather the shards' Gram operands while this rank's rows run
-        against its OWN columns (the operand it already holds), then against
-        the other shards' columns; returns the gathered operand.  Every column
-        range is a whole number of shards (multiples of 512), so the exact
-        fixed-point sum is the same bits as one call over all columns.  The
-        own-shard launch leaves ``reserve_cus`` CUs free for RCCL's kernels.
+    def exchange_density(self, comm, u_local, parts=None, reserve_cus: int = RCCL_RESERVED_CUS):
+        """All-gather the shards' Gram operands (and the canonical partials)
+        while this rank's rows run against its OWN columns (the operand it
+        already holds), then against the other shards' columns; returns
+        (gathered operand, gathered partials).  Every column range is a whole
+        number of shards (multiples of 512), so the exact fixed-point sum is the
+        same bits as one call over all columns.
+
+        With RCCL (``comm.overlaps``) the own-shard Gram is queued FIRST, on
+        all but ``reserve_cus`` CUs, and the collectives are enqueued behind it
+        from a side stream that only waits for the operand -- the host's
+        collective-issue time runs under the Gram instead of in front of it.
         gram "sym": the accumulator spans every global row (this rank's pairs
         also yield column sums for other ranks' rows) and is reduce-scattered."""
+        torch = __import__("torch")
         st = self.state
-        u_full, work = comm.all_gather_start(u_local)
         acc = self._new_acc()
-        if st.n:
-            grid = max(1, 2 * (_device_cus(st.device) - reserve_cus)) if work is not None else 0
+        if getattr(comm, "overlaps", False) and st.n:
+            main = torch.cuda.current_stream(st.device)
+            ready = main.record_event()
+            grid = max(1, 2 * (_device_cus(st.device) - reserve_cus))
             st.gram_accumulate(acc, u_local, self.shard, grid_blocks=grid, col_row0=self.lo)
-        comm.wait(work)
+            side = _side_stream(st.device)
+            side.wait_event(ready)
+            with torch.cuda.stream(side):
+                parts_full, pwork = comm.all_gather_start(parts) if parts is not None else (None, None)
+                u_full, work = comm.all_gather_start(u_local)
+            for t in (u_full, parts_full):
+                if t is not None:
+                    t.record_stream(main)
+            main.wait_stream(side)
+            comm.wait(work)   # the current (main) stream waits for the collectives
+            comm.wait(pwork)
+        else:
+            parts_full, pwork = comm.all_gather_start(parts) if parts is not None else (None, None)
+            u_full, work = comm.all_gather_start(u_local)
+            if st.n:
+                st.gram_accumulate(acc, u_local, self.shard, col_row0=self.lo)
+            comm.wait(work)
+            comm.wait(pwork)
         if st.n and self.world > 1:
             if st.gram == "sym":  # one launch over every other column
                 st.gram_accumulate(acc, u_full, self.world * self.shard, col_row0=0,
@@ -158,7 +182,7 @@ class ShardedSelector:
         if st.gram == "sym":
             acc = comm.reduce_scatter_sum(acc)
         self.set_density(acc)
-        return u_full
+        return u_full, parts_full
 
     def _new_acc(self):
         torch = __import__("torch")
@@ -267,6 +291,19 @@ def _needs_bytes(dtype) -> bool:
     return any(getattr(torch, n, None) == dtype for n in names)
 
 
+_SIDE_STREAMS = {}
+
+
+def _side_stream(device):
+    """A second stream per device from which collectives are enqueued behind
+    an already queued Gram launch."""
+    torch = __import__("torch")
+    key = str(device)
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
+    return _SIDE_STREAMS[key]
+
+
 class TorchComm:
     """all-gather over torch.distributed (RCCL on ROCm GPUs, gloo on CPU)."""
 
@@ -276,6 +313,9 @@ class TorchComm:
         self.dist = dist
         self.group = group
         self.world = dist.get_world_size(group)
+        # RCCL collectives are asynchronous on their own stream: they can run
+        # beside a Gram launch (gloo stages through the host synchronously)
+        self.overlaps = dist.get_backend(group) == "nccl"
 
     def all_gather(self, t):
         out, work = self.all_gather_start(t)
@@ -325,12 +365,12 @@ def select(sel: ShardedSelector, comm, unlabeled_idx, forest, k: int, mode: str 
     identical on every rank."""
     unl = sel.index_tensor(unlabeled_idx)
     u_local, parts = sel.prep()
-    # the (small) canonical partials travel first, asynchronously: on RCCL's
-    # stream they finish while the Gram runs, off the step's critical path
-    parts_full, pwork = comm.all_gather_start(parts) if mode == "dw" else (None, None)
     need_u = mode == "dw" and density_mode == "gram" and sel._density is None
-    u_full = sel.exchange_density(comm, u_local) if need_u else None
-    comm.wait(pwork)
+    if need_u:  # the (small) canonical partials travel with the operand, beside the Gram
+        u_full, parts_full = sel.exchange_density(comm, u_local, parts)
+    else:
+        u_full = None
+        parts_full = comm.all_gather(parts) if mode == "dw" else None
     top = sel.local_select(u_full, parts_full, unl, forest, k, mode, strategy, beta, density_mode)
     # every rank's status word (zero-norm rows, re-rank capacity overflow)
     # rides in the top-k all-gather and is read once, after the merge is

@@ -54,8 +54,8 @@ class OracleShard(parallel.ShardedSelector):
                 parts[c] = torch.from_numpy(acc)
         return u, parts
 
-    def exchange_density(self, comm, u_local):
-        return comm.all_gather(u_local)
+    def exchange_density(self, comm, u_local, parts=None):
+        return comm.all_gather(u_local), (comm.all_gather(parts) if parts is not None else None)
 
     def index_tensor(self, unl):
         return torch.as_tensor(np.asarray(unl), dtype=torch.int64)
