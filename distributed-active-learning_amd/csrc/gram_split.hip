@@ -712,8 +712,9 @@ struct Sym2Cfg {
   static constexpr int ROWB = KS * 4;                 // bytes per column row (H + L)
   static constexpr int SLOTS = ROWB / 16;
   static constexpr int HI = KS / 8;
-  static constexpr int SC = 128;                      // columns per stage
-  static constexpr int STAGE = SC * ROWB;             // 32 KiB (KS 64) or 16 KiB (KS 32)
+  static constexpr int STAGE = 32768;                 // bytes per LDS stage
+  static constexpr int SC = STAGE / ROWB;             // columns per stage: 128 (KS 64) or 256 (KS 32)
+  static constexpr int SPP = 256 / SC;                // stages per 512 x 256 pair: 2 or 1
   static constexpr int F4 = STAGE / 16;
   static constexpr int SWZ = (SLOTS < 16 ? SLOTS : 16) - 1;
   static constexpr int PIECES = STAGE / (4 * 1024);   // 1-KiB DMA pieces per wave per stage
@@ -723,7 +724,7 @@ struct Sym2Cfg {
   static constexpr int NCT = SC / MT;                 // column tiles per stage
   static constexpr int NV = 4;                        // accumulator values per lane
   static constexpr int SB = 512;                      // super block
-  static_assert(NKS >= 1 && PIECES >= 1, "bad slice");
+  static_assert(NKS >= 1 && PIECES >= 1 && (SPP == 1 || SPP == 2), "bad slice");
 };
 
 template <int KS>
@@ -951,6 +952,7 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
   issue(0, J, 0);
   load_a(P);
   int cb = 0;        // colacc buffer of the current pair
+  int buf = 0;       // LDS stage of the pair's first stage (alternates per pair when SPP == 1)
   int flushJ = -1;   // column block whose sums wait in colacc[cb ^ 1]
   int flushP = -1;   // row super block whose sums wait in rowacc
 
@@ -966,12 +968,17 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
     if (flushJ >= 0) flush_cols(cb ^ 1, flushJ);
     if (flushP >= 0) flush_rows(flushP);
     flushP = -1;
-    issue(1, J, 1);
-    compute(0, cmul, cb, 0, true);
-
-    block_sync();
-    if (has_next) issue(0, nJ, 0);
-    compute(1, cmul, cb, 128, false);
+    if constexpr (C::SPP == 2) {  // KS 64: two 128-column stages
+      issue(1, J, 1);
+      compute(0, cmul, cb, 0, true);
+      block_sync();
+      if (has_next) issue(0, nJ, 0);
+      compute(1, cmul, cb, 128, false);
+    } else {                      // KS 32: one 256-column stage, buffers alternate per pair
+      if (has_next) issue(buf ^ 1, nJ, 0);
+      compute(buf, cmul, cb, 0, true);
+      buf ^= 1;
+    }
     fold_rows();
 
     flushJ = diag ? -1 : J;
