@@ -1,0 +1,14 @@
+set -u
+R=$GRAFT_REPO_ROOT
+cd $R
+AB_LIBS=none AB_KNOBS=contig=DAL_GRAM_CONTIG:1,chunk=DAL_GRAM_CONTIG:0,nc10=DAL_GRAM_NC:10 AB_SHAPES=100000x64,200000x64,284807x30,500000x256 AB_ROUNDS=5 timeout -k 10 300 python -u scripts/gram_ablate.py > gpurun_out/ab47.log 2>&1; rc=$?
+echo "ab rc=$rc"; grep -v amdgpu.ids gpurun_out/ab47.log | cut -c1-200
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+DAL_GRAM_CONTIG=0 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu_chunk.log 2>&1; rc=$?
+echo "pytest chunk rc=$rc"; tail -3 gpurun_out/pytest_gpu_chunk.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u bench.py > gpurun_out/bench_default.log 2>&1; rc=$?
+echo "bench rc=$rc"; tail -1 gpurun_out/bench_default.log | cut -c1-1500
