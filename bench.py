@@ -240,12 +240,21 @@ def bench_diversity(args, cfg, world, rank, dev, dist, backend):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default: 50; config 4: 3)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default: 10; config 4: 1)")
     ap.add_argument("--config", default="2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--warm-steps", type=int, default=5)
+    ap.add_argument("--warm-steps", type=int, default=None)
     args = ap.parse_args()
+    # steady-state defaults: enough steps that allocator / stream set-up of the
+    # first steps is outside the timed region (a 100k-row step is ~1.5 ms)
+    big = args.config == "4"
+    if args.steps is None:
+        args.steps = 3 if big else 50
+    if args.warmup is None:
+        args.warmup = 1 if big else 10
+    if args.warm_steps is None:
+        args.warm_steps = 3 if big else 20
 
     import torch
     import torch.distributed as dist

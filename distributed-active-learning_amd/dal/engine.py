@@ -11,7 +11,6 @@ Reference loop body being replaced (one ``while True`` iteration):
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
 
 import numpy as np
 
@@ -45,7 +44,6 @@ def _require_cuda(device):
     return torch.device(device if device is not None else "cuda")
 
 
-@dataclass
 class Selection:
     """Result of one selection step (all tensors on the pool's device).
 
@@ -53,12 +51,38 @@ class Selection:
     indices         int64 [k]: selected global row indices, best first
     selected_scores fp64 [k]: their scores (canonical fp64 for density weighting)
     votes           int32 [U]: forest votes for class 1 of every unlabeled row
+
+    ``scores`` / ``votes`` may be given as (per-row tensor, positions): they are
+    gathered into unlabeled order on first access (the per-row arrays are
+    complete in HBM when the step returns; the gather is only a re-layout, so
+    a caller that reads just the selection pays no extra launches).
     """
 
-    scores: object
-    indices: object
-    selected_scores: object
-    votes: object = None
+    def __init__(self, scores, indices, selected_scores, votes=None):
+        self._scores = scores
+        self.indices = indices
+        self.selected_scores = selected_scores
+        self._votes = votes
+
+    @staticmethod
+    def _gathered(v):
+        if isinstance(v, tuple):
+            full, pos = v
+            return full if pos is None else full[pos]
+        return v
+
+    @property
+    def scores(self):
+        self._scores = self._gathered(self._scores)
+        return self._scores
+
+    @property
+    def votes(self):
+        self._votes = self._gathered(self._votes)
+        return self._votes
+
+    def __repr__(self):
+        return f"Selection(indices={self.indices!r}, selected_scores={self.selected_scores!r})"
 
     def as_pairs(self):
         """``add_to_labeled_set`` of the reference: a list of (index, score)."""
@@ -110,6 +134,7 @@ class PoolState:
         self._colsum = None
         self._density_exact = None
         self.gram_events = None  # list -> (start, end) HIP events around each Gram call
+        self.last_status = 0     # status word read by the last synchronising select
 
     def clear_caches(self):
         """Drop normalised rows, density and column sums (forces a cold step)."""
@@ -157,10 +182,12 @@ class PoolState:
                  _stream(self.device))
         return self._u, self._norm64
 
-    def gram_operand(self):
+    def gram_operand(self, with_partials: bool = True):
         """The density GEMM's operand for this shard's rows: the fp32 unit rows
         (gram "f32") or their two-term fp16 split [n_pad, 2*d_pad] (gram
-        "split", dal_split_f16).  All-gathered as is in the multi-GPU path."""
+        "split", dal_split_f16).  All-gathered as is in the multi-GPU path.
+        with_partials: the fused prep also writes the canonical column-sum
+        partials (else they are left to colsum_partials())."""
         if self.gram == "f32":
             u, _ = self.normalized()
             return u
@@ -178,7 +205,7 @@ class PoolState:
                 norm64 = torch.empty(self.n, dtype=torch.float64, device=self.device)
                 chunks = (self.n + DAL_CANON_CHUNK - 1) // DAL_CANON_CHUNK
                 parts = None
-                if self._colsum_partials is None:
+                if self._colsum_partials is None and with_partials:
                     parts = torch.empty((chunks, self.d), dtype=torch.float64, device=self.device)
                 call("dal_prep_split", _ptr(self.x), self.n, self.d, self.d, _ptr(self.flags),
                      self.n_pad, self.d_pad, _ptr(self._split), _ptr(norm64),
@@ -320,13 +347,15 @@ class PoolState:
 
     def local_positions(self, unl):
         """Rows of this shard for global indices ``unl`` (single GPU: all of them)."""
-        loc = unl - self.row_base
         if self.row_base == 0 and self.n == self.n_total:
-            return loc
+            return unl
+        loc = unl - self.row_base
         return loc[(loc >= 0) & (loc < self.n)]
 
-    def check_status(self):
-        st = int(self.status.item())
+    def check_status(self, st=None):
+        """Raise on the device status word (``st``: a value already read)."""
+        if st is None:
+            st = int(self.status.item())
         if st & DAL_FLAG_ZERO_NORM:
             raise ValueError("pool contains a zero-norm row: cosine similarity is undefined "
                              "(the reference would propagate NaN into every density)")
@@ -367,6 +396,18 @@ def as_pool_state(pool, excluded=None, device=None) -> PoolState:
 
 
 _LUT_CACHE = {}
+
+
+_SIDE_STREAMS = {}
+
+
+def _side_stream(device):
+    """One auxiliary HIP stream per device (created once)."""
+    torch = _torch()
+    key = str(device)
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = torch.cuda.Stream(device=device)
+    return _SIDE_STREAMS[key]
 
 
 def device_lut(strategy: str, n_trees: int, device):
@@ -467,6 +508,7 @@ def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k
             return out_idx, out_scores, out_keys
         # the step's one host sync: status word (zero-norm rows, candidate overflow)
         st = int(state.status.item())
+        state.last_status = st
         if cap >= n or not (st & DAL_FLAG_CAND_OVERFLOW):
             return out_idx, out_scores, out_keys
         state.status.bitwise_and_(~DAL_FLAG_CAND_OVERFLOW)
@@ -501,7 +543,7 @@ def uncertainty_step(state: PoolState, unlabeled_idx, forest: Forest, k: int,
     idx, _ = topk_keys(keys, kk, state.row_base)
     sel_scores = scores[idx - state.row_base]
     state.check_status()
-    return Selection(scores=scores[loc], indices=idx, selected_scores=sel_scores, votes=votes[loc])
+    return Selection(scores=(scores, loc), indices=idx, selected_scores=sel_scores, votes=(votes, loc))
 
 
 def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: float = 1.0,
@@ -521,7 +563,23 @@ def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: 
     if int(unl.shape[0]) == 0:
         raise ValueError("unlabeled set is empty (the reference loop breaks here)")
     # the density GEMM goes to the GPU first; the host prepares the rest while it runs
-    dens = state.density_fixed() if density_fixed is None else density_fixed
+    colsum_ready = None
+    if density_fixed is None and state._density is None and state._colsum is None and state.n:
+        # cold step: the canonical column sum (only the exact re-rank needs it)
+        # runs on a side stream AFTER the Gram, beside the vote / score chain
+        # (beside the Gram itself it would slow the persistent Gram blocks)
+        torch = _torch()
+        state.gram_operand(with_partials=False)
+        dens = state.density_fixed()
+        main = torch.cuda.current_stream(state.device)
+        side = _side_stream(state.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            cs = state.colsum()
+        cs.record_stream(main)
+        colsum_ready = side
+    else:
+        dens = state.density_fixed() if density_fixed is None else density_fixed
     flags, unl, n_cand = state.row_flags(unl)
     kk = min(int(k), n_cand)
     loc = state.local_positions(unl)
@@ -529,11 +587,12 @@ def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: 
     votes, scores, keys_lo, keys_hi = forest_score(
         state, forest, lut_dev, flags, DAL_DESCENDING, density=dens,
         density_err=density_error(state), beta=beta, want_hi=True)
-    out_scores, out_votes = scores[loc], votes[loc]  # queued before the selection's sync
+    if colsum_ready is not None:
+        _torch().cuda.current_stream(state.device).wait_stream(colsum_ready)
     idx, sel_scores, _ = dw_select_local(state, flags, votes, keys_lo, keys_hi, lut_dev, kk, beta,
                                          state.colsum())
-    state.check_status()  # already synchronised by dw_select_local
-    return Selection(scores=out_scores, indices=idx, selected_scores=sel_scores, votes=out_votes)
+    state.check_status(state.last_status)  # the word dw_select_local read (no second sync)
+    return Selection(scores=(scores, loc), indices=idx, selected_scores=sel_scores, votes=(votes, loc))
 
 
 def _density_step_separable(state: PoolState, unlabeled_idx, forest: Forest, k: int,
@@ -549,4 +608,4 @@ def _density_step_separable(state: PoolState, unlabeled_idx, forest: Forest, k: 
     idx, _ = topk_keys(keys, kk, state.row_base)
     sel_scores = scores[idx - state.row_base]
     state.check_status()
-    return Selection(scores=scores[loc], indices=idx, selected_scores=sel_scores, votes=votes[loc])
+    return Selection(scores=(scores, loc), indices=idx, selected_scores=sel_scores, votes=(votes, loc))

@@ -1,0 +1,44 @@
+"""Host-side cost of one cold config-2 density step: time from the step's
+start until the Gram launch has been queued (the GPU idles for most of it
+after the previous step's sync), and the wall time per step."""
+import os
+import sys
+import time
+
+REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(REPO, "distributed-active-learning_amd"))
+sys.path.insert(0, REPO)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from dal import engine  # noqa: E402
+from dal.forest import Forest  # noqa: E402
+
+dev = torch.device("cuda:0")
+n, d = 100000, 64
+x = bench.make_pool_rows(0, n, d, "uniform", dev)
+forest = Forest.synthetic(10, 4, d, seed=1, dist="uniform")
+unl = torch.arange(10, n, device=dev, dtype=torch.int64)
+state = engine.PoolState(x, excluded=np.arange(10), device=dev)
+orig = engine.PoolState.density_fixed
+marks = []
+
+
+def timed_density_fixed(self, *a, **k):
+    r = orig(self, *a, **k)
+    marks.append(time.perf_counter())
+    return r
+
+
+engine.PoolState.density_fixed = timed_density_fixed
+pre, wall = [], []
+for i in range(30):
+    t0 = time.perf_counter()
+    state.clear_caches()
+    r = engine.density_step(state, unl, forest, 100)
+    t1 = time.perf_counter()
+    if i >= 5:
+        pre.append((marks[-1] - t0) * 1e6)
+        wall.append((t1 - t0) * 1e6)
+print(f"host time to Gram launch: median {np.median(pre):.1f} us; step wall median {np.median(wall):.1f} us")

@@ -1,0 +1,53 @@
+"""One cold config-2 density step, repeated, for a kernel timeline under
+rocprofv3 --kernel-trace (analyse with scripts/step_timeline.py --analyse DIR).
+usage: rocprofv3 --kernel-trace -d gpurun_out/tl -o tl --output-format csv -- python scripts/step_timeline.py"""
+import glob
+import os
+import sys
+
+REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+
+
+def analyse(d):
+    import csv
+    f = sorted(glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True))[-1]
+    rows = list(csv.DictReader(open(f)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    # the last step: from the last Gram launch's predecessor normalize_split
+    starts = [i for i, r in enumerate(rows) if "normalize_split" in r["Kernel_Name"]]
+    i0 = starts[-1]
+    t0 = int(rows[i0]["Start_Timestamp"])
+    prev_end = t0
+    tot = 0
+    for r in rows[i0:]:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        name = r["Kernel_Name"].split("(")[0][-60:]
+        print(f"{(s - t0) / 1e3:9.1f} us  gap {(s - prev_end) / 1e3:7.1f}  dur {(e - s) / 1e3:8.1f}  {name}")
+        prev_end = e
+        tot = e - t0
+    print(f"step span {tot / 1e3:.1f} us")
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "--analyse":
+        analyse(sys.argv[2])
+        sys.exit(0)
+    sys.path.insert(0, os.path.join(REPO, "distributed-active-learning_amd"))
+    sys.path.insert(0, REPO)
+    import numpy as np
+    import torch
+    from dal import engine
+    from dal.forest import Forest
+    import bench
+
+    dev = torch.device("cuda:0")
+    n, d = 100000, 64
+    x = bench.make_pool_rows(0, n, d, "uniform", dev)
+    forest = Forest.synthetic(10, 4, d, seed=1, dist="uniform")
+    unl = torch.arange(10, n, device=dev, dtype=torch.int64)
+    state = engine.PoolState(x, excluded=np.arange(10), device=dev)
+    for _ in range(6):
+        state.clear_caches()
+        r = engine.density_step(state, unl, forest, 100)
+    torch.cuda.synchronize()
+    print("ok", r.indices[:5].tolist())
