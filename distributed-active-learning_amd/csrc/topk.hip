@@ -9,9 +9,9 @@
 // (score_key in common.hpp).
 //
 // Pipeline (all device-side, no host round trip):
-//   8 x radix_hist   exact k-th smallest key, 8-bit digits MSB first; every
+//   6 x radix_hist   exact k-th smallest key, 11-bit digits MSB first; every
 //                    block re-derives the running (prefix, remaining-k) state
-//                    from the previous pass's 256-bin histogram.
+//                    from the previous pass's 2048-bin histogram.
 //   count/scan/write ordered compaction: every key < K*, plus the first
 //                    (in row order) keys == K* -- stable, so ties go to the
 //                    lower index.
@@ -26,10 +26,25 @@ constexpr int kRadixThreads = 256;
 constexpr int kCompactRows = 1024;  // rows per compaction block (4 per thread)
 constexpr int kSortThreads = 1024;
 
+// Radix digits: 11 bits MSB first -> 6 passes over the 64-bit key (the last
+// pass covers the low 9 bits).  8-bit digits needed 8 dependent launches; each
+// pass costs about one launch on small pools, so fewer passes is the win.
+constexpr int kDigitBits = 11;
+constexpr int kPasses = (64 + kDigitBits - 1) / kDigitBits;  // 6
+constexpr int kBins = 1 << kDigitBits;                       // 2048
+constexpr int kBinsPerThread = kBins / kRadixThreads;        // 8
+
+__host__ __device__ constexpr int digit_shift(int p) {
+  return 64 - kDigitBits * (p + 1) > 0 ? 64 - kDigitBits * (p + 1) : 0;
+}
+__host__ __device__ constexpr int digit_bins(int p) {
+  return 1 << (64 - kDigitBits * p - digit_shift(p));
+}
+
 struct TopkHdr {
-  uint32_t hist[8][256];
-  unsigned long long prefix[9];
-  unsigned long long krem[9];
+  uint32_t hist[kPasses][kBins];
+  unsigned long long prefix[kPasses + 1];
+  unsigned long long krem[kPasses + 1];
   unsigned long long kstar, kfinal, total_lt, total_eq;
   unsigned int cand_count, overflow, pad0, pad1;
 };
@@ -61,26 +76,43 @@ TopkLayout topk_layout(int64_t n, int64_t cap) {
 }
 
 // ---------------------------------------------------------------- radix ----
-// Resolve the digit of pass p-1 from its histogram: the first bucket whose
-// inclusive count reaches the remaining k.  256 threads, one bucket each.
+// Resolve the digit of pass p from its histogram: the first bucket whose
+// inclusive count reaches the remaining k.  256 threads x 8 consecutive
+// buckets; a block scan of the per-thread totals locates the crossing.
 __device__ void resolve_digit(const TopkHdr* h, int p, unsigned long long& prefix,
                               unsigned long long& krem, uint32_t* sh) {
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const unsigned long long kr = h->krem[p];
-  uint32_t c = h->hist[p][tid];
-  sh[tid] = c;
-  __syncthreads();
-  for (int o = 1; o < 256; o <<= 1) {
-    const uint32_t y = tid >= o ? sh[tid - o] : 0;
-    __syncthreads();
-    sh[tid] += y;
-    __syncthreads();
+  const int nb = digit_bins(p);
+  uint32_t c[kBinsPerThread];
+  uint32_t tot = 0;
+#pragma unroll
+  for (int j = 0; j < kBinsPerThread; ++j) {
+    const int b = tid * kBinsPerThread + j;
+    c[j] = b < nb ? h->hist[p][b] : 0u;
+    tot += c[j];
+  }
+  uint32_t x = tot;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
   }
   __shared__ unsigned long long s_pre, s_krem;
-  const uint32_t incl = sh[tid], excl = incl - c;
-  if (incl >= kr && excl < kr) {
-    s_pre = h->prefix[p] | (static_cast<unsigned long long>(tid) << (56 - 8 * p));
-    s_krem = kr - excl;
+  if (lane == 63) sh[w] = x;
+  __syncthreads();
+  uint32_t excl = x - tot;
+  for (int i = 0; i < w; ++i) excl += sh[i];
+  if (excl < kr && excl + tot >= kr) {
+    uint32_t run = excl;
+#pragma unroll
+    for (int j = 0; j < kBinsPerThread; ++j) {
+      if (run < kr && run + c[j] >= kr) {
+        s_pre = h->prefix[p] |
+                (static_cast<unsigned long long>(tid * kBinsPerThread + j) << digit_shift(p));
+        s_krem = kr - run;
+      }
+      run += c[j];
+    }
   }
   __syncthreads();
   prefix = s_pre;
@@ -91,8 +123,8 @@ __device__ void resolve_digit(const TopkHdr* h, int p, unsigned long long& prefi
 __global__ __launch_bounds__(kRadixThreads) void radix_hist_kernel(const uint64_t* __restrict__ keys,
                                                                    int64_t n, int64_t k, int pass,
                                                                    TopkHdr* __restrict__ h) {
-  __shared__ uint32_t hist[256];
-  __shared__ uint32_t scan[256];
+  __shared__ uint32_t hist[kBins];
+  __shared__ uint32_t scan[kRadixThreads / 64];
   const int tid = threadIdx.x;
   unsigned long long prefix = 0, krem = static_cast<unsigned long long>(k);
   if (pass > 0) resolve_digit(h, pass - 1, prefix, krem, scan);
@@ -100,17 +132,24 @@ __global__ __launch_bounds__(kRadixThreads) void radix_hist_kernel(const uint64_
     h->prefix[pass] = prefix;
     h->krem[pass] = krem;
   }
-  hist[tid] = 0;
+#pragma unroll
+  for (int j = 0; j < kBinsPerThread; ++j) hist[j * kRadixThreads + tid] = 0;
   __syncthreads();
-  const int shift = 56 - 8 * pass;
-  const unsigned long long hmask = pass == 0 ? 0ull : (~0ull << (64 - 8 * pass));
+  const int shift = digit_shift(pass);
+  const unsigned long long dmask = static_cast<unsigned long long>(digit_bins(pass) - 1);
+  const unsigned long long hmask = pass == 0 ? 0ull : (~0ull << (64 - kDigitBits * pass));
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kRadixThreads;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kRadixThreads + tid; i < n; i += stride) {
     const unsigned long long key = keys[i];
-    if ((key & hmask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
+    if ((key & hmask) == prefix) atomicAdd(&hist[(key >> shift) & dmask], 1u);
   }
   __syncthreads();
-  if (hist[tid]) atomicAdd(&h->hist[pass][tid], hist[tid]);
+#pragma unroll
+  for (int j = 0; j < kBinsPerThread; ++j) {
+    const int b = j * kRadixThreads + tid;
+    const uint32_t v = hist[b];
+    if (v) atomicAdd(&h->hist[pass][b], v);
+  }
 }
 
 // ----------------------------------------------------------- compaction ---
@@ -141,7 +180,7 @@ __device__ __forceinline__ void predicate(const uint64_t* keys, const IntervalAr
 
 __device__ __forceinline__ void final_threshold(TopkHdr* h, unsigned long long& K,
                                                 unsigned long long& krem, uint32_t* scan) {
-  resolve_digit(h, 7, K, krem, scan);
+  resolve_digit(h, kPasses - 1, K, krem, scan);
 }
 
 template <bool INTERVAL>
@@ -568,7 +607,7 @@ int run_radix(const uint64_t* keys, int64_t n, int64_t k, TopkHdr* h, hipStream_
   int64_t blocks = ceil_div(n, kRadixThreads * 8);
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
-  for (int p = 0; p < 8; ++p) {
+  for (int p = 0; p < kPasses; ++p) {
     hipLaunchKernelGGL(radix_hist_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kRadixThreads), 0,
                        st, keys, n, k, p, h);
   }
@@ -683,19 +722,24 @@ extern "C" int dal_dw_select(const uint64_t* keys_lo, const uint64_t* keys_hi, c
                              const double* lut, double beta, const float* x, int64_t d, int64_t ldx,
                              const double* norm64, const double* colsum, int64_t cap, void* ws,
                              size_t ws_bytes, int64_t* out_idx, double* out_scores, uint64_t* out_keys,
-                             int32_t* dev_status, dal_stream_t stream) {
+                             int32_t* dev_status, dal_event_t colsum_ready, dal_stream_t stream) {
   if (!keys_lo || !keys_hi || !votes || !lut || !x || !norm64 || !colsum || !ws || !out_idx ||
       !out_scores || !dev_status)
     return DAL_ERR_ARG;
   if (d < 1 || ldx < d) return DAL_ERR_SHAPE;
   hipStream_t st = as_stream(stream);
+  bool wait_failed = false;
   auto rerank = [&](TopkHdr* h, uint64_t* ckey, int64_t* cidx, double* cpay, int64_t cp) {
+    // the only consumer of colsum: join its producer stream here, not before the call
+    if (colsum_ready && hipStreamWaitEvent(st, reinterpret_cast<hipEvent_t>(colsum_ready), 0) != hipSuccess)
+      wait_failed = true;
     hipLaunchKernelGGL(rerank_kernel, dim3(static_cast<unsigned>(ceil_div(cp, 256))), dim3(256), 0, st, h,
                        idx_base, x, static_cast<int>(d), ldx, norm64, colsum, lut, votes, row_flags, beta,
                        ckey, cidx, cpay, cp);
   };
-  return select_with_rerank(keys_lo, keys_hi, n, k, idx_base, cap, ws, ws_bytes, rerank, out_idx, out_scores,
-                            out_keys, dev_status, st);
+  const int rc = select_with_rerank(keys_lo, keys_hi, n, k, idx_base, cap, ws, ws_bytes, rerank, out_idx,
+                                    out_scores, out_keys, dev_status, st);
+  return rc ? rc : (wait_failed ? DAL_ERR_HIP : DAL_OK);
 }
 
 extern "C" size_t dal_maxcos_select_workspace_bytes(int64_t n, int64_t k, int64_t cap) {

@@ -484,9 +484,11 @@ def workspace(nbytes: int, device):
 
 
 def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k: int,
-                    beta: float, colsum, cap_scale: int = 1, sync: bool = True):
+                    beta: float, colsum, cap_scale: int = 1, sync: bool = True, colsum_ready=None):
     """dal_dw_select on this shard: exact canonical top-k of the shard.  The
     candidate capacity grows (and the step re-runs) on DAL_FLAG_CAND_OVERFLOW.
+    colsum_ready: a torch.cuda.Event recorded after ``colsum`` on another
+    stream; the library joins it just before the re-rank (its only reader).
     sync=False: no status read here -- the caller checks state.status later
     and re-runs with a larger cap_scale on overflow (multi-GPU path)."""
     torch = _torch()
@@ -503,7 +505,8 @@ def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k
         call("dal_dw_select", _ptr(keys_lo), _ptr(keys_hi), _ptr(votes), _ptr(flags), n, k,
              state.row_base, _ptr(lut_dev), float(beta), _ptr(state.x), state.d, state.d,
              _ptr(norm64), _ptr(colsum), cap, wsp, wsb, _ptr(out_idx), _ptr(out_scores),
-             _ptr(out_keys), _ptr(state.status), _stream(state.device))
+             _ptr(out_keys), _ptr(state.status),
+             0 if colsum_ready is None else colsum_ready.cuda_event, _stream(state.device))
         if not sync:
             return out_idx, out_scores, out_keys
         # the step's one host sync: status word (zero-norm rows, candidate overflow)
@@ -576,8 +579,9 @@ def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: 
         side.wait_stream(main)
         with torch.cuda.stream(side):
             cs = state.colsum()
+            colsum_ready = torch.cuda.Event()
+            colsum_ready.record(side)
         cs.record_stream(main)
-        colsum_ready = side
     else:
         dens = state.density_fixed() if density_fixed is None else density_fixed
     flags, unl, n_cand = state.row_flags(unl)
@@ -587,10 +591,9 @@ def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: 
     votes, scores, keys_lo, keys_hi = forest_score(
         state, forest, lut_dev, flags, DAL_DESCENDING, density=dens,
         density_err=density_error(state), beta=beta, want_hi=True)
-    if colsum_ready is not None:
-        _torch().cuda.current_stream(state.device).wait_stream(colsum_ready)
+    # the main stream joins the column sum inside the call, just before the re-rank
     idx, sel_scores, _ = dw_select_local(state, flags, votes, keys_lo, keys_hi, lut_dev, kk, beta,
-                                         state.colsum())
+                                         state.colsum(), colsum_ready=colsum_ready)
     state.check_status(state.last_status)  # the word dw_select_local read (no second sync)
     return Selection(scores=(scores, loc), indices=idx, selected_scores=sel_scores, votes=(votes, loc))
 

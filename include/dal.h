@@ -40,6 +40,7 @@ extern "C" {
 #endif
 
 typedef void* dal_stream_t; /* hipStream_t */
+typedef void* dal_event_t;  /* hipEvent_t */
 
 enum dal_status {
   DAL_OK = 0,
@@ -232,14 +233,18 @@ int dal_topk(const uint64_t* keys, int64_t n, int64_t k, int64_t idx_base, void*
  * no FMA) is recomputed and an exact top-k over the candidates returns the k
  * best by (score desc, NaN last, index asc): bit-exact with the fp64 oracle.
  * out_scores are canonical fp64 scores, out_keys (nullable) their keys.  More
- * than ``cap`` candidates sets DAL_FLAG_CAND_OVERFLOW (retry with a larger cap). */
+ * than ``cap`` candidates sets DAL_FLAG_CAND_OVERFLOW (retry with a larger cap).
+ * colsum_ready (nullable): an event recorded after ``colsum`` was written on
+ * another stream; the call makes ``stream`` wait for it just before the
+ * re-rank (the radix select and compaction run without it), so a cold step's
+ * canonical column sum overlaps the candidate search. */
 size_t dal_dw_select_workspace_bytes(int64_t n, int64_t k, int64_t cap);
 int dal_dw_select(const uint64_t* keys_lo, const uint64_t* keys_hi, const int32_t* votes,
                   const uint8_t* row_flags, int64_t n, int64_t k, int64_t idx_base,
                   const double* lut, double beta, const float* x, int64_t d, int64_t ldx,
                   const double* norm64, const double* colsum, int64_t cap, void* ws,
                   size_t ws_bytes, int64_t* out_idx, double* out_scores, uint64_t* out_keys,
-                  int32_t* dev_status, dal_stream_t stream);
+                  int32_t* dev_status, dal_event_t colsum_ready, dal_stream_t stream);
 
 /* ---- (a12, config 5) max-cosine to a labeled set -----------------------
  * Restates similarity.py:26-43 (columnSimilarities of the normalised pool) as
