@@ -126,6 +126,18 @@ __global__ __launch_bounds__(kRadixThreads) void radix_hist_kernel(const uint64_
   __shared__ uint32_t hist[kBins];
   __shared__ uint32_t scan[kRadixThreads / 64];
   const int tid = threadIdx.x;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kRadixThreads;
+  const int64_t i0 = static_cast<int64_t>(blockIdx.x) * kRadixThreads + tid;
+  // the first kPre keys of the thread are loaded before the previous pass is
+  // resolved: the key fetch and the histogram read overlap (on small pools
+  // these are all the keys, and each pass is latency-bound)
+  constexpr int kPre = 8;
+  unsigned long long pre[kPre];
+#pragma unroll
+  for (int j = 0; j < kPre; ++j) {
+    const int64_t i = i0 + j * stride;
+    pre[j] = i < n ? keys[i] : 0ull;
+  }
   unsigned long long prefix = 0, krem = static_cast<unsigned long long>(k);
   if (pass > 0) resolve_digit(h, pass - 1, prefix, krem, scan);
   if (blockIdx.x == 0 && tid == 0) {
@@ -138,8 +150,12 @@ __global__ __launch_bounds__(kRadixThreads) void radix_hist_kernel(const uint64_
   const int shift = digit_shift(pass);
   const unsigned long long dmask = static_cast<unsigned long long>(digit_bins(pass) - 1);
   const unsigned long long hmask = pass == 0 ? 0ull : (~0ull << (64 - kDigitBits * pass));
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kRadixThreads;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kRadixThreads + tid; i < n; i += stride) {
+#pragma unroll
+  for (int j = 0; j < kPre; ++j) {
+    const unsigned long long key = pre[j];
+    if (i0 + j * stride < n && (key & hmask) == prefix) atomicAdd(&hist[(key >> shift) & dmask], 1u);
+  }
+  for (int64_t i = i0 + kPre * stride; i < n; i += stride) {
     const unsigned long long key = keys[i];
     if ((key & hmask) == prefix) atomicAdd(&hist[(key >> shift) & dmask], 1u);
   }
