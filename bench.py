@@ -30,6 +30,7 @@ sys.path.insert(0, REPO)
 
 METRIC = "pool rows scored/sec (density-weighted uncertainty), 1–8 GPU; % MFMA/HBM peak"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s measured float4 copy)
 
 CONFIGS = {
     "2": dict(workload="config2: density_weighting.py cosine information density (beta=1), "
@@ -146,6 +147,30 @@ def gram_roofline(gram, achieved, traffic, gram_ms, gram_ms_max, flops):
             "executed_fp16_tflops": 3.0 * achieved, "vs_fp32_mfma_peak": achieved / FP32_MFMA_PEAK_TFLOPS,
             "traffic": traffic, "launch_ms": gram_ms, "launch_ms_max_over_ranks": gram_ms_max,
             "algorithmic_flops_per_launch": flops}
+
+
+def forest_roofline(n_rows, d, trees, forest_ms, config, world):
+    """K2 (dal_forest_score, density mode): HBM-bound.  Algorithmic bytes per
+    launch = every row's features once (n*d*4) + row flag (1) + fixed-point
+    density in (8) + votes (4) + fp64 score (8) + the two interval keys (16)."""
+    if not forest_ms:
+        return None
+    per_row = d * 4 + 1 + 8 + 4 + 8 + 16
+    nbytes = float(n_rows) * per_row
+    gbs = nbytes / (forest_ms * 1e-3) / 1e9
+    traffic = None
+    tpath = os.path.join(REPO, "profiles", "hbm_traffic.json")
+    if os.path.exists(tpath) and world == 1:
+        try:
+            traffic = (json.load(open(tpath)).get(f"config{config}") or {}).get("forest_score_bytes_per_launch")
+        except Exception:
+            traffic = None
+    return {"bound": "hbm", "kernel": f"dal_forest_score (T={trees} depth-4 trees, LDS-resident SoA; "
+                                      "votes -> LUT -> density-weighted interval keys)",
+            "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+            "traffic": traffic, "launch_ms": forest_ms, "algorithmic_bytes_per_launch": nbytes,
+            "bytes_per_row": per_row, "note": "timed with HIP events on the launch stream over the warm "
+                                              "steps (density cached, nothing concurrent)"}
 
 
 def bench_diversity(args, cfg, world, rank, dev, dist, backend):
@@ -334,7 +359,7 @@ def main():
     elapsed, gram_ms_max = float(t[0]), float(t[1])
 
     # warm path: density cached (the reference's density is constant per pool)
-    warm_ms = None
+    warm_ms = forest_ms = None
     if args.warm_steps > 0:
         if world > 1:
             parallel.select(sel, comm, unl, forest, k, mode="dw")
@@ -342,6 +367,7 @@ def main():
             engine.density_step(state, unl, forest, k)
         torch.cuda.synchronize()
         barrier()
+        state.forest_events = []
         tw = time.perf_counter()
         for _ in range(args.warm_steps):
             if world > 1:
@@ -354,6 +380,10 @@ def main():
         if world > 1:
             dist.all_reduce(tw, op=dist.ReduceOp.MAX)
         warm_ms = float(tw[0]) * 1000 / args.warm_steps
+        fev = state.forest_events
+        state.forest_events = None
+        if fev:
+            forest_ms = sum(a.elapsed_time(b) for a, b in fev) / len(fev)
 
     # separable density mode (exact O(N*D) identity): cold step, reported beside
     sep_ms = None
@@ -418,6 +448,7 @@ def main():
                                "(canonical fp64, same selection); HBM-bound, not the MFMA path"}
                       if sep_ms else None),
         "roofline": gram_roofline(state.gram, achieved, traffic, gram_ms, gram_ms_max, flops),
+        "roofline_forest": forest_roofline(state.n, d, cfg["trees"], forest_ms, args.config, world),
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

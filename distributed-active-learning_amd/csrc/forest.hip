@@ -66,7 +66,7 @@ __device__ __forceinline__ double density_pow_err(double d, double derr, double 
 
 template <bool X_LDS, bool F_LDS>
 __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs A, int R, int tpr,
-                                                                      int x_floats) {
+                                                                      int x_floats, bool vec4) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* xs = reinterpret_cast<float*>(smem);
   const int n_inner = (1 << A.depth) - 1;
@@ -85,10 +85,41 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
   const int xstride = A.d + 1;
   const int64_t row0 = static_cast<int64_t>(blockIdx.x) * R;
   if (X_LDS) {
-    const int64_t rows_here = min(static_cast<int64_t>(R), A.n - row0);
-    for (int e = tid; e < rows_here * A.d; e += kForestThreads) {
-      const int r = e / A.d, c = e - r * A.d;
-      xs[r * xstride + c] = A.x[(row0 + r) * A.ldx + c];
+    const int rows_here = static_cast<int>(min(static_cast<int64_t>(R), A.n - row0));
+    if (vec4) {
+      // 16-B loads, kStageBatch per thread issued before any LDS write (the
+      // block's whole tile in flight: this kernel is an HBM stream)
+      constexpr int kStageBatch = 8;
+      const int q = A.d >> 2, total = rows_here * q;
+      for (int e0 = 0; e0 < total; e0 += kForestThreads * kStageBatch) {
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        v4f v[kStageBatch];
+#pragma unroll
+        for (int j = 0; j < kStageBatch; ++j) {
+          const int e = e0 + j * kForestThreads + tid;
+          if (e < total) {
+            const int r = e / q, c = e - r * q;
+            v[j] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(A.x + (row0 + r) * A.ldx) + c);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < kStageBatch; ++j) {
+          const int e = e0 + j * kForestThreads + tid;
+          if (e < total) {
+            const int r = e / q, c = e - r * q;
+            float* dst = xs + r * xstride + 4 * c;
+            dst[0] = v[j].x;
+            dst[1] = v[j].y;
+            dst[2] = v[j].z;
+            dst[3] = v[j].w;
+          }
+        }
+      }
+    } else {
+      for (int e = tid; e < rows_here * A.d; e += kForestThreads) {
+        const int r = e / A.d, c = e - r * A.d;
+        xs[r * xstride + c] = A.x[(row0 + r) * A.ldx + c];
+      }
     }
   }
   __syncthreads();
@@ -189,6 +220,7 @@ extern "C" int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ld
   size_t smem = static_cast<size_t>(xf) * 4 + (f_lds ? static_cast<size_t>(f_bytes) : 0);
   if (smem == 0) smem = 16;
   const dim3 grid(static_cast<unsigned>(ceil_div(n, R)));
+  const bool vec4 = (d % 4 == 0) && (ldx % 4 == 0) && (reinterpret_cast<uintptr_t>(x) % 16 == 0);
   hipStream_t st = as_stream(stream);
 #define DAL_FOREST_LAUNCH(XL, FL)                                                                   \
   do {                                                                                              \
@@ -197,7 +229,7 @@ extern "C" int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ld
         hipSuccess)                                                                                 \
       return DAL_ERR_HIP;                                                                           \
     hipLaunchKernelGGL((forest_score_kernel<XL, FL>), grid, dim3(kForestThreads), smem, st, A, R,  \
-                       tpr, xf);                                                                    \
+                       tpr, xf, vec4);                                                              \
   } while (0)
   if (x_lds && f_lds) DAL_FOREST_LAUNCH(true, true);
   else if (x_lds) DAL_FOREST_LAUNCH(true, false);

@@ -134,6 +134,7 @@ class PoolState:
         self._colsum = None
         self._density_exact = None
         self.gram_events = None  # list -> (start, end) HIP events around each Gram call
+        self.forest_events = None  # list -> (start, end) HIP events around each forest-score call
         self.last_status = 0     # status word read by the last synchronising select
 
     def clear_caches(self):
@@ -436,10 +437,17 @@ def forest_score(state: PoolState, forest: Forest, lut_dev, flags, order: int, d
         kind = density_kind
     else:
         kind = DAL_DENSITY_EXACT if density.dtype == torch.float64 else DAL_DENSITY_FIXED
+    ev = None
+    if state.forest_events is not None:  # bench: K2 launch timing on the launch stream
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
     call("dal_forest_score", _ptr(state.x), n, state.d, state.d, _ptr(inner), _ptr(leaf),
          forest.n_trees, forest.depth, _ptr(lut_dev), 0 if density is None else _ptr(density), kind,
          float(density_err), _ptr(flags), float(beta), int(order), _ptr(votes), _ptr(scores),
          _ptr(keys), 0 if keys_hi is None else _ptr(keys_hi), _stream(state.device))
+    if ev is not None:
+        ev[1].record()
+        state.forest_events.append(ev)
     return votes, scores, keys, keys_hi
 
 
