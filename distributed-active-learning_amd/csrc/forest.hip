@@ -21,6 +21,8 @@
 // flight (ILP over trees).  Votes are integers; the score comes from an fp64
 // look-up table indexed by v, so US scores are exact fp64 and identical to the
 // reference's Python float arithmetic.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace dal {
@@ -210,6 +212,13 @@ extern "C" int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ld
   if (static_cast<int64_t>(R) * (d + 1) * 4 > 65536) {
     x_lds = false;
     R = 256;
+  }
+  // many trees (config 3: T = 100): spread a row's trees over more lanes --
+  // the traversal's dependent LDS round trips, not HBM, bound that case
+  int tpr_min = n_trees >= 64 ? 2 : 1;  // config 3: 60.7 -> 51.8 us (4: 53.5, 8: 60.9)
+  if (const char* e = getenv("DAL_FOREST_TPR")) tpr_min = atoi(e);  // timing knob (A/B runs)
+  if (x_lds) {
+    while (R > 1 && kForestThreads / R < tpr_min) R >>= 1;
   }
   const int tpr = kForestThreads / R;
   const int x_floats = x_lds ? R * static_cast<int>(d + 1) : 0;
