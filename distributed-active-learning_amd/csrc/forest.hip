@@ -205,10 +205,16 @@ extern "C" int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ld
   ForestArgs A{x, n, static_cast<int>(d), ldx, reinterpret_cast<const int2*>(inner), leaf, n_trees,
                depth, lut, density_kind ? density : nullptr, density_kind, density_err, row_flags, beta,
                order, votes, scores, keys, keys_hi};
-  // rows per block: stage up to 64 KiB of pool rows in LDS
+  // rows per block: stage up to ~16 KiB of pool rows in LDS.  Small tiles keep
+  // more blocks (and their loads) resident per CU: at 2M x 256 a 16 KiB tile
+  // runs 0.52 ms vs 0.60 (32 KiB) / 0.85 (96 KiB) / 0.75 (8 KiB); neutral at
+  // 100k x 64 and 284,807 x 30 (scripts/gpu_job63.sh, gpu_job64.sh)
   int R = 256;
   bool x_lds = true;
-  while (R > 16 && static_cast<int64_t>(R) * (d + 1) * 4 > 65536) R >>= 1;
+  int64_t tile_cap = 16640;
+  if (const char* e = getenv("DAL_FOREST_TILE_BYTES")) tile_cap = atoll(e);  // timing knob (A/B runs)
+  while (R > 16 && static_cast<int64_t>(R) * (d + 1) * 4 > tile_cap) R >>= 1;
+  // wide rows: 16 rows may exceed the preferred tile; LDS staging up to 64 KiB
   if (static_cast<int64_t>(R) * (d + 1) * 4 > 65536) {
     x_lds = false;
     R = 256;
