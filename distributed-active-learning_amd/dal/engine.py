@@ -135,6 +135,7 @@ class PoolState:
         self._density_exact = None
         self.gram_events = None  # list -> (start, end) HIP events around each Gram call
         self.forest_events = None  # list -> (start, end) HIP events around each forest-score call
+        self.cap_scale = 1  # re-rank candidate capacity multiplier, kept after an overflow
         self.last_status = 0     # status word read by the last synchronising select
 
     def clear_caches(self):
@@ -503,6 +504,8 @@ def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k
     lib = _lib.load()
     n = state.n
     norm64 = state.norms()
+    if sync:  # single-GPU: start from the capacity a previous overflow grew to
+        cap_scale = max(cap_scale, state.cap_scale)
     cap = int(min(n, candidate_cap(n, k) * cap_scale))
     while True:
         wsb = int(lib.dal_dw_select_workspace_bytes(n, k, cap))
@@ -524,6 +527,7 @@ def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k
             return out_idx, out_scores, out_keys
         state.status.bitwise_and_(~DAL_FLAG_CAND_OVERFLOW)
         cap = min(n, cap * 4)
+        state.cap_scale *= 4  # later steps (same pool, same score spread) start here
 
 
 def sort_pairs(keys, idx, k: int, payload=None):
