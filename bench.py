@@ -3,13 +3,19 @@ query selection (BASELINE.json metric), 1..N GPUs of one node.
 
 One step = one cold query-selection iteration of density_weighting.py
 (:58-100 proximity/density, :133-172 votes, entropy x density, top-k) over a
-synthetic pool already resident in HBM: row L2-normalise -> fused fp32-MFMA
-Gram row-sum (density) -> forest votes + score -> exact top-k with fp64
-re-rank.  Nothing is cached across timed steps.  With N > 1 the pool is
-row-sharded (strong scaling: the same pool on every N) and the two exchanges
-run over RCCL.
+pool already resident in HBM: row L2-normalise -> fused symmetric MFMA Gram
+row-sum (density) -> forest votes + score -> exact top-k with fp64 re-rank.
+Nothing is cached across timed steps.  With N > 1 the pool is row-sharded
+(strong scaling: the same pool on every N) and the two exchanges run over RCCL.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4]
+Default workload (N = 1 and N > 1): BASELINE config 4, the north-star pool
+(2,000,000 x 256 U[0,1) fp32 from numpy default_rng(0), the BASELINE.md pool),
+T = 10, k = 100, E = {0..9}.  Config 2 (100k x 64) runs beside it as the
+``extra.config2`` key.  After timing, the bench checks its own work: the last
+timed step's selection must equal (indices and fp64 scores, bit for bit) the
+selection of the exact separable density path on the same pool.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Prints ONE JSON line on rank 0.
@@ -21,6 +27,7 @@ import json
 import os
 import sys
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -31,46 +38,75 @@ sys.path.insert(0, REPO)
 METRIC = "pool rows scored/sec (density-weighted uncertainty), 1–8 GPU; % MFMA/HBM peak"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s measured float4 copy)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
+F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 MFMA (same cycles as bf16)
 
 CONFIGS = {
     "2": dict(workload="config2: density_weighting.py cosine information density (beta=1), "
-                       "synthetic U[0,1) 100,000 x 64 fp32 pool, T=10 depth-4 forest, k=100, E=L0={0..9}",
+                       "U[0,1) 100,000 x 64 fp32 pool (default_rng(0)), T=10 depth-4 forest, k=100, "
+                       "E=L0={0..9}",
               n=100_000, d=64, trees=10, depth=4, k=100, dist="uniform"),
-    "3": dict(workload="config3: credit-card shape 284,807 x 30 N(0,1) fp32, RF T=100 depth 4, "
-                       "entropy x density, k=100, E={0..9}",
+    "3": dict(workload="config3: credit-card shape 284,807 x 30 N(0,1) fp32 (default_rng(0)), RF T=100 "
+                       "depth 4, entropy x density, k=100, E={0..9}",
               n=284_807, d=30, trees=100, depth=4, k=100, dist="normal"),
-    "4": dict(workload="config4: synthetic U[0,1) 2,000,000 x 256 fp32 pool, T=10 depth-4 forest, "
+    "4": dict(workload="config4: U[0,1) 2,000,000 x 256 fp32 pool (default_rng(0)), T=10 depth-4 forest, "
                        "entropy x density, k=100, E={0..9}",
               n=2_000_000, d=256, trees=10, depth=4, k=100, dist="uniform"),
     "5": dict(workload="config5: batch-mode diversity selection (similarity.py max-cosine to the labeled "
-                       "set), U[0,1)->bf16 8,000,000 x 128 pool, L = first 1,024 rows, k=1000, fp32 accumulate",
+                       "set), U[0,1)->bf16 8,000,000 x 128 pool (default_rng(0)), L = first 1,024 rows, "
+                       "k=1000, fp32 accumulate",
               n=8_000_000, d=128, k=1000, m=1024, dist="uniform", mode="div"),
 }
 N_EXCLUDED = 10
-GEN_CHUNK = 65536
+POOL_SEED = 0
+DATA_NOTE = ("synthetic: numpy default_rng(0) pool of the BASELINE.md shape (rows of a shard generated "
+             "by PCG64 advance, identical for every GPU count); forest synthetic (default_rng(1))")
+# K3 (dal_dw_select level 1) algorithmic bytes per row: the radix select reads
+# the pessimistic key once per pass; the ordered compaction reads both
+# interval keys twice (count, write).
+TOPK_RADIX_PASSES = 6
 
 
-def make_pool_rows(lo: int, hi: int, d: int, dist: str, device):
-    """Rows [lo, hi) of the synthetic pool, generated on the GPU in fixed
-    65,536-row chunks (seed = chunk id) so every rank/GPU count sees the same pool."""
+# ------------------------------------------------------------------ pool --
+def host_pool(lo: int, hi: int, d: int, dist: str, seed: int = POOL_SEED) -> np.ndarray:
+    """Rows [lo, hi) of ``default_rng(seed).random((N, d), float32)`` (or
+    ``standard_normal``).  Uniform rows are generated in parallel chunks, each
+    from a PCG64 advanced to the chunk's first value (one 64-bit draw per two
+    float32 values; chunk starts are even), so any shard is generated alone and
+    equals the same rows of the full pool."""
+    if dist == "normal":  # rejection sampling: not advanceable -> full pool, sliced
+        return np.random.default_rng(seed).standard_normal((hi, d), dtype=np.float32)[lo:hi].copy()
+    out = np.empty((hi - lo, d), dtype=np.float32)
+    chunk = 65536
+
+    def fill(r0):
+        r1 = min(r0 + chunk, hi)
+        g = np.random.default_rng(seed)
+        g.bit_generator.advance(r0 * d // 2)
+        out[r0 - lo:r1 - lo] = g.random((r1 - r0, d), dtype=np.float32)
+
+    starts = list(range(lo, hi, chunk))
+    if starts and (lo * d) % 2:
+        raise ValueError("shard start must be an even value offset")
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        list(ex.map(fill, starts))
+    return out
+
+
+def upload(x: np.ndarray, dev):
     import torch
 
-    out = torch.empty((hi - lo, d), dtype=torch.float32, device=device)
-    c0 = lo // GEN_CHUNK
-    c1 = (hi + GEN_CHUNK - 1) // GEN_CHUNK
-    for c in range(c0, c1):
-        g = torch.Generator(device=device)
-        g.manual_seed(1_000_003 * 7 + c)
-        r0, r1 = c * GEN_CHUNK, (c + 1) * GEN_CHUNK
-        if dist == "uniform":
-            blk = torch.rand((GEN_CHUNK, d), generator=g, device=device, dtype=torch.float32)
-            blk.clamp_(min=1e-7)  # keep every row's norm > 0
-        else:
-            blk = torch.randn((GEN_CHUNK, d), generator=g, device=device, dtype=torch.float32)
-        a, b = max(lo, r0), min(hi, r1)
-        if a < b:
-            out[a - lo:b - lo] = blk[a - r0:b - r0]
-    return out
+    return torch.from_numpy(x).to(dev)
+
+
+# ------------------------------------------------------------ baselines --
+def _cores():
+    try:
+        from threadpoolctl import threadpool_info
+
+        return max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        return len(os.sched_getaffinity(0))
 
 
 def cpu_baseline(x_host: np.ndarray, cfg, of, budget_s: float = 12.0):
@@ -80,12 +116,6 @@ def cpu_baseline(x_host: np.ndarray, cfg, of, budget_s: float = 12.0):
     score and the descending sort; rows/s = sample rows / elapsed."""
     from oracle import dal_oracle as O
 
-    try:
-        from threadpoolctl import threadpool_info
-
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:  # pragma: no cover
-        threads = len(os.sched_getaffinity(0))
     n = x_host.shape[0]
     keep = np.ones(n, dtype=bool)
     keep[:N_EXCLUDED] = False
@@ -108,16 +138,40 @@ def cpu_baseline(x_host: np.ndarray, cfg, of, budget_s: float = 12.0):
     dt = run(rows)
     rows = int(min(n - N_EXCLUDED, max(64, rows * budget_s / max(dt, 1e-3))))
     dt = run(rows)
-    return {"value": rows / dt, "unit": "rows/s", "cores": int(threads), "kind": "port",
+    full = rows >= n - N_EXCLUDED
+    return {"value": rows / dt, "unit": "rows/s", "cores": int(_cores()), "kind": "port",
             "sample": f"{rows} pool rows scored against all {n - N_EXCLUDED} non-excluded columns "
                       f"(fp64 BLAS Gram row-sum + {cfg['trees']}-tree votes + entropy score + sort), "
-                      f"{dt:.1f} s on the host"}
+                      f"{dt:.1f} s on the host" + ("" if full else "; rows/s of the sample (the O(N^2) "
+                                                    "per-row cost is the same for every row)")}
 
 
-BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
-F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 MFMA (same cycles as bf16)
+def cpu_baseline_div(x_host_bf16_as_f32: np.ndarray, m: int, k: int, n_total: int, budget_s: float = 12.0):
+    """Config 5 on the host: fp64 max-cosine of a row slice to the labeled set
+    (BLAS) + the k smallest; rows/s of the slice (the per-row cost is constant,
+    so the full 8M-row job time is the slice rate extrapolated linearly)."""
+    from oracle import dal_oracle as O
+
+    lab = O.l2_normalize(x_host_bf16_as_f32[:m])
+
+    def run(rows):
+        t0 = time.perf_counter()
+        U = O.l2_normalize(x_host_bf16_as_f32[m:m + rows])
+        mx = (U @ lab.T).max(axis=1)
+        O.select_topk(mx, np.arange(m, m + rows), k, ascending=True)
+        return time.perf_counter() - t0
+
+    rows = 4096
+    dt = run(rows)
+    rows = int(min(x_host_bf16_as_f32.shape[0] - m, max(4096, rows * budget_s / max(dt, 1e-3))))
+    dt = run(rows)
+    return {"value": rows / dt, "unit": "rows/s", "cores": int(_cores()), "kind": "port",
+            "sample": f"{rows}-row slice (of {n_total - m}) scored against the {m} labeled "
+                      f"rows (fp64 BLAS max-cosine + top-{k}), {dt:.1f} s on the host; linear "
+                      f"extrapolation to the full pool = {(n_total - m) / (rows / dt):.0f} s"}
 
 
+# ------------------------------------------------------------ rooflines --
 def gram_roofline(gram, achieved, traffic, gram_ms, gram_ms_max, flops):
     """Roofline entry of the density GEMM.  achieved = ALGORITHMIC flops
     (2 per feature per (row, column) pair) / launch time.  The split kernel
@@ -149,44 +203,228 @@ def gram_roofline(gram, achieved, traffic, gram_ms, gram_ms_max, flops):
             "algorithmic_flops_per_launch": flops}
 
 
+def _traffic(config, key, world):
+    tpath = os.path.join(REPO, "profiles", "hbm_traffic.json")
+    if world != 1 or not os.path.exists(tpath):
+        return None
+    try:
+        return (json.load(open(tpath)).get(f"config{config}") or {}).get(key)
+    except Exception:
+        return None
+
+
 def forest_roofline(n_rows, d, trees, forest_ms, config, world):
-    """K2 (dal_forest_score, density mode): HBM-bound.  Algorithmic bytes per
-    launch = every row's features once (n*d*4) + row flag (1) + fixed-point
-    density in (8) + votes (4) + fp64 score (8) + the two interval keys (16)."""
+    """K2 (dal_forest_score, density mode).  Algorithmic bytes per launch =
+    every row's features once (n*d*4) + row flag (1) + fixed-point density in
+    (8) + votes (4) + fp64 score (8) + the two interval keys (16).  At T = 10
+    the kernel streams HBM; at T = 100 (config 3) the dependent LDS traversal
+    (4 levels x T trees per row) bounds it, so the HBM fraction is reported
+    with bound "lds-latency"."""
     if not forest_ms:
         return None
     per_row = d * 4 + 1 + 8 + 4 + 8 + 16
     nbytes = float(n_rows) * per_row
     gbs = nbytes / (forest_ms * 1e-3) / 1e9
-    traffic = None
-    tpath = os.path.join(REPO, "profiles", "hbm_traffic.json")
-    if os.path.exists(tpath) and world == 1:
-        try:
-            traffic = (json.load(open(tpath)).get(f"config{config}") or {}).get("forest_score_bytes_per_launch")
-        except Exception:
-            traffic = None
-    return {"bound": "hbm", "kernel": f"dal_forest_score (T={trees} depth-4 trees, LDS-resident SoA; "
-                                      "votes -> LUT -> density-weighted interval keys)",
+    return {"bound": "hbm" if trees <= 32 else "lds-latency",
+            "kernel": f"dal_forest_score (T={trees} depth-4 trees, LDS-resident SoA; "
+                      "votes -> LUT -> density-weighted interval keys)",
             "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
-            "traffic": traffic, "launch_ms": forest_ms, "algorithmic_bytes_per_launch": nbytes,
-            "bytes_per_row": per_row, "note": "timed with HIP events on the launch stream over the warm "
-                                              "steps (density cached, nothing concurrent)"}
+            "traffic": _traffic(config, "forest_score_bytes_per_launch", world), "launch_ms": forest_ms,
+            "algorithmic_bytes_per_launch": nbytes, "bytes_per_row": per_row,
+            "note": "timed with HIP events on the launch stream over the warm steps (density cached)"}
 
 
-def bench_diversity(args, cfg, world, rank, dev, dist, backend):
+def topk_roofline(n_rows, select_ms, config, world):
+    """K3 (dal_dw_select: radix select of the k-th pessimistic key, ordered
+    compaction of the interval candidates, exact fp64 re-rank, one-block
+    sort).  Algorithmic bytes per call = 8 B per row per radix pass + 2 x 16 B
+    per row (both interval keys, count and write passes); the re-rank and sort
+    touch O(candidates) bytes."""
+    if not select_ms:
+        return None
+    per_row = 8 * TOPK_RADIX_PASSES + 32
+    nbytes = float(n_rows) * per_row
+    gbs = nbytes / (select_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": "dal_dw_select (radix select + interval compaction + fp64 re-rank + sort)",
+            "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+            "traffic": _traffic(config, "dw_select_bytes_per_launch", world), "launch_ms": select_ms,
+            "algorithmic_bytes_per_launch": nbytes, "bytes_per_row": per_row,
+            "note": "one C-ABI call (several dependent launches), HIP events on the launch stream, warm steps"}
+
+
+# ----------------------------------------------------------- workloads --
+def _timed(fn, steps, barrier):
+    import torch
+
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(steps):
+        out = fn()
+    torch.cuda.synchronize()
+    barrier()
+    return time.perf_counter() - t0, out
+
+
+def _max_over_ranks(vals, world, dist, tdev):
+    import torch
+
+    t = torch.tensor(vals, dtype=torch.float64, device=tdev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t]
+
+
+def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, backend, cpu=True):
+    """Density-weighted selection on one config; returns the JSON dict."""
+    import torch
+
+    from dal import engine, parallel
+    from dal.forest import Forest
+
+    cfg = CONFIGS[config]
+    n, d, k = cfg["n"], cfg["d"], cfg["k"]
+    lo, hi, _ = parallel.shard_range(n, world, rank)
+    x_host = host_pool(lo, hi, d, cfg["dist"])  # this rank's rows (world 1: the whole pool)
+    x = upload(x_host, dev)
+    forest = Forest.synthetic(cfg["trees"], cfg["depth"], d, seed=1, dist=cfg["dist"])
+    excluded = np.arange(N_EXCLUDED)
+    unl = torch.arange(N_EXCLUDED, n, device=dev, dtype=torch.int64)
+    n_scored = n - N_EXCLUDED
+    tdev = dev if backend == "nccl" else "cpu"
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    if world > 1:
+        sel = parallel.ShardedSelector(x, n, rank, world, excluded=excluded, device=dev)
+        comm = parallel.TorchComm()
+        state = sel.state
+
+        def step(density_mode="gram", cold=True):
+            if cold:
+                sel.clear_caches()
+            return parallel.select(sel, comm, unl, forest, k, mode="dw", density_mode=density_mode)
+    else:
+        state = engine.PoolState(x, excluded=excluded, device=dev)
+
+        def step(density_mode="gram", cold=True):
+            if cold:
+                state.clear_caches()
+            r = engine.density_step(state, unl, forest, k, mode=density_mode)
+            return r.indices, r.selected_scores
+
+    for _ in range(warmup):
+        step()
+    state.gram_events = []
+    elapsed, (idx_g, sc_g) = _timed(step, steps, barrier)
+    events, state.gram_events = state.gram_events, None
+    # the Gram launches of one step (one, or own-shard + rest when N > 1), averaged over steps
+    gram_ms = sum(a.elapsed_time(b) for a, b in events) / max(steps, 1)
+    elapsed, gram_ms_max = _max_over_ranks([elapsed, gram_ms], world, dist, tdev)
+
+    # self-check (outside the timed region): the timed step's selection equals
+    # the exact separable-density selection, indices and fp64 score bits
+    idx_s, sc_s = step("separable")
+    same = bool(torch.equal(idx_g, idx_s)) and bool(torch.equal(sc_g.view(torch.int64), sc_s.view(torch.int64)))
+    if not same:
+        raise SystemExit(f"bench self-check FAILED: gram-mode selection != separable-mode selection "
+                         f"({idx_g[:8].tolist()} vs {idx_s[:8].tolist()})")
+
+    # warm path: density cached (the reference's density is constant per pool)
+    warm_ms = forest_ms = select_ms = None
+    if warm_steps > 0:
+        step()
+        state.forest_events, state.select_events = [], []
+        tw, _ = _timed(lambda: step(cold=False), warm_steps, barrier)
+        (tw,) = _max_over_ranks([tw], world, dist, tdev)
+        warm_ms = tw * 1000 / warm_steps
+        fev, sev = state.forest_events, state.select_events
+        state.forest_events = state.select_events = None
+        if fev:
+            forest_ms = sum(a.elapsed_time(b) for a, b in fev) / len(fev)
+        if sev:
+            select_ms = sum(a.elapsed_time(b) for a, b in sev) / len(sev)
+
+    # separable density mode (exact O(N*D) identity): cold step, reported beside
+    sep_ms = None
+    if warm_steps > 0:
+        step("separable")
+        ts, _ = _timed(lambda: step("separable"), warm_steps, barrier)
+        (ts,) = _max_over_ranks([ts], world, dist, tdev)
+        sep_ms = ts * 1000 / warm_steps
+
+    # roofline of the dominant kernel (density Gram row-sum), this rank's launch
+    rows_local = (hi - lo) - int(np.sum((excluded >= lo) & (excluded < hi)))
+    flops = 2.0 * rows_local * (n - N_EXCLUDED) * d
+    achieved = flops / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else 0.0
+    traffic = _traffic(config, {"sym": "gram_rowsum_sym_bytes_per_launch",
+                                "split": "gram_rowsum_split_bytes_per_launch"}.get(
+                                    state.gram, "gram_rowsum_bytes_per_launch"), world)
+    ms_per_step = elapsed * 1000 / steps
+    out = {
+        "metric": METRIC,
+        "value": n_scored * steps / elapsed,
+        "unit": "rows/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32" if state.gram == "f32" else "f32 (fp16-split MFMA, fp32 accumulate)",
+        "data": DATA_NOTE,
+        "config": {"workload": cfg["workload"], "pool_rows": n, "features": d, "trees": cfg["trees"],
+                   "depth": cfg["depth"], "k": k, "excluded": N_EXCLUDED, "rows_scored": n_scored,
+                   "parallelism": f"row-shard dp{world} (RCCL all-gather)" if world > 1 else "single GPU"},
+        "selection_latency_ms": ms_per_step,
+        "warm_selection_latency_ms": warm_ms,
+        "warm_rows_per_s": (n_scored / (warm_ms * 1e-3)) if warm_ms else None,
+        "self_check": {"gram_selection_equals_separable_selection": same, "k": k,
+                       "note": "last timed step vs the exact O(N*D) density path, indices + fp64 score bits"},
+        "separable": ({"cold_selection_latency_ms": sep_ms, "rows_per_s": n_scored / (sep_ms * 1e-3),
+                       "note": "density via the exact O(N*D) identity sum_j<u_i,u_j> = <u_i, sum_j u_j> "
+                               "(canonical fp64, same selection); HBM-bound, not the MFMA path"}
+                      if sep_ms else None),
+        "roofline": gram_roofline(state.gram, achieved, traffic, gram_ms, gram_ms_max, flops),
+        "roofline_forest": forest_roofline(state.n, d, cfg["trees"], forest_ms, config, world),
+        "roofline_topk": topk_roofline(state.n, select_ms, config, world),
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and cpu and not args.no_cpu_baseline:
+        from oracle import dal_oracle as O
+
+        of = O.synthetic_forest(cfg["trees"], cfg["depth"], d, seed=1, dist=cfg["dist"])
+        out["cpu_baseline"] = cpu_baseline(x_host, cfg, of)
+    del state, x
+    if world > 1:
+        del sel
+    torch.cuda.empty_cache()
+    return out
+
+
+def bench_div(args, steps, warmup, world, rank, dev, dist, backend):
     """Config 5: one step = max-cosine of every pool row to the labeled set
     (bf16 MFMA, fp32 accumulate) + exact top-k of the least similar rows."""
     import torch
 
-    from dal import parallel
-    from dal.similarity import diversity_select
+    from dal import _lib, parallel
+    from dal.engine import _ptr, _stream
+    from dal.similarity import LabeledSet, diversity_select
 
+    cfg = CONFIGS["5"]
     n, d, k, m = cfg["n"], cfg["d"], cfg["k"], cfg["m"]
     lo, hi, _ = parallel.shard_range(n, world, rank)
-    x = make_pool_rows(lo, hi, d, cfg["dist"], dev).to(torch.bfloat16)
-    lab = make_pool_rows(0, m, d, cfg["dist"], dev).to(torch.bfloat16)
+    x = upload(host_pool(lo, hi, d, cfg["dist"]), dev).to(torch.bfloat16)
+    lab_host = host_pool(0, m, d, cfg["dist"])
+    lab = upload(lab_host, dev).to(torch.bfloat16)
     cand = torch.arange(max(lo, m), hi, device=dev, dtype=torch.int64)
     comm = parallel.TorchComm() if world > 1 else None
+    tdev = dev if backend == "nccl" else "cpu"
 
     def step():
         if world > 1:
@@ -198,21 +436,10 @@ def bench_diversity(args, cfg, world, rank, dev, dist, backend):
         if world > 1:
             dist.barrier()
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
-    torch.cuda.synchronize()
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed, _ = _timed(step, steps, barrier)
     # kernel-only timing of the max-cosine launch on this rank
-    from dal import _lib
-    from dal.engine import _ptr, _stream
-    from dal.similarity import LabeledSet
-
     L = LabeledSet(lab, dev)
     st = torch.zeros(1, dtype=torch.int32, device=dev)
     out = torch.empty(hi - lo, dtype=torch.float32, device=dev)
@@ -221,65 +448,52 @@ def bench_diversity(args, cfg, world, rank, dev, dist, backend):
     for _ in range(3):
         e0.record()
         _lib.call("dal_max_cosine", _ptr(x), hi - lo, d, _ptr(L.rows), L.m_pad, _ptr(L.inv), 0,
-                  _ptr(out), _ptr(st), _stream(dev))
+                  _ptr(out), 0, _ptr(st), _stream(dev))
         e1.record()
         torch.cuda.synchronize()
         ms.append(e0.elapsed_time(e1))
     kms = sorted(ms)[1]
-    tdev = dev if backend == "nccl" else "cpu"
-    t = torch.tensor([elapsed, kms], dtype=torch.float64, device=tdev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t[0])
+    elapsed, _ = _max_over_ranks([elapsed, kms], world, dist, tdev)
     flops = 2.0 * (hi - lo) * m * d
     achieved = flops / (kms * 1e-3) / 1e12
-    traffic = None
-    tpath = os.path.join(REPO, "profiles", "hbm_traffic.json")
-    if os.path.exists(tpath) and world == 1:
-        try:
-            traffic = json.load(open(tpath)).get(f"config{args.config}", {}).get("maxcos_bytes_per_launch")
-        except Exception:
-            traffic = None
-    out_line = {
+    res = {
         "metric": "pool rows scored/sec (diversity: max-cosine to labeled set + exact top-k)",
-        "value": (n - m) * args.steps / elapsed, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": elapsed * 1000 / args.steps, "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
-        "data": "synthetic (GPU-generated, fixed seeds per 65,536-row chunk)",
+        "value": (n - m) * steps / elapsed, "unit": "rows/s", "n_gpus": world, "steps": steps,
+        "warmup": warmup, "ms_per_step": elapsed * 1000 / steps, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "bf16", "data": DATA_NOTE,
         "config": {"workload": cfg["workload"], "pool_rows": n, "features": d, "labeled": m, "k": k,
                    "parallelism": f"row-shard dp{world}" if world > 1 else "single GPU"},
         "roofline": {"bound": "mfma", "kernel": "dal_max_cosine (v_mfma_f32_32x32x16_bf16)",
                      "achieved": achieved, "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / BF16_MFMA_PEAK_TFLOPS, "traffic": traffic, "launch_ms": kms,
-                     "algorithmic_flops_per_launch": flops,
-                     "pool_bytes_per_launch": (hi - lo) * d * 2,
+                     "frac": achieved / BF16_MFMA_PEAK_TFLOPS,
+                     "traffic": _traffic("5", "maxcos_bytes_per_launch", world), "launch_ms": kms,
+                     "algorithmic_flops_per_launch": flops, "pool_bytes_per_launch": (hi - lo) * d * 2,
                      "hbm_frac_of_8TBs": (hi - lo) * d * 2 / (kms * 1e-3) / 8e12},
         "cpu_baseline": None,
     }
-    if rank == 0:
-        print(json.dumps(out_line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        xs = x[: 300_000].float().cpu().numpy()  # the bf16 values the GPU scores, as fp32
+        res["cpu_baseline"] = cpu_baseline_div(xs, m, k, n)
+    return res
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=None, help="timed steps (default: 50; config 4: 3)")
-    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default: 10; config 4: 1)")
-    ap.add_argument("--config", default="2", choices=sorted(CONFIGS))
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default: config 4: 5, else 50)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default: config 4: 1, else 10)")
+    ap.add_argument("--config", default="4", choices=sorted(CONFIGS))
+    ap.add_argument("--extra", default=None,
+                    help="comma list of extra configs reported under 'extra' (default: '2' with config 4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--warm-steps", type=int, default=None)
     args = ap.parse_args()
-    # steady-state defaults: enough steps that allocator / stream set-up of the
-    # first steps is outside the timed region (a 100k-row step is ~1.5 ms)
-    big = args.config == "4"
-    if args.steps is None:
-        args.steps = 3 if big else 50
-    if args.warmup is None:
-        args.warmup = 1 if big else 10
-    if args.warm_steps is None:
-        args.warm_steps = 3 if big else 20
+    big = args.config in ("4",)
+    steps = args.steps if args.steps is not None else (5 if big else 50)
+    warmup = args.warmup if args.warmup is not None else (1 if big else 10)
+    warm_steps = args.warm_steps if args.warm_steps is not None else (5 if big else 20)
+    extra = args.extra if args.extra is not None else ("2" if args.config == "4" else "")
+    extra = [c for c in extra.split(",") if c]
 
     import torch
     import torch.distributed as dist
@@ -301,161 +515,20 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    from dal import engine, parallel
-    from dal.forest import Forest
-
-    cfg = CONFIGS[args.config]
-    if cfg.get("mode") == "div":
-        return bench_diversity(args, cfg, world, rank, dev, dist, backend)
-    n, d, k = cfg["n"], cfg["d"], cfg["k"]
-    lo, hi, shard = parallel.shard_range(n, world, rank)
-    x = make_pool_rows(lo, hi, d, cfg["dist"], dev)
-    forest = Forest.synthetic(cfg["trees"], cfg["depth"], d, seed=1, dist=cfg["dist"])
-    excluded = np.arange(N_EXCLUDED)
-    unl = torch.arange(N_EXCLUDED, n, device=dev, dtype=torch.int64)
-    n_scored = n - N_EXCLUDED
-
-    if world > 1:
-        sel = parallel.ShardedSelector(x, n, rank, world, excluded=excluded, device=dev)
-        comm = parallel.TorchComm()
-        state = sel.state
-
-        def step():
-            state.clear_caches()
-            sel._density = None
-            return parallel.select(sel, comm, unl, forest, k, mode="dw")
+    if CONFIGS[args.config].get("mode") == "div":
+        out = bench_div(args, steps, warmup, world, rank, dev, dist, backend)
     else:
-        state = engine.PoolState(x, excluded=excluded, device=dev)
-
-        def step():
-            state.clear_caches()
-            r = engine.density_step(state, unl, forest, k)
-            return r.indices, r.selected_scores
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    state.gram_events = []
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        idx, scores = step()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    events = state.gram_events
-    state.gram_events = None
-    # the Gram launches of one step (one, or own-shard + rest when N > 1), averaged over steps
-    gram_ms = sum(a.elapsed_time(b) for a, b in events) / max(args.steps, 1)
-    tdev = dev if backend == "nccl" else "cpu"
-    t = torch.tensor([elapsed, gram_ms], dtype=torch.float64, device=tdev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, gram_ms_max = float(t[0]), float(t[1])
-
-    # warm path: density cached (the reference's density is constant per pool)
-    warm_ms = forest_ms = None
-    if args.warm_steps > 0:
-        if world > 1:
-            parallel.select(sel, comm, unl, forest, k, mode="dw")
-        else:
-            engine.density_step(state, unl, forest, k)
-        torch.cuda.synchronize()
-        barrier()
-        state.forest_events = []
-        tw = time.perf_counter()
-        for _ in range(args.warm_steps):
-            if world > 1:
-                parallel.select(sel, comm, unl, forest, k, mode="dw")
+        out = bench_dw(args, args.config, steps, warmup, warm_steps, world, rank, dev, dist, backend)
+    if extra:
+        out["extra"] = {}
+        for c in extra:
+            if CONFIGS[c].get("mode") == "div":
+                r = bench_div(args, 20, 5, world, rank, dev, dist, backend)
             else:
-                engine.density_step(state, unl, forest, k)
-        torch.cuda.synchronize()
-        barrier()
-        tw = torch.tensor([time.perf_counter() - tw], dtype=torch.float64, device=tdev)
-        if world > 1:
-            dist.all_reduce(tw, op=dist.ReduceOp.MAX)
-        warm_ms = float(tw[0]) * 1000 / args.warm_steps
-        fev = state.forest_events
-        state.forest_events = None
-        if fev:
-            forest_ms = sum(a.elapsed_time(b) for a, b in fev) / len(fev)
-
-    # separable density mode (exact O(N*D) identity): cold step, reported beside
-    sep_ms = None
-    if args.warm_steps > 0:
-        def sep_step():
-            state.clear_caches()
-            if world > 1:
-                sel._density = None
-                return parallel.select(sel, comm, unl, forest, k, mode="dw", density_mode="separable")
-            return engine.density_step(state, unl, forest, k, mode="separable")
-        sep_step()
-        torch.cuda.synchronize()
-        barrier()
-        ts = time.perf_counter()
-        for _ in range(args.warm_steps):
-            sep_step()
-        torch.cuda.synchronize()
-        barrier()
-        ts = torch.tensor([time.perf_counter() - ts], dtype=torch.float64, device=tdev)
-        if world > 1:
-            dist.all_reduce(ts, op=dist.ReduceOp.MAX)
-        sep_ms = float(ts[0]) * 1000 / args.warm_steps
-
-    # roofline of the dominant kernel (density Gram row-sum), this rank's launch
-    rows_local = (hi - lo) - int(np.sum((excluded >= lo) & (excluded < hi)))
-    flops = 2.0 * rows_local * (n - N_EXCLUDED) * d
-    achieved = flops / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else 0.0
-    traffic = None
-    tpath = os.path.join(REPO, "profiles", "hbm_traffic.json")
-    if os.path.exists(tpath):
-        try:
-            tr = json.load(open(tpath)).get(f"config{args.config}")
-            if tr and world == 1:
-                traffic = tr.get({"sym": "gram_rowsum_sym_bytes_per_launch",
-                                  "split": "gram_rowsum_split_bytes_per_launch"}.get(
-                                      state.gram, "gram_rowsum_bytes_per_launch"))
-        except Exception:
-            traffic = None
-
-    ms_per_step = elapsed * 1000 / args.steps
-    out = {
-        "metric": METRIC,
-        "value": n_scored * args.steps / elapsed,
-        "unit": "rows/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": ms_per_step,
-        "higher_is_better": True,
-        "scaling": "strong",
-        "vs_baseline": None,
-        "dtype": "f32" if state.gram == "f32" else "f32 (fp16-split MFMA, fp32 accumulate)",
-        "data": "synthetic (GPU-generated, fixed seeds per 65,536-row chunk); forest synthetic (seed 1)",
-        "config": {"workload": cfg["workload"], "pool_rows": n, "features": d, "trees": cfg["trees"],
-                   "depth": cfg["depth"], "k": k, "excluded": N_EXCLUDED, "rows_scored": n_scored,
-                   "parallelism": f"row-shard dp{world} (RCCL all-gather)" if world > 1 else "single GPU"},
-        "selection_latency_ms": ms_per_step,
-        "warm_selection_latency_ms": warm_ms,
-        "warm_rows_per_s": (n_scored / (warm_ms * 1e-3)) if warm_ms else None,
-        "separable": ({"cold_selection_latency_ms": sep_ms, "rows_per_s": n_scored / (sep_ms * 1e-3),
-                       "note": "density via the exact O(N*D) identity sum_j<u_i,u_j> = <u_i, sum_j u_j> "
-                               "(canonical fp64, same selection); HBM-bound, not the MFMA path"}
-                      if sep_ms else None),
-        "roofline": gram_roofline(state.gram, achieved, traffic, gram_ms, gram_ms_max, flops),
-        "roofline_forest": forest_roofline(state.n, d, cfg["trees"], forest_ms, args.config, world),
-        "cpu_baseline": None,
-    }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle import dal_oracle as O
-
-        of = O.synthetic_forest(cfg["trees"], cfg["depth"], d, seed=1, dist=cfg["dist"])
-        out["cpu_baseline"] = cpu_baseline(x.cpu().numpy(), cfg, of)
+                r = bench_dw(args, c, 20, 5, 20, world, rank, dev, dist, backend, cpu=False)
+            out["extra"][f"config{c}"] = {kk: r[kk] for kk in (
+                "value", "unit", "steps", "ms_per_step", "config", "warm_selection_latency_ms", "self_check",
+                "roofline", "roofline_forest", "roofline_topk") if kk in r}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -68,11 +68,20 @@ struct Mc2Cfg {
 // NW = waves per block (64 pool rows each).  NW = 8 (one 512-thread block per
 // CU, still two waves per SIMD, half the DMA issue per MFMA) measured 12 %
 // slower than NW = 4 at 8M x 128 (barriers over 8 waves), so NW = 4 is used.
-template <int DK, int OCC, int NW>
+//
+// ARG: also the arg-max (labeled-row position l) of every pool row.  Each lane
+// keeps, per accumulator slot, its best value b1 (first l on equal values: l
+// grows along a lane's columns and only a strictly larger value replaces b1),
+// that value's l, and the runner-up b2; a butterfly over the 32 column lanes
+// merges the triples.  When the scaled top two are more than 2 x the error
+// bound apart the fp32 arg-max is the canonical one (|m_gpu - m_canon| <= err
+// per entry); otherwise the row gets -1 - l and dal_maxcos_argmax_resolve
+// recomputes it in canonical fp64.
+template <int DK, int OCC, int NW, bool ARG = false>
 __global__ __launch_bounds__(64 * NW, OCC) void maxcos2_kernel(
     const uint16_t* __restrict__ pool, int64_t n, const uint16_t* __restrict__ lab, int64_t m_pad,
     const float* __restrict__ inv_lab, const float* __restrict__ inv_pool, float* __restrict__ out,
-    int32_t* __restrict__ status) {
+    int32_t* __restrict__ out_arg, double gap, int32_t* __restrict__ status) {
   using C = Mc2Cfg<DK, OCC, NW>;
   extern __shared__ __attribute__((aligned(16))) float4 mc_dyn[];
   float4* lds = mc_dyn;
@@ -142,8 +151,27 @@ __global__ __launch_bounds__(64 * NW, OCC) void maxcos2_kernel(
   }
 
   float mx0[16], mx1[16];
+  float sb0[ARG ? 16 : 1], sb1[ARG ? 16 : 1];  // runner-up values (ARG)
+  int ag0[ARG ? 16 : 1], ag1[ARG ? 16 : 1];    // arg of mx (ARG)
 #pragma unroll
   for (int r = 0; r < 16; ++r) mx0[r] = mx1[r] = -__builtin_inff();
+  if constexpr (ARG) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sb0[r] = sb1[r] = -__builtin_inff();
+      ag0[r] = ag1[r] = 0x7FFFFFFF;
+    }
+  }
+  // (b1, l, b2) <- v at column l; NaN (padding) never replaces b1 or b2
+  auto upd = [](float& b1, float& b2, int& a, float v, int l) {
+    if (v > b1) {
+      b2 = b1;
+      b1 = v;
+      a = l;
+    } else {
+      b2 = fmaxf(b2, v);
+    }
+  };
   const f32x16 zero = {};
 
   // per-lane LDS offsets of the B fragment of each k-step (float4 units);
@@ -175,10 +203,21 @@ __global__ __launch_bounds__(64 * NW, OCC) void maxcos2_kernel(
       }
       // padded labeled rows carry NaN -> ignored by fmaxf
       const float ila = invl[st * C::SR + ct * 32 + li], ilb = invl[st * C::SR + ct * 32 + 32 + li];
+      if constexpr (ARG) {
+        const int la = st * C::SR + ct * 32 + li;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        mx0[r] = fmaxf(fmaxf(mx0[r], c0[r] * ila), d0[r] * ilb);  // one v_max3
-        mx1[r] = fmaxf(fmaxf(mx1[r], c1[r] * ila), d1[r] * ilb);
+        for (int r = 0; r < 16; ++r) {
+          upd(mx0[r], sb0[r], ag0[r], c0[r] * ila, la);
+          upd(mx0[r], sb0[r], ag0[r], d0[r] * ilb, la + 32);
+          upd(mx1[r], sb1[r], ag1[r], c1[r] * ila, la);
+          upd(mx1[r], sb1[r], ag1[r], d1[r] * ilb, la + 32);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          mx0[r] = fmaxf(fmaxf(mx0[r], c0[r] * ila), d0[r] * ilb);  // one v_max3
+          mx1[r] = fmaxf(fmaxf(mx1[r], c1[r] * ila), d1[r] * ilb);
+        }
       }
     }
   };
@@ -205,10 +244,21 @@ __global__ __launch_bounds__(64 * NW, OCC) void maxcos2_kernel(
       }
       // padded labeled rows carry NaN -> ignored by fmaxf
       const float ila = invl[st * C::SR + ct * 32 + li], ilb = invl[st * C::SR + ct * 32 + 32 + li];
+      if constexpr (ARG) {
+        const int la = st * C::SR + ct * 32 + li;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        mx0[r] = fmaxf(fmaxf(mx0[r], c0[r] * ila), d0[r] * ilb);  // one v_max3
-        mx1[r] = fmaxf(fmaxf(mx1[r], c1[r] * ila), d1[r] * ilb);
+        for (int r = 0; r < 16; ++r) {
+          upd(mx0[r], sb0[r], ag0[r], c0[r] * ila, la);
+          upd(mx0[r], sb0[r], ag0[r], d0[r] * ilb, la + 32);
+          upd(mx1[r], sb1[r], ag1[r], c1[r] * ila, la);
+          upd(mx1[r], sb1[r], ag1[r], d1[r] * ilb, la + 32);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          mx0[r] = fmaxf(fmaxf(mx0[r], c0[r] * ila), d0[r] * ilb);  // one v_max3
+          mx1[r] = fmaxf(fmaxf(mx1[r], c1[r] * ila), d1[r] * ilb);
+        }
       }
     }
   };
@@ -225,6 +275,59 @@ __global__ __launch_bounds__(64 * NW, OCC) void maxcos2_kernel(
   } else {
     // d = 64 unrolled twice exceeds the 256-register budget: keep one body
     for (int st = 0; st < n_stages; ++st) stage_body_rt(st);
+  }
+  if constexpr (ARG) {
+    // butterfly over the 32 column lanes, every slot j: merge (b1, l, b2)
+    float b1[32], b2[32];
+    int ag[32];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      b1[r] = mx0[r];
+      b1[16 + r] = mx1[r];
+      b2[r] = sb0[r];
+      b2[16 + r] = sb1[r];
+      ag[r] = ag0[r];
+      ag[16 + r] = ag1[r];
+    }
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        const float ob1 = __shfl_xor(b1[j], o), ob2 = __shfl_xor(b2[j], o);
+        const int oa = __shfl_xor(ag[j], o);
+        if (ob1 > b1[j] || (ob1 == b1[j] && oa < ag[j])) {
+          b2[j] = fmaxf(b1[j], ob2);
+          b1[j] = ob1;
+          ag[j] = oa;
+        } else {
+          b2[j] = fmaxf(b2[j], ob1);
+        }
+      }
+    }
+    // lane li finishes slot j = li: row tile li>>4, accumulator element li&15
+    float v1 = b1[0], v2 = b2[0];
+    int va = ag[0];
+#pragma unroll
+    for (int j = 1; j < 32; ++j) {
+      if (li == j) {
+        v1 = b1[j];
+        v2 = b2[j];
+        va = ag[j];
+      }
+    }
+    const int r = li & 15;
+    const int rl = (li >> 4) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+    const float inv0 = __shfl(inv_row[0], rl & 31), inv1 = __shfl(inv_row[1], rl & 31);
+    const int64_t row = row0 + rl;
+    if (row < n) {
+      const float iv = inv_pool ? inv_pool[row] : ((rl >> 5) ? inv1 : inv0);
+      if (!(iv < __builtin_inff())) atomicOr(status, DAL_FLAG_ZERO_NORM);
+      const float m1 = v1 * iv, m2 = v2 * iv;
+      out[row] = m1;
+      const bool certain = static_cast<double>(m1) - static_cast<double>(m2) > gap;
+      out_arg[row] = certain ? va : -1 - va;
+    }
+    return;
   }
   // max over the 32 column lanes by recursive halving: at mask m a lane keeps
   // the half of its 2m values selected by (li & m) and folds in the partner's
@@ -301,19 +404,101 @@ __global__ __launch_bounds__(64) void canon_unit_rows_bf16_kernel(const uint16_t
   }
 }
 
-template <int DK>
-int launch_maxcos(const uint16_t* pool, int64_t n, const uint16_t* lab, int64_t m_pad, const float* inv_lab,
-                  const float* inv_pool, float* out, int32_t* status, hipStream_t st) {
+// Canonical fp64 arg-max of the rows dal_max_cosine marked ambiguous
+// (out_arg < 0): u_i = x_i / sqrt(sum_f x_if^2) (sequential), cos_il =
+// sum_f u_if * ulab[f][l] (sequential in f, no FMA), max over l, first l on
+// ties (oracle max_cosine_canonical).  One block per 256 rows; a block walks
+// its ambiguous rows one at a time with the 256 lanes over labeled rows.
+__global__ __launch_bounds__(256) void maxcos_argmax_resolve_kernel(const uint16_t* __restrict__ pool, int64_t n,
+                                                                    int d, int64_t ld,
+                                                                    const double* __restrict__ ulabT, int64_t m,
+                                                                    int32_t* __restrict__ out_arg) {
+  __shared__ int list[256];
+  __shared__ int count;
+  __shared__ double su[256];
+  __shared__ double s_nr;
+  __shared__ double rb[4];
+  __shared__ int ra[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + tid;
+  if (tid == 0) count = 0;
+  __syncthreads();
+  if (i < n && out_arg[i] < 0) list[atomicAdd(&count, 1)] = tid;
+  __syncthreads();
+  const int cnt = count;
+  for (int q = 0; q < cnt; ++q) {
+    const int64_t row = static_cast<int64_t>(blockIdx.x) * 256 + list[q];
+    const uint16_t* xr = pool + row * ld;
+    if (tid == 0) {
+      double n2 = 0.0;
+      for (int f = 0; f < d; ++f) {
+        const double v = bf16_to_f32(xr[f]);
+        n2 = n2 + v * v;
+      }
+      s_nr = __builtin_sqrt(n2);
+    }
+    __syncthreads();
+    if (tid < d) su[tid] = static_cast<double>(bf16_to_f32(xr[tid])) / s_nr;
+    __syncthreads();
+    double best = -__builtin_inf();
+    int arg = 0x7FFFFFFF;
+    for (int64_t l = tid; l < m; l += 256) {
+      double acc = 0.0;
+      for (int f = 0; f < d; ++f) acc = acc + su[f] * ulabT[static_cast<int64_t>(f) * m + l];
+      if (acc > best) {  // l grows per lane: strict > keeps the first
+        best = acc;
+        arg = static_cast<int>(l);
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ob = __shfl_xor(best, o);
+      const int oa = __shfl_xor(arg, o);
+      if (ob > best || (ob == best && oa < arg)) {
+        best = ob;
+        arg = oa;
+      }
+    }
+    if (lane == 0) {
+      rb[wave] = best;
+      ra[wave] = arg;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double b = rb[0];
+      int a = ra[0];
+      for (int w = 1; w < 4; ++w) {
+        if (rb[w] > b || (rb[w] == b && ra[w] < a)) {
+          b = rb[w];
+          a = ra[w];
+        }
+      }
+      out_arg[row] = a;
+    }
+    __syncthreads();
+  }
+}
+
+template <int DK, bool ARG>
+int launch_maxcos_t(const uint16_t* pool, int64_t n, const uint16_t* lab, int64_t m_pad, const float* inv_lab,
+                    const float* inv_pool, float* out, int32_t* out_arg, double gap, int32_t* status,
+                    hipStream_t st) {
   const int64_t blocks = ceil_div(n, kMcRows);
   constexpr int OCC = DK <= 128 ? 2 : 1;
   const size_t shm = 2 * Mc2Cfg<DK, OCC>::STAGE + static_cast<size_t>(m_pad) * 4;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(maxcos2_kernel<DK, OCC, 4>),
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(maxcos2_kernel<DK, OCC, 4, ARG>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm)) != hipSuccess)
     return DAL_ERR_HIP;
-  hipLaunchKernelGGL((maxcos2_kernel<DK, OCC, 4>), dim3(static_cast<unsigned>(blocks)), dim3(kMcThreads), shm, st,
-                     pool, n, lab, m_pad, inv_lab, inv_pool, out, status);
+  hipLaunchKernelGGL((maxcos2_kernel<DK, OCC, 4, ARG>), dim3(static_cast<unsigned>(blocks)), dim3(kMcThreads), shm,
+                     st, pool, n, lab, m_pad, inv_lab, inv_pool, out, out_arg, gap, status);
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
+}
+
+template <int DK>
+int launch_maxcos(const uint16_t* pool, int64_t n, const uint16_t* lab, int64_t m_pad, const float* inv_lab,
+                  const float* inv_pool, float* out, int32_t* out_arg, double gap, int32_t* status, hipStream_t st) {
+  if (out_arg) return launch_maxcos_t<DK, true>(pool, n, lab, m_pad, inv_lab, inv_pool, out, out_arg, gap, status, st);
+  return launch_maxcos_t<DK, false>(pool, n, lab, m_pad, inv_lab, inv_pool, out, nullptr, 0.0, status, st);
 }
 
 }  // namespace
@@ -350,14 +535,29 @@ extern "C" double dal_maxcos_error_bound(int64_t d) {
 }
 
 extern "C" int dal_max_cosine(const uint16_t* pool, int64_t n, int64_t d, const uint16_t* lab, int64_t m_pad,
-                              const float* inv_lab, const float* inv_pool, float* out_max,
+                              const float* inv_lab, const float* inv_pool, float* out_max, int32_t* out_arg,
                               int32_t* dev_status, dal_stream_t stream) {
   if (!pool || !lab || !inv_lab || !out_max || !dev_status) return DAL_ERR_ARG;
   if (n < 1 || (d != 64 && d != 128 && d != 256)) return DAL_ERR_SHAPE;
   if (m_pad < 1 || m_pad % dal_maxcos_label_rows_granule(d) || m_pad > kMaxLab) return DAL_ERR_SHAPE;
   if ((reinterpret_cast<uintptr_t>(pool) | reinterpret_cast<uintptr_t>(lab)) & 15) return DAL_ERR_SHAPE;
   hipStream_t st = as_stream(stream);
-  if (d == 64) return launch_maxcos<64>(pool, n, lab, m_pad, inv_lab, inv_pool, out_max, dev_status, st);
-  if (d == 128) return launch_maxcos<128>(pool, n, lab, m_pad, inv_lab, inv_pool, out_max, dev_status, st);
-  return launch_maxcos<256>(pool, n, lab, m_pad, inv_lab, inv_pool, out_max, dev_status, st);
+  // two entries within err of their canonical values are ordered canonically
+  // when their fp32 values differ by more than 2 err (+ slack for the fp32
+  // row scaling, which is monotone)
+  const double gap = 2.0 * dal_maxcos_error_bound(d) * (1.0 + 1e-6) + 1e-30;
+  if (d == 64) return launch_maxcos<64>(pool, n, lab, m_pad, inv_lab, inv_pool, out_max, out_arg, gap, dev_status, st);
+  if (d == 128)
+    return launch_maxcos<128>(pool, n, lab, m_pad, inv_lab, inv_pool, out_max, out_arg, gap, dev_status, st);
+  return launch_maxcos<256>(pool, n, lab, m_pad, inv_lab, inv_pool, out_max, out_arg, gap, dev_status, st);
+}
+
+extern "C" int dal_maxcos_argmax_resolve(const uint16_t* pool, int64_t n, int64_t d, int64_t ld, const double* ulab,
+                                         int64_t m, int32_t* out_arg, dal_stream_t stream) {
+  if (!pool || !ulab || !out_arg) return DAL_ERR_ARG;
+  if (n < 1 || d < 1 || d > 256 || ld < d || m < 1 || m > 0x7FFFFFFF) return DAL_ERR_SHAPE;
+  hipLaunchKernelGGL(maxcos_argmax_resolve_kernel, dim3(static_cast<unsigned>(ceil_div(n, 256))), dim3(256), 0,
+                     as_stream(stream), pool, n, static_cast<int>(d), ld, ulab, m, out_arg);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
 }

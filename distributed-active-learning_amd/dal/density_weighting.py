@@ -34,17 +34,30 @@ def information_density(pool, excluded_idx=None, device=None, mode: str = "gram"
     return d
 
 
-def select(pool, unlabeled_idx, forest: Forest, k: int, beta: float = 1.0, excluded_idx=None,
-           density=None, device=None, mode: str = "gram") -> Selection:
+L0 = "L0"  # excluded_idx default: the reference's initial labeled window
+
+
+def select(pool, unlabeled_idx, forest: Forest, k: int, beta: float = 1.0, excluded_idx=L0,
+           density=None, device=None, mode: str = "gram", window_size=None) -> Selection:
     """Score every unlabeled row by entropy x density^beta and select the top k.
 
-    excluded_idx  rows dropped from the density (default: none; the reference
-                  passes its initial labeled window, range(window_size))
+    excluded_idx  rows dropped from the density as i and as j.  Default "L0":
+                  the reference's initial labeled window range(window_size)
+                  (density_weighting.py:89,95-100; window_size defaults to k,
+                  as the script's take(window_size) at :172); for a PoolState
+                  the default keeps the state's own excluded set.  None or []
+                  excludes nothing.
     density       optional int64 fixed-point density from a previous call
                   (PoolState.density_fixed()); by default the pool's cached one
     mode          "gram" (default, the reference's algorithm on MFMA) or
                   "separable" (exact O(N*D) identity; same selection)
     """
+    if isinstance(excluded_idx, str):
+        if excluded_idx != L0:
+            raise ValueError(f"excluded_idx must be index-like, None or {L0!r}")
+        excluded_idx = None if isinstance(pool, PoolState) else range(int(window_size or k))
+    elif excluded_idx is None and isinstance(pool, PoolState):
+        excluded_idx = []
     state = as_pool_state(pool, excluded=excluded_idx, device=device)
     return density_step(state, unlabeled_idx, forest, k, beta=beta, density_fixed=density, mode=mode)
 

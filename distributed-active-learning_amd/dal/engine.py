@@ -81,6 +81,10 @@ class Selection:
         self._votes = self._gathered(self._votes)
         return self._votes
 
+    def __iter__(self):
+        """Unpacks as the reference-shaped triple (scores, indices, selected_scores)."""
+        return iter((self.scores, self.indices, self.selected_scores))
+
     def __repr__(self):
         return f"Selection(indices={self.indices!r}, selected_scores={self.selected_scores!r})"
 
@@ -135,7 +139,9 @@ class PoolState:
         self._density_exact = None
         self.gram_events = None  # list -> (start, end) HIP events around each Gram call
         self.forest_events = None  # list -> (start, end) HIP events around each forest-score call
+        self.select_events = None  # list -> (start, end) HIP events around each dal_dw_select call
         self.cap_scale = 1  # re-rank candidate capacity multiplier, kept after an overflow
+        self.cap_base = None  # initial re-rank capacity override (tests: force the overflow path)
         self.last_status = 0     # status word read by the last synchronising select
 
     def clear_caches(self):
@@ -148,7 +154,12 @@ class PoolState:
         """E (global indices): dropped from the density as i and as j
         (density_weighting.py:95-100)."""
         torch = _torch()
-        ex = np.unique(np.asarray([] if excluded is None else excluded, dtype=np.int64))
+        ex = np.unique(np.asarray([] if excluded is None else list(excluded) if isinstance(excluded, range)
+                                  else excluded, dtype=np.int64).reshape(-1))
+        if ex.size and (ex[0] < 0 or ex[-1] >= self.n_total):
+            # the density error bound counts |E| columns: an index outside the
+            # pool would make the interval keys (and the exact selection) unsound
+            raise ValueError(f"excluded indices must lie in [0, {self.n_total})")
         if np.array_equal(ex, self.excluded) and hasattr(self, "_u"):
             return
         self.excluded = ex
@@ -506,18 +517,26 @@ def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k
     norm64 = state.norms()
     if sync:  # single-GPU: start from the capacity a previous overflow grew to
         cap_scale = max(cap_scale, state.cap_scale)
-    cap = int(min(n, candidate_cap(n, k) * cap_scale))
+    base = candidate_cap(n, k) if state.cap_base is None else max(int(k), int(state.cap_base))
+    cap = int(min(n, base * cap_scale))
     while True:
         wsb = int(lib.dal_dw_select_workspace_bytes(n, k, cap))
         ws, wsp = workspace(wsb, state.device)
         out_idx = torch.empty(k, dtype=torch.int64, device=state.device)
         out_scores = torch.empty(k, dtype=torch.float64, device=state.device)
         out_keys = torch.empty(k, dtype=torch.int64, device=state.device)
+        ev = None
+        if state.select_events is not None:  # bench: K3 timing on the launch stream
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         call("dal_dw_select", _ptr(keys_lo), _ptr(keys_hi), _ptr(votes), _ptr(flags), n, k,
              state.row_base, _ptr(lut_dev), float(beta), _ptr(state.x), state.d, state.d,
              _ptr(norm64), _ptr(colsum), cap, wsp, wsb, _ptr(out_idx), _ptr(out_scores),
              _ptr(out_keys), _ptr(state.status),
              0 if colsum_ready is None else colsum_ready.cuda_event, _stream(state.device))
+        if ev is not None:
+            ev[1].record()
+            state.select_events.append(ev)
         if not sync:
             return out_idx, out_scores, out_keys
         # the step's one host sync: status word (zero-norm rows, candidate overflow)

@@ -99,6 +99,7 @@ class ShardedSelector:
         self.state = PoolState(x_local, excluded=excluded, device=device, row_base=self.lo,
                                n_total=self.n_total, n_pad=self.shard, gram=gram)
         self._density = None
+        self._parts_full = None  # all ranks' canonical column-sum partials (cached with the density)
         self.cap_scale = 1      # re-rank candidate capacity multiplier (grown on overflow)
 
     def index_tensor(self, unlabeled_idx):
@@ -111,11 +112,17 @@ class ShardedSelector:
         return self.state.status
 
     def prepare_retry(self):
-        """After a re-rank capacity overflow anywhere: clear, grow, go again."""
+        """After a re-rank capacity overflow anywhere: grow the capacity and go
+        again.  The density, operand and column-sum caches stay valid (only the
+        re-rank capacity changed), so the retry does not redo the Gram."""
         self.state.status.zero_()
         self.cap_scale *= 4
+
+    def clear_caches(self):
+        """Drop the shard's normalised rows, density and column sums (cold step)."""
         self.state.clear_caches()
         self._density = None
+        self._parts_full = None
 
     # ---- phase A: local normalisation + canonical partials ------------
     def prep(self):
@@ -364,13 +371,17 @@ def select(sel: ShardedSelector, comm, unlabeled_idx, forest, k: int, mode: str 
     """One selection step across all ranks; returns (indices [k], scores [k]),
     identical on every rank."""
     unl = sel.index_tensor(unlabeled_idx)
-    u_local, parts = sel.prep()
-    need_u = mode == "dw" and density_mode == "gram" and sel._density is None
-    if need_u:  # the (small) canonical partials travel with the operand, beside the Gram
-        u_full, parts_full = sel.exchange_density(comm, u_local, parts)
-    else:
-        u_full = None
-        parts_full = comm.all_gather(parts) if mode == "dw" else None
+    u_full = parts_full = None
+    if mode == "dw":  # uncertainty sampling never normalises (no density, no zero-norm check)
+        need_u = density_mode == "gram" and sel._density is None
+        if need_u or sel._parts_full is None:
+            u_local, parts = sel.prep()
+            if need_u:  # the (small) canonical partials travel with the operand, beside the Gram
+                u_full, parts_full = sel.exchange_density(comm, u_local, parts)
+            else:
+                parts_full = comm.all_gather(parts)
+            sel._parts_full = parts_full
+        parts_full = sel._parts_full
     top = sel.local_select(u_full, parts_full, unl, forest, k, mode, strategy, beta, density_mode)
     # every rank's status word (zero-norm rows, re-rank capacity overflow)
     # rides in the top-k all-gather and is read once, after the merge is
@@ -381,6 +392,8 @@ def select(sel: ShardedSelector, comm, unlabeled_idx, forest, k: int, mode: str 
     st = 0
     for v in st_all.tolist():
         st |= int(v)
+    if mode != "dw":
+        st &= ~_lib.DAL_FLAG_ZERO_NORM  # a zero row only matters to the cosine density
     if st & _lib.DAL_FLAG_ZERO_NORM:
         raise ValueError("pool contains a zero-norm row: cosine similarity is undefined "
                          "(the reference would propagate NaN into every density)")

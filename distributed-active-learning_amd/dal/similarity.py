@@ -20,9 +20,6 @@ def column_similarities(pool, device=None):
     return ij[0], ij[1], S[ij[0], ij[1]]
 
 
-
-
-
 # ---------------------------------------------------------------------------
 # Batch-mode diversity (BASELINE config 5): max-cosine to a labeled set
 # ---------------------------------------------------------------------------
@@ -74,8 +71,14 @@ class LabeledSet:
 
 
 def max_cosine(pool, labeled_idx, device=None):
-    """m_i = max_{l in labeled} cos(x_i, x_l) for every pool row (fp32 [N]),
-    bf16 MFMA with fp32 accumulation (|error| <= dal_maxcos_error_bound(d))."""
+    """(m, arg): m_i = max_{l in labeled} cos(x_i, x_l) for every pool row
+    (fp32 [N]; bf16 MFMA with fp32 accumulation, |error| <=
+    dal_maxcos_error_bound(d)) and its arg-max (int32 [N], the position l in
+    ``labeled_idx``; the canonical fp64 arg-max, first l on ties -- rows whose
+    fp32 top two cannot be ordered are re-ranked exactly in fp64).
+
+    Restates similarity.py:34-38 (columnSimilarities of the normalised pool,
+    i.e. every pairwise cosine) reduced to the nearest labeled row."""
     import torch
 
     from . import _lib
@@ -86,11 +89,14 @@ def max_cosine(pool, labeled_idx, device=None):
     lab = LabeledSet(x[_as_index(labeled_idx, dev)], dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     out = torch.empty(n, dtype=torch.float32, device=dev)
+    arg = torch.empty(n, dtype=torch.int32, device=dev)
     _lib.call("dal_max_cosine", _ptr(x), n, d, _ptr(lab.rows), lab.m_pad, _ptr(lab.inv), 0,
-              _ptr(out), _ptr(status), _stream(dev))
+              _ptr(out), _ptr(arg), _ptr(status), _stream(dev))
+    _lib.call("dal_maxcos_argmax_resolve", _ptr(x), n, d, d, _ptr(lab.unit64_t), lab.m, _ptr(arg),
+              _stream(dev))
     if int(status.item()) | int(lab.status.item()):
         raise ValueError("zero-norm row: cosine undefined")
-    return out
+    return out, arg
 
 
 def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, row_base: int = 0,
@@ -121,7 +127,7 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     mx = torch.empty(n, dtype=torch.float32, device=dev)
     _lib.call("dal_max_cosine", _ptr(x), n, d, _ptr(lab.rows), lab.m_pad, _ptr(lab.inv), 0,
-              _ptr(mx), _ptr(status), _stream(dev))
+              _ptr(mx), 0, _ptr(status), _stream(dev))
     if candidates is None:
         flags = torch.full((n,), DAL_ROW_CANDIDATE, dtype=torch.uint8, device=dev)
         cand = torch.arange(n, device=dev)
@@ -132,9 +138,11 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
         _lib.call("dal_mark_rows", _ptr(gidx), int(gidx.shape[0]), int(row_base), n, DAL_ROW_CANDIDATE,
                   _ptr(flags), _stream(dev))
         cand = gidx - row_base
-        if row_base != 0:
-            cand = cand[(cand >= 0) & (cand < n)]
+        cand = cand[(cand >= 0) & (cand < n)]  # global candidates of other shards are not ours
         n_cand = int(cand.shape[0])
+        if n_cand == 0:
+            return Selection(scores=mx[cand], indices=torch.empty(0, dtype=torch.int64, device=dev),
+                             selected_scores=torch.empty(0, dtype=torch.float64, device=dev))
     kk = min(int(k), n_cand)
     lo = torch.empty(n, dtype=torch.int64, device=dev)
     hi = torch.empty(n, dtype=torch.int64, device=dev)

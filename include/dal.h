@@ -264,9 +264,22 @@ int dal_inv_norms_bf16(const uint16_t* x, int64_t n, int64_t n_pad, int64_t d, i
  * rows: u[i * d + f] (feature_major = 0) or u[f * n + i] (feature_major = 1). */
 int dal_canon_unit_rows_bf16(const uint16_t* x, int64_t n, int64_t d, int64_t ld, int feature_major,
                              double* u, dal_stream_t stream);
+/* out_arg (nullable): the arg-max l (position in the labeled table, first l
+ * among equal values) of every row.  A row whose two largest fp32 cosines are
+ * within 2 x dal_maxcos_error_bound(d) of each other cannot be ordered from
+ * the fp32 values: it gets -1 - l, and dal_maxcos_argmax_resolve replaces
+ * every such entry by the canonical fp64 arg-max (similarity.py:34-38,
+ * columnSimilarities' exact cosines; ties -> first l).  Every other entry is
+ * already the canonical arg-max. */
 int dal_max_cosine(const uint16_t* pool, int64_t n, int64_t d, const uint16_t* lab, int64_t m_pad,
-                   const float* inv_lab, const float* inv_pool, float* out_max,
+                   const float* inv_lab, const float* inv_pool, float* out_max, int32_t* out_arg,
                    int32_t* dev_status, dal_stream_t stream);
+/* Canonical fp64 arg-max (oracle max_cosine_canonical: sequential norm and
+ * dot products, no FMA, first l on ties) of every row with out_arg < 0;
+ * ulab = canonical fp64 unit rows of the m labeled rows, feature-major [d][m]
+ * (dal_canon_unit_rows_bf16 with feature_major = 1); d <= 256. */
+int dal_maxcos_argmax_resolve(const uint16_t* pool, int64_t n, int64_t d, int64_t ld, const double* ulab,
+                              int64_t m, int32_t* out_arg, dal_stream_t stream);
 /* Interval keys [v - err, v + err] of fp32 values (pessimistic -> keys_lo). */
 int dal_interval_keys_f32(const float* values, int64_t n, double err, const uint8_t* row_flags,
                           int order, uint64_t* keys_lo, uint64_t* keys_hi, dal_stream_t stream);

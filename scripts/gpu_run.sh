@@ -1,0 +1,80 @@
+#!/bin/bash
+# One parameterised GPU-box runner (replaces the round-1 one-shot job files).
+#
+#   gpurun --timeout 900 -- bash scripts/gpu_run.sh STEP [STEP ...]
+#
+# STEP (run in order, each under its own time limit; the first failure ends
+# the call -- no GPU step runs after a fault, abort or timeout):
+#   tests[=EXPR]          pytest -m gpu (optionally -k EXPR)  -> gpurun_out/pytest_gpu.log
+#   smoke                 __graft_entry__.smoke()             -> gpurun_out/smoke.log
+#   bench[=ARGS]          python bench.py ARGS (',' = space)  -> gpurun_out/bench_<n>.log
+#   stats=TAG[=ARGS]      rocprofv3 --kernel-trace --stats of bench.py ARGS -> gpurun_out/prof_TAG/
+#   pmc=TAG=CTRS[=ARGS]   rocprofv3 --pmc CTRS (',' = space) of bench.py ARGS -> gpurun_out/pmc_TAG/
+#   py=SCRIPT[=ARGS]      python SCRIPT ARGS                  -> gpurun_out/py_<n>.log
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+n=0
+for step in "$@"; do
+  n=$((n + 1))
+  kind=${step%%=*}
+  rest=""
+  [[ "$step" == *=* ]] && rest=${step#*=}
+  case "$kind" in
+    tests)
+      k=()
+      [ -n "$rest" ] && k=(-k "$rest")
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread "${k[@]}" \
+        > gpurun_out/pytest_gpu.log 2>&1
+      rc=$?
+      echo "[$n] tests rc=$rc: $(tail -1 gpurun_out/pytest_gpu.log)"
+      ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+      rc=$?
+      echo "[$n] smoke rc=$rc: $(tail -1 gpurun_out/smoke.log)"
+      ;;
+    bench)
+      timeout -k 10 900 python -u bench.py ${rest//,/ } > gpurun_out/bench_$n.log 2>&1
+      rc=$?
+      echo "[$n] bench ${rest//,/ } rc=$rc"
+      tail -1 gpurun_out/bench_$n.log | cut -c1-600
+      ;;
+    stats)
+      tag=${rest%%=*}
+      args=""
+      [[ "$rest" == *=* ]] && args=${rest#*=}
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$tag -o run -- \
+        python3 -u bench.py ${args//,/ } > gpurun_out/prof_$tag.log 2>&1
+      rc=$?
+      echo "[$n] stats $tag rc=$rc"
+      tail -1 gpurun_out/prof_$tag.log | cut -c1-300
+      ;;
+    pmc)
+      tag=${rest%%=*}
+      r2=${rest#*=}
+      ctrs=${r2%%=*}
+      args=""
+      [[ "$r2" == *=* ]] && args=${r2#*=}
+      timeout -s KILL 240 rocprofv3 --pmc ${ctrs//,/ } -d gpurun_out/pmc_$tag -o run -- \
+        python3 -u bench.py ${args//,/ } > gpurun_out/pmc_$tag.log 2>&1
+      rc=$?
+      echo "[$n] pmc $tag rc=$rc"
+      ;;
+    py)
+      scr=${rest%%=*}
+      args=""
+      [[ "$rest" == *=* ]] && args=${rest#*=}
+      timeout -k 10 900 python -u $scr ${args//,/ } > gpurun_out/py_$n.log 2>&1
+      rc=$?
+      echo "[$n] py $scr rc=$rc"
+      tail -5 gpurun_out/py_$n.log | cut -c1-600
+      ;;
+    *)
+      echo "unknown step $step"
+      exit 2
+      ;;
+  esac
+  [ $rc -eq 0 ] || exit $rc
+done

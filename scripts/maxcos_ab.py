@@ -37,7 +37,7 @@ for n, d, m in shapes:
             torch.cuda.synchronize()
             e0.record()
             _lib.call("dal_max_cosine", _ptr(x), n, d, _ptr(lab.rows), lab.m_pad, _ptr(lab.inv), 0,
-                      _ptr(out), _ptr(st), _stream(dev))
+                      _ptr(out), 0, _ptr(st), _stream(dev))
             e1.record()
             torch.cuda.synchronize()
             if r:

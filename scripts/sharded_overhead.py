@@ -34,8 +34,7 @@ st = engine.PoolState(x, excluded=E, device=dev)
 
 
 def sharded():
-    sel.state.clear_caches()
-    sel._density = None
+    sel.clear_caches()
     return parallel.select(sel, comm, unl, forest, k, mode="dw")
 
 

@@ -1,0 +1,139 @@
+"""Full-size parity of the density-weighted selection at BASELINE configs 3
+and 4: the HIP path against the CPU oracle on the exact
+pools bench.py times (numpy default_rng(0), E = L0 = {0..9}, synthetic
+forests from default_rng(1)).
+
+* config 4: 2,000,000 x 256 U[0,1), T = 10, k = 100 and k = 1000 -- selected
+  indices and canonical fp64 scores bit-exact; every row's score within
+  1e-5 relative of the oracle's (the north-star bar), measured at 2M columns;
+* config 3: 284,807 x 30 N(0,1), T = 100, k = 100 -- the signed-data case,
+  bit-exact selection, density within the rigorous bound and within
+  1e-5 x sum_j |S_ij| (SURVEY §8 config 3 tolerance) on sampled rows; the
+  re-rank capacity overflow / grow-and-retry path is forced at full size.
+
+Reference: final_thesis/density_weighting.py:58-100 (density), :136-172
+(votes, entropy x density, sortBy desc, take).
+"""
+import numpy as np
+import pytest
+
+from oracle import dal_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+E = np.arange(10)
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def _rel_err(got, ref):
+    ok = np.isfinite(ref) & (ref != 0)
+    return float(np.max(np.abs(got[ok] - ref[ok]) / np.abs(ref[ok]))) if ok.any() else 0.0
+
+
+@pytest.fixture(scope="module")
+def config4():
+    n, d = 2_000_000, 256
+    X = O.synthetic_pool(n, d, seed=0)
+    of = O.synthetic_forest(10, 4, d, seed=1)
+    dens = O.density_canonical(X, E)
+    return X, of, dens
+
+
+def test_config4_full_size_selection_bit_exact(cuda, config4):
+    import torch
+
+    from dal import density_weighting as dw
+    from dal.engine import PoolState, density_error
+    from dal.forest import Forest
+
+    X, of, dens = config4
+    n = X.shape[0]
+    unl = np.arange(10, n)
+    st = PoolState(torch.from_numpy(X).to(cuda), excluded=E, device=cuda)
+    F = Forest.synthetic(10, 4, X.shape[1], seed=1)
+    # density: within the rigorous bound, and far inside 1e-5 relative
+    d_gpu = _np(st.density("gram"))
+    keep = np.ones(n, bool)
+    keep[E] = False
+    err = np.abs(d_gpu[keep] - dens[keep])
+    assert err.max() <= density_error(st)
+    rel_d = float((err / np.abs(dens[keep])).max())
+    assert rel_d <= 1e-5
+    for k in (100, 1000):
+        sel = dw.select(st, unl, F, k)
+        ref_sc, ref_idx, ref_ss = O.density_select(X, unl, of, k, 1.0, E, density=dens)
+        assert np.array_equal(_np(sel.indices), ref_idx), k
+        assert np.array_equal(_np(sel.selected_scores).view(np.int64), ref_ss.view(np.int64)), k
+        sc = _np(sel.scores)
+        assert np.array_equal(np.isnan(sc), np.isnan(ref_sc))
+        rel = _rel_err(sc, ref_sc)
+        assert rel <= 1e-5, rel
+        print(f"config4 k={k}: max per-score relative error {rel:.3e} (density {rel_d:.3e}) at 2M columns")
+
+
+def test_config4_full_size_separable_mode_identical(cuda, config4):
+    import torch
+
+    from dal import density_weighting as dw
+    from dal.forest import Forest
+
+    X, of, dens = config4
+    unl = np.arange(10, X.shape[0])
+    F = Forest.synthetic(10, 4, X.shape[1], seed=1)
+    sel = dw.select(torch.from_numpy(X).to(cuda), unl, F, 100, excluded_idx=E, mode="separable", device=cuda)
+    ref_sc, ref_idx, ref_ss = O.density_select(X, unl, of, 100, 1.0, E, density=dens)
+    assert np.array_equal(_np(sel.indices), ref_idx)
+    sc = _np(sel.scores)
+    nan = np.isnan(ref_sc)
+    assert np.array_equal(np.isnan(sc), nan)
+    # every score canonical: bit-identical (NaN payloads aside, v = T rows)
+    assert np.array_equal(sc[~nan].view(np.int64), ref_sc[~nan].view(np.int64))
+
+
+@pytest.fixture(scope="module")
+def config3():
+    n, d = 284_807, 30
+    X = O.synthetic_pool(n, d, seed=0, dist="normal")
+    of = O.synthetic_forest(100, 4, d, seed=1, dist="normal")
+    dens = O.density_canonical(X, E)
+    return X, of, dens
+
+
+@pytest.mark.parametrize("forced_cap", [None, 128])
+def test_config3_full_size_selection_bit_exact(cuda, config3, forced_cap):
+    import torch
+
+    from dal import density_weighting as dw
+    from dal.engine import PoolState, density_error
+    from dal.forest import Forest
+
+    X, of, dens = config3
+    n = X.shape[0]
+    unl = np.arange(10, n)
+    st = PoolState(torch.from_numpy(X).to(cuda), excluded=E, device=cuda)
+    if forced_cap is not None:
+        st.cap_base = forced_cap  # 128 slots for k = 100: the overflow -> grow -> retry path
+    F = Forest.synthetic(100, 4, X.shape[1], seed=1, dist="normal")
+    sel = dw.select(st, unl, F, 100)
+    ref_sc, ref_idx, ref_ss = O.density_select(X, unl, of, 100, 1.0, E, density=dens)
+    assert np.array_equal(_np(sel.indices), ref_idx)
+    assert np.array_equal(_np(sel.selected_scores).view(np.int64), ref_ss.view(np.int64))
+    if forced_cap is not None:
+        assert st.cap_scale > 1  # the retry path ran
+        again = dw.select(st, unl, F, 100)  # warm step at the grown capacity
+        assert np.array_equal(_np(again.indices), ref_idx)
+    # density: rigorous bound everywhere; SURVEY's signed-data tolerance
+    # |dd_i| <= 1e-5 * sum_j |S_ij| on a sample of rows (exact fp64 sum_j |S_ij|)
+    d_gpu = _np(st.density("gram"))
+    keep = np.ones(n, bool)
+    keep[E] = False
+    err = np.abs(d_gpu - dens)
+    assert err[keep].max() <= density_error(st)
+    U = O.l2_normalize(X)
+    Uc = U[keep]
+    rows = np.random.default_rng(3).choice(np.arange(10, n), 256, replace=False)
+    abs_sum = np.abs(U[rows] @ Uc.T).sum(axis=1)
+    assert np.all(err[rows] <= 1e-5 * abs_sum)

@@ -19,11 +19,13 @@ def test_max_cosine_within_bound(cuda, n, d, m):
 
     X = O.bf16_round(O.synthetic_pool(n, d, seed=n + d))
     L = np.arange(0, n, max(1, n // m))[:m]
-    got = _np(sim.max_cosine(X, L, device=cuda))
-    ref, _ = O.max_cosine_canonical(X, L)
+    got, arg = sim.max_cosine(X, L, device=cuda)
+    got, arg = _np(got), _np(arg)
+    ref, ref_arg = O.max_cosine_canonical(X, L)
     bound = _lib.load().dal_maxcos_error_bound(d)
     assert np.abs(got - ref).max() <= bound
     assert np.allclose(got[L], 1.0, atol=bound)  # labeled rows match themselves
+    assert np.array_equal(arg, ref_arg)  # canonical arg-max, first l on ties
 
 
 def test_max_cosine_signed_data(cuda):
@@ -32,9 +34,30 @@ def test_max_cosine_signed_data(cuda):
 
     X = O.bf16_round(O.synthetic_pool(2000, 128, seed=5, dist="normal"))
     L = np.arange(100, 612)
-    got = _np(sim.max_cosine(X, L, device=cuda))
-    ref, _ = O.max_cosine_canonical(X, L)
-    assert np.abs(got - ref).max() <= _lib.load().dal_maxcos_error_bound(128)
+    got, arg = sim.max_cosine(X, L, device=cuda)
+    ref, ref_arg = O.max_cosine_canonical(X, L)
+    assert np.abs(_np(got) - ref).max() <= _lib.load().dal_maxcos_error_bound(128)
+    assert np.array_equal(_np(arg), ref_arg)
+
+
+@pytest.mark.parametrize("d", [64, 128, 256])
+def test_max_cosine_argmax_duplicate_labeled_rows(cuda, d):
+    """Duplicated labeled rows (and labeled rows equal up to a positive scale)
+    tie exactly: the arg-max is the FIRST position l, as in the canonical
+    fp64 oracle (similarity.py:34-38 restated; SURVEY §8(b) max_cosine)."""
+    from dal import _lib
+    from dal import similarity as sim
+
+    n = 3000
+    X = O.bf16_round(O.synthetic_pool(n, d, seed=11 + d))
+    X[1000:1010] = X[5]           # pool rows equal to a labeled row
+    L = np.concatenate([np.arange(0, 200), [5, 5, 7, 1005], np.arange(200, 300)])
+    X[7] = X[3] * 2.0             # same direction as row 3 (exact in bf16)
+    got, arg = sim.max_cosine(X, L, device=cuda)
+    ref, ref_arg = O.max_cosine_canonical(X, L)
+    assert np.abs(_np(got) - ref).max() <= _lib.load().dal_maxcos_error_bound(d)
+    assert np.array_equal(_np(arg), ref_arg)
+    assert (ref_arg[1000:1010] == 5).all()  # first of the duplicated positions
 
 
 @pytest.mark.parametrize("n,d,m,k", [(4000, 128, 256, 50), (3000, 64, 700, 200), (2000, 256, 64, 1)])

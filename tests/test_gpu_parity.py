@@ -433,7 +433,7 @@ def test_dw_nan_scores_rank_last(cuda):
     leaf[0] = [0, 1]  # rows with x0 <= 0.5 get v = 3 (finite), others NaN
     F = Forest(inner=inner, leaf=leaf, depth=1)
     unl = np.arange(800)
-    sel = dw.select(X, unl, F, 800)
+    sel = dw.select(X, unl, F, 800, excluded_idx=None)
     of = O.OracleForest  # oracle reference via the golden-free path
     ref_sc, ref_idx, ref_ss = O.density_select(X, unl, _oracle_from(F), 800, 1.0, None)
     assert np.array_equal(_np(sel.indices), ref_idx)

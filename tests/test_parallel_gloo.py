@@ -37,6 +37,7 @@ class OracleShard(parallel.ShardedSelector):
         self.excluded = np.asarray(excluded)
         self.of = of
         self._density = None
+        self._parts_full = None
 
     def prep(self):
         ex = O.exclusion_mask(self.n_total, self.excluded)[self.lo:self.hi]
