@@ -493,7 +493,7 @@ def main():
     warmup = args.warmup if args.warmup is not None else (1 if big else 10)
     warm_steps = args.warm_steps if args.warm_steps is not None else (5 if big else 20)
     extra = args.extra if args.extra is not None else ("2" if args.config == "4" else "")
-    extra = [c for c in extra.split(",") if c]
+    extra = [c for c in extra.split(",") if c and c != "none"]
 
     import torch
     import torch.distributed as dist

@@ -80,6 +80,8 @@ SIGNATURES = {
     "dal_canon_unit_rows_bf16": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p]),
     "dal_max_cosine": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p, c_void_p]),
+    "dal_text_shape": (c_int, [c_void_p, c_size_t, c_int64, c_void_p, c_void_p]),
+    "dal_parse_labeled_text": (c_int, [c_void_p, c_size_t, c_int64, c_int64, c_int, c_void_p, c_void_p, c_int]),
     "dal_maxcos_argmax_resolve": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64, c_void_p,
                                           c_void_p]),
     "dal_interval_keys_f32": (c_int, [c_void_p, c_int64, c_double, c_void_p, c_int, c_void_p,

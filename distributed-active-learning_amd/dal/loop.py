@@ -31,26 +31,12 @@ def load_labeled_text(path: str, n_samples=None, label_map: str = "reference"):
     """Whitespace-separated rows, features then label.  label_map="reference"
     applies the scripts' ``0 if int(label) == -1 else 1`` (uncertainty_sampling.py:39,
     written for the +-1 striatum labels); "as_is" keeps 0/1 labels (the LAL
-    checkerboard files).  Returns (X fp32 [N, D], y int64 [N])."""
-    rows = []
-    with open(path) as fh:
-        for line in fh:
-            parts = line.strip().split()
-            if not parts:
-                continue
-            rows.append(parts)
-            if n_samples is not None and len(rows) >= n_samples:  # data.take(n_samples)
-                break
-    arr = np.array(rows, dtype=np.float64)
-    X = arr[:, :-1].astype(np.float32)
-    lab = arr[:, -1].astype(np.int64)
-    if label_map == "reference":
-        y = np.where(lab == -1, 0, 1).astype(np.int64)
-    elif label_map == "as_is":
-        y = lab
-    else:
-        raise ValueError(label_map)
-    return X, y
+    checkerboard files).  Returns (X fp32 [N, D], y int64 [N]).  Parsed by the
+    native multi-threaded parser (dal.ingest; dal.ingest.load_pool uploads the
+    pool to HBM through pinned memory instead)."""
+    from .ingest import parse_labeled_text
+
+    return parse_labeled_text(path, n_samples=n_samples, label_map=label_map)
 
 
 def train_forest(X, y, n_estimators: int = 10, seed: int = 0, max_depth: int = 4):

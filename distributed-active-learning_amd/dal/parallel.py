@@ -428,9 +428,11 @@ def emulate(selectors, unlabeled_idx, forest, k: int, mode: str = "dw",
             density_mode: str = "gram"):
     """Run P shards in one process (tests): the all-gathers become concatenations."""
     torch = __import__("torch")
-    preps = [s.prep() for s in selectors]
-    u_full = torch.cat([p[0] for p in preps]) if mode == "dw" else None
-    parts_full = torch.cat([p[1] for p in preps]) if mode == "dw" else None
+    u_full = parts_full = None
+    if mode == "dw":  # uncertainty sampling never normalises
+        preps = [s.prep() for s in selectors]
+        u_full = torch.cat([p[0] for p in preps])
+        parts_full = torch.cat([p[1] for p in preps])
     if mode == "dw" and density_mode == "gram" and selectors and selectors[0]._density is None:
         contrib = [s.density_contribution(u_full) for s in selectors]
         if selectors[0].state.gram == "sym":

@@ -302,6 +302,21 @@ int dal_sort_pairs(const uint64_t* keys, const int64_t* idx, const double* paylo
                    int64_t k, uint64_t* out_keys, int64_t* out_idx, double* out_payload,
                    dal_stream_t stream);
 
+/* ---- pool ingest (host-side parser) -------------------------------------
+ * Replaces uncertainty_sampling.py:37-42 / density_weighting.py:45-53,59-65
+ * (sc.textFile -> split -> LabeledPoint(0 if int(_[-1]) == -1 else 1,
+ * np.array(_[:-1]).astype(float)), take(n_samples)).  HOST pointers (the one
+ * exception to the device-pointer convention): ``text`` is a byte range of
+ * whitespace-separated rows, label last; blank lines are skipped.
+ * dal_text_shape: rows (at most max_rows if >= 0) and fields per row.
+ * dal_parse_labeled_text: x [rows][cols-1] fp32 = (float)strtod(field) (the
+ * bits of np.float64 parsing narrowed to fp32), labels [rows] (label_map 0:
+ * -1 -> 0, else 1; 1: as is); x may be pinned memory handed straight to an
+ * async H2D copy.  DAL_ERR_SHAPE: ragged rows; DAL_ERR_ARG: a bad field. */
+int dal_text_shape(const char* text, size_t len, int64_t max_rows, int64_t* rows, int64_t* cols);
+int dal_parse_labeled_text(const char* text, size_t len, int64_t rows, int64_t cols, int label_map, float* x,
+                           int64_t* labels, int n_threads);
+
 /* ---- standalone similarity kernels --------------------------------------
  * cosine_similarity.py:42-45: every entry of U.U^T (fp32 MFMA), written to
  * out[n_pad][n_pad] (fp32).  similarity.py:38 (columnSimilarities, i<j) is

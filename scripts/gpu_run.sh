@@ -45,7 +45,7 @@ for step in "$@"; do
       tag=${rest%%=*}
       args=""
       [[ "$rest" == *=* ]] && args=${rest#*=}
-      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$tag -o run -- \
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -o run -- \
         python3 -u bench.py ${args//,/ } > gpurun_out/prof_$tag.log 2>&1
       rc=$?
       echo "[$n] stats $tag rc=$rc"
@@ -57,7 +57,7 @@ for step in "$@"; do
       ctrs=${r2%%=*}
       args=""
       [[ "$r2" == *=* ]] && args=${r2#*=}
-      timeout -s KILL 240 rocprofv3 --pmc ${ctrs//,/ } -d gpurun_out/pmc_$tag -o run -- \
+      timeout -s KILL 240 rocprofv3 --pmc ${ctrs//,/ } --output-format csv -d gpurun_out/pmc_$tag -o run -- \
         python3 -u bench.py ${args//,/ } > gpurun_out/pmc_$tag.log 2>&1
       rc=$?
       echo "[$n] pmc $tag rc=$rc"
