@@ -217,21 +217,27 @@ def forest_roofline(n_rows, d, trees, forest_ms, config, world):
     """K2 (dal_forest_score, density mode).  Algorithmic bytes per launch =
     every row's features once (n*d*4) + row flag (1) + fixed-point density in
     (8) + votes (4) + fp64 score (8) + the two interval keys (16).  At T = 10
-    the kernel streams HBM; at T = 100 (config 3) the dependent LDS traversal
-    (4 levels x T trees per row) bounds it, so the HBM fraction is reported
-    with bound "lds-latency"."""
+    the kernel streams HBM; at T = 100 (config 3) the LDS traversal (4 levels
+    x T trees per row: a node read + a feature gather per level) and its
+    instruction issue bound it, so the HBM fraction is reported with bound
+    "lds-issue" (counters: profiles/r02/forest_config3_pmc.csv)."""
     if not forest_ms:
         return None
     per_row = d * 4 + 1 + 8 + 4 + 8 + 16
     nbytes = float(n_rows) * per_row
     gbs = nbytes / (forest_ms * 1e-3) / 1e9
-    return {"bound": "hbm" if trees <= 32 else "lds-latency",
-            "kernel": f"dal_forest_score (T={trees} depth-4 trees, LDS-resident SoA; "
-                      "votes -> LUT -> density-weighted interval keys)",
-            "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
-            "traffic": _traffic(config, "forest_score_bytes_per_launch", world), "launch_ms": forest_ms,
-            "algorithmic_bytes_per_launch": nbytes, "bytes_per_row": per_row,
-            "note": "timed with HIP events on the launch stream over the warm steps (density cached)"}
+    out = {"bound": "hbm" if trees <= 32 else "lds-issue",
+           "kernel": f"dal_forest_score (T={trees} depth-4 trees, LDS-resident SoA; "
+                     "votes -> LUT -> density-weighted interval keys)",
+           "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+           "traffic": _traffic(config, "forest_score_bytes_per_launch", world), "launch_ms": forest_ms,
+           "algorithmic_bytes_per_launch": nbytes, "bytes_per_row": per_row,
+           "note": "timed with HIP events on the launch stream over the warm steps (density cached)"}
+    if trees > 32:
+        out["counters"] = ("PMC per launch at config 3 (profiles/r02/forest_config3_pmc.csv): LDS array busy "
+                           "SQ_LDS_IDX_ACTIVE, 42% of it bank-conflict cycles (lane-divergent feature gathers); "
+                           "waves parked on s_waitcnt 51% / issue-stalled 22% / issuing 27% of their cycles")
+    return out
 
 
 def topk_roofline(n_rows, select_ms, config, world):

@@ -19,7 +19,7 @@ side_fn = engine._side_stream
 
 def run(n, d, trees, mode, steps=40):
     engine._side_stream = side_fn if mode == "side" else (lambda device: torch.cuda.current_stream(device))
-    x = bench.make_pool_rows(0, n, d, "uniform", dev)
+    x = bench.upload(bench.host_pool(0, n, d, "uniform"), dev)
     forest = Forest.synthetic(trees, 4, d, seed=1, dist="uniform")
     unl = torch.arange(10, n, device=dev, dtype=torch.int64)
     state = engine.PoolState(x, excluded=np.arange(10), device=dev)

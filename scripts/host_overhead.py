@@ -17,7 +17,7 @@ from dal.forest import Forest  # noqa: E402
 
 dev = torch.device("cuda:0")
 n, d = 100000, 64
-x = bench.make_pool_rows(0, n, d, "uniform", dev)
+x = bench.upload(bench.host_pool(0, n, d, "uniform"), dev)
 forest = Forest.synthetic(10, 4, d, seed=1, dist="uniform")
 unl = torch.arange(10, n, device=dev, dtype=torch.int64)
 state = engine.PoolState(x, excluded=np.arange(10), device=dev)

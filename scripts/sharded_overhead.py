@@ -13,7 +13,7 @@ import torch.distributed as dist
 REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, os.path.join(REPO, "distributed-active-learning_amd"))
 sys.path.insert(0, REPO)
-from bench import make_pool_rows  # noqa: E402
+from bench import host_pool, upload  # noqa: E402
 from dal import engine, parallel  # noqa: E402
 from dal.forest import Forest  # noqa: E402
 
@@ -24,7 +24,7 @@ dev = torch.device("cuda:0")
 torch.cuda.set_device(dev)
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
 n, d, k = 100_000, 64, 100
-x = make_pool_rows(0, n, d, "uniform", dev)
+x = upload(host_pool(0, n, d, "uniform"), dev)
 forest = Forest.synthetic(10, 4, d, seed=1)
 E = np.arange(10)
 unl = torch.arange(10, n, device=dev, dtype=torch.int64)
