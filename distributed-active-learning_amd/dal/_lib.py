@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(_HERE, "libdal.so")
 DAL_OK = 0
 DAL_FLAG_ZERO_NORM = 1
 DAL_FLAG_CAND_OVERFLOW = 2
+DAL_FLAG_RF_SPLITS = 4
 DAL_ROW_CANDIDATE = 1
 DAL_ROW_EXCLUDED = 2
 DAL_DENSITY_NONE = 0
@@ -32,6 +33,9 @@ DAL_CANON_CHUNK = 256
 DAL_MAX_TREE_DEPTH = 16
 DAL_SORT_CAP = 8192
 DAL_SORT_CAP_PAYLOAD = 4096
+DAL_RF_MAX_SPLITS = 255
+DAL_RF_MAX_SPLIT_SAMPLE = 16384
+DAL_RF_MAX_DEPTH = 10
 
 # name -> (restype, argtypes); every symbol of include/dal.h
 SIGNATURES = {
@@ -93,6 +97,12 @@ SIGNATURES = {
     "dal_sort_pairs": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
                                c_void_p, c_void_p]),
     "dal_gram_entries": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p]),
+    "dal_rf_find_splits": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64, c_int32, c_void_p,
+                                   c_void_p, c_void_p, c_void_p]),
+    "dal_rf_train_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int32, c_int32, c_int32, c_int32]),
+    "dal_rf_train": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_int32,
+                             c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_double, c_void_p,
+                             c_void_p, c_void_p, c_size_t, c_void_p]),
 }
 
 _lib = None

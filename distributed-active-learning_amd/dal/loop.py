@@ -14,9 +14,11 @@ GPU query step:
   log        ``labeled =  L  unlabeled =  U`` (:65) and
              ``Iteration  i  -- accu =  a`` (:113)
 
-Forest training stays on the CPU (scikit-learn, MLlib's defaults:
-max_depth=4, sqrt features, bootstrap, gini); the selection step is the GPU
-path (dal.uncertainty_sampling / dal.density_weighting).  The random baseline
+Forest training (RandomForest.trainClassifier, uncertainty_sampling.py:71-76)
+runs on the GPU by default (dal.random_forest: MLlib 2.1's gini / maxDepth 4 /
+maxBins 32 / sqrt-feature algorithm, seeded bagging draws); trainer="sklearn"
+keeps the scikit-learn fit of round 1.  The selection step is the GPU path
+(dal.uncertainty_sampling / dal.density_weighting).  The random baseline
 (random_sampling.py:88-89, ``sortBy(np.random.uniform).take``) has no
 arithmetic and runs on the host.
 """
@@ -39,9 +41,36 @@ def load_labeled_text(path: str, n_samples=None, label_map: str = "reference"):
     return parse_labeled_text(path, n_samples=n_samples, label_map=label_map)
 
 
-def train_forest(X, y, n_estimators: int = 10, seed: int = 0, max_depth: int = 4):
+class GpuForestModel:
+    """A forest trained by dal.random_forest, with MLlib's RandomForestModel
+    ``predict`` (majority vote) on the GPU."""
+
+    def __init__(self, forest, device=None):
+        self.forest = forest
+        self.device = device
+
+    def predict(self, X):
+        from .random_forest import predict
+
+        labels, _ = predict(self.forest, X, device=self.device)
+        return labels.cpu().numpy()
+
+
+def train_forest(X, y, n_estimators: int = 10, seed: int = 0, max_depth: int = 4, trainer="gpu",
+                 device=None):
     """RandomForest.trainClassifier(numTrees=T, featureSubsetStrategy='auto',
-    impurity='gini') with MLlib's default maxDepth=4, via scikit-learn."""
+    impurity='gini') with MLlib's default maxDepth=4.  trainer: "gpu"
+    (dal.random_forest), "sklearn", or a callable (X, y, T, seed) -> model with
+    ``predict``."""
+    if callable(trainer):
+        return trainer(X, y, n_estimators, seed)
+    if trainer == "gpu":
+        from .random_forest import train_classifier
+
+        return GpuForestModel(train_classifier(X, y, n_estimators, max_depth=max_depth, seed=seed,
+                                               device=device), device)
+    if trainer != "sklearn":
+        raise ValueError(f"unknown trainer {trainer!r}")
     from sklearn.ensemble import RandomForestClassifier
 
     rf = RandomForestClassifier(n_estimators=n_estimators, max_depth=max_depth,
@@ -60,12 +89,13 @@ class LoopResult:
 def run_loop(X, y, X_test=None, y_test=None, strategy: str = "uncertainty",
              window_size: int = 10, n_estimators: int = 10, max_iterations=None,
              seed: int = 0, select_fn=None, device=None, beta: float = 1.0,
-             verbose: bool = False) -> LoopResult:
+             verbose: bool = False, trainer="gpu") -> LoopResult:
     """Run the AL loop.  strategy: "uncertainty" (uncertainty_sampling.py),
     "density" (density_weighting.py, E = L0 = range(window_size)) or "random".
+    trainer: see train_forest.
 
-    ``select_fn(strategy, pool, unlabeled, forest_sklearn, k) -> indices`` can
-    replace the GPU step (tests use the oracle); by default the dal GPU path runs.
+    ``select_fn(strategy, pool, unlabeled, model, k) -> indices`` can replace
+    the GPU step (tests use the oracle); by default the dal GPU path runs.
     """
     from .forest import Forest
 
@@ -74,7 +104,7 @@ def run_loop(X, y, X_test=None, y_test=None, strategy: str = "uncertainty",
     unlabeled = np.arange(len(labeled), n, dtype=np.int64)
     res = LoopResult()
     rng = np.random.default_rng(seed)
-    state = None
+    state = test_state = None
     if select_fn is None and strategy != "random":
         from .engine import PoolState
 
@@ -91,10 +121,14 @@ def run_loop(X, y, X_test=None, y_test=None, strategy: str = "uncertainty",
         if max_iterations is not None and it > max_iterations:
             break
         lab = np.asarray(labeled)
-        rf = train_forest(X[lab], y[lab], n_estimators, seed + it)
+        rf = train_forest(X[lab], y[lab], n_estimators, seed + it, trainer=trainer, device=device)
         acc = None
         if X_test is not None:
-            pred = rf.predict(X_test)
+            if isinstance(rf, GpuForestModel) and test_state is None:
+                from .engine import PoolState
+
+                test_state = PoolState(X_test, device=device)  # uploaded once
+            pred = rf.predict(test_state if isinstance(rf, GpuForestModel) else X_test)
             acc = (1 - np.mean(pred != y_test)) * 100
         k = min(window_size, unlabeled.size)
         if strategy == "random":
@@ -103,7 +137,7 @@ def run_loop(X, y, X_test=None, y_test=None, strategy: str = "uncertainty",
         elif select_fn is not None:
             chosen = np.asarray(select_fn(strategy, X, unlabeled, rf, k))
         else:
-            forest = Forest.from_sklearn(rf)
+            forest = rf.forest if isinstance(rf, GpuForestModel) else Forest.from_sklearn(rf)
             if strategy == "uncertainty":
                 from .uncertainty_sampling import select
                 sel = select(state, unlabeled, forest, k)

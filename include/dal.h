@@ -54,6 +54,7 @@ enum dal_status {
 /* bits OR-ed into *dev_status by kernels */
 #define DAL_FLAG_ZERO_NORM 1      /* a pool row has ||x|| == 0 (cosine undefined) */
 #define DAL_FLAG_CAND_OVERFLOW 2  /* re-rank candidate set exceeded capacity */
+#define DAL_FLAG_RF_SPLITS 4      /* a feature produced more than num_splits + 1 thresholds */
 
 /* per-row flags (uint8 per pool row) */
 #define DAL_ROW_CANDIDATE 1 /* row is in the unlabeled set and may be selected */
@@ -74,6 +75,9 @@ enum dal_status {
 #define DAL_MAX_TREE_DEPTH 16
 #define DAL_SORT_CAP 8192          /* max pairs the single-block sort handles */
 #define DAL_SORT_CAP_PAYLOAD 4096  /* ... when it also carries an fp64 payload */
+#define DAL_RF_MAX_SPLITS 255          /* thresholds per feature (bins fit a uint8) */
+#define DAL_RF_MAX_SPLIT_SAMPLE 16384  /* rows one threshold search sorts in LDS */
+#define DAL_RF_MAX_DEPTH 10            /* deepest tree dal_rf_train grows */
 
 const char* dal_status_string(int status);
 int dal_abi_version(void);
@@ -316,6 +320,41 @@ int dal_sort_pairs(const uint64_t* keys, const int64_t* idx, const double* paylo
 int dal_text_shape(const char* text, size_t len, int64_t max_rows, int64_t* rows, int64_t* cols);
 int dal_parse_labeled_text(const char* text, size_t len, int64_t rows, int64_t cols, int label_map, float* x,
                            int64_t* labels, int n_threads);
+
+/* ---- GPU random-forest training ---------------------
+ * Replaces RandomForest.trainClassifier(train, numClasses=2,
+ * categoricalFeaturesInfo={}, numTrees=T, featureSubsetStrategy="auto",
+ * impurity='gini', maxDepth=4, maxBins=32) (uncertainty_sampling.py:71-76,
+ * density_weighting.py:119-124; Spark 2.1 MLlib, continuous features, binary
+ * labels).  The training rows x [n][ldx] fp32 are the labeled set.
+ *
+ * dal_rf_find_splits: findSplitsForContinuousFeature per feature over the
+ * sample rows (sample_rows nullable = rows 0..n_sample-1; n_sample <=
+ * DAL_RF_MAX_SPLIT_SAMPLE): thresholds [d][DAL_RF_MAX_SPLITS] fp32 (ascending),
+ * n_splits [d].  num_splits = min(maxBins, n) - 1.  A feature that would emit
+ * more than num_splits + 1 thresholds sets DAL_FLAG_RF_SPLITS in *dev_status.
+ *
+ * dal_rf_train: grows T trees level by level on the given bagging weights
+ * [T][n] (integer Poisson counts; 0 = row not drawn) and per-node feature
+ * subsets [T][2^max_depth - 1][m] (heap order, evaluation order; MLlib draws
+ * both from JVM RNGs, so they are inputs).  Gini gain in fp64 in MLlib's
+ * operation order, first maximum over subset order then split index; a node
+ * is a leaf when gain <= 0 (or no valid split) or at max_depth; a child is
+ * created as a leaf when pure.  Output in dal_forest_score's heap layout:
+ * out_inner [T][2^D - 1][2] = (feature, fp32 threshold bits), (0, +inf) below
+ * a leaf; out_leaf [T][2^D] = class (first maximum of the weighted counts),
+ * a shallow leaf's class repeated over its subtree.  ws: 256-B aligned,
+ * dal_rf_train_workspace_bytes(...) bytes. */
+int dal_rf_find_splits(const float* x, int64_t n, int64_t d, int64_t ldx, const int64_t* sample_rows,
+                       int64_t n_sample, int32_t num_splits, float* thresholds, int32_t* n_splits,
+                       int32_t* dev_status, dal_stream_t stream);
+size_t dal_rf_train_workspace_bytes(int64_t n, int64_t d, int32_t n_trees, int32_t max_depth, int32_t m,
+                                    int32_t num_splits);
+int dal_rf_train(const float* x, int64_t n, int64_t d, int64_t ldx, const uint8_t* labels,
+                 const float* thresholds, const int32_t* n_splits, int32_t num_splits, const int32_t* weights,
+                 const int32_t* feature_subsets, int32_t m, int32_t n_trees, int32_t max_depth,
+                 int32_t min_instances, double min_info_gain, int32_t* out_inner, uint8_t* out_leaf, void* ws,
+                 size_t ws_bytes, dal_stream_t stream);
 
 /* ---- standalone similarity kernels --------------------------------------
  * cosine_similarity.py:42-45: every entry of U.U^T (fp32 MFMA), written to

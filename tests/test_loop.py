@@ -32,7 +32,7 @@ def test_loop_runs_to_exhaustion_with_reference_log(strategy):
     g = load_golden("checkerboard2x2.npz")
     X, y = g["X"][:120], g["y"][:120]
     res = loop.run_loop(X, y, X, y, strategy=strategy, window_size=10,
-                        select_fn=oracle_select)
+                        select_fn=oracle_select, trainer="sklearn")
     assert res.log[0] == "labeled =  10  unlabeled =  110"
     assert res.log[-1] == "labeled =  120  unlabeled =  0"
     assert res.log[2].startswith("labeled =  20")
