@@ -17,6 +17,25 @@
 //                    lower index.
 //   sort             one 1024-thread block, bitonic on (key, index) in LDS.
 // HBM-bound: each pass reads 8 B/row.
+//
+// Truncated level 1 of the interval selections (dal_dw_select with
+// level1_passes = p in 1..5; small pools, where the 6 dependent radix
+// launches and the 3-launch ordered compaction are latency, not bytes):
+//   p x radix_hist   the first p digits of the k-th smallest pessimistic key
+//                    K: K lies in the resolved bucket, so tau = the bucket's
+//                    upper edge (prefix | all-ones below) satisfies tau >= K
+//                    and >= k pessimistic keys are <= tau;
+//   threshold_append every row whose OPTIMISTIC key is <= tau joins the
+//                    candidates (ballot + one atomic per wave; order does not
+//                    matter: the candidates are sorted by (exact key, row)).
+// {optimistic <= tau} contains {optimistic <= K}, the exact path's candidate
+// set, so the selection is the same; 2 digits resolve a DW score to ~2^-11
+// relative, about the width of its density interval, so the candidate set
+// stays small.  More than cap candidates raises DAL_FLAG_SAMPLE_MISS (the
+// caller re-runs with level1_passes = 0).
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace dal {
@@ -371,6 +390,48 @@ __global__ __launch_bounds__(kRadixThreads) void compact_write_kernel(
   }
 }
 
+// ---------------------------------------------------- truncated level 1 ----
+__global__ __launch_bounds__(kRadixThreads) void threshold_append_kernel(
+    const uint64_t* __restrict__ keys_lo, const uint64_t* __restrict__ keys_hi, int64_t n, int64_t idx_base,
+    int passes, TopkHdr* __restrict__ h, int64_t* __restrict__ cidx, int64_t cap) {
+  __shared__ uint32_t scan[kRadixThreads / 64];
+  __shared__ unsigned long long red[kRadixThreads / 64];
+  unsigned long long prefix, krem;
+  resolve_digit(h, passes - 1, prefix, krem, scan);
+  const int sh = digit_shift(passes - 1);
+  const unsigned long long tau = prefix | (sh ? ((1ull << sh) - 1ull) : 0ull);
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (blockIdx.x == 0 && tid == 0) h->kstar = tau;
+  unsigned long long below = 0;
+  for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * kRadixThreads; i0 < n;
+       i0 += static_cast<int64_t>(gridDim.x) * kRadixThreads) {
+    const int64_t i = i0 + tid;
+    bool cand = false;
+    if (i < n) {
+      below += keys_lo[i] <= tau;
+      const unsigned long long hi = keys_hi[i];
+      cand = hi <= tau && hi != DAL_KEY_NONE;
+    }
+    const unsigned long long m = __ballot(cand);
+    if (!m) continue;
+    unsigned int base = 0;
+    if (lane == 0) base = atomicAdd(&h->cand_count, static_cast<unsigned int>(__popcll(m)));
+    base = __shfl(base, 0);
+    if (cand) {
+      const int64_t pos = base + __popcll(m & ((1ull << lane) - 1ull));
+      if (pos < cap) cidx[pos] = idx_base + i;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) below += __shfl_xor(below, o);
+  if (lane == 0) red[tid >> 6] = below;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kRadixThreads / 64; ++w) t += red[w];
+    atomicAdd(&h->total_lt, t);
+  }
+}
+
 // ------------------------------------------------------------- re-rank ----
 // Canonical fp64 density-weighted score of each candidate (bit-identical to
 // oracle.density_canonical: x/norm, then sequential mul+add over features;
@@ -384,8 +445,11 @@ __global__ __launch_bounds__(256) void rerank_kernel(const TopkHdr* __restrict__
                                                      const uint8_t* __restrict__ flags, double beta,
                                                      uint64_t* __restrict__ ckey,
                                                      const int64_t* __restrict__ cidx,
-                                                     double* __restrict__ cpay, int64_t cap) {
+                                                     double* __restrict__ cpay, int64_t cap,
+                                                     int64_t need_k, int32_t* __restrict__ status) {
   const int64_t c = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (need_k && c == 0 && (h->total_lt < static_cast<unsigned long long>(need_k) || h->cand_count > cap))
+    atomicOr(status, DAL_FLAG_SAMPLE_MISS);  // truncated level 1 over capacity: the caller re-runs exactly
   if (c >= cap) return;
   if (c >= h->cand_count) {
     ckey[c] = DAL_KEY_NONE;
@@ -616,14 +680,35 @@ __global__ __launch_bounds__(kSortThreads) void sort_kernel(const uint64_t* __re
     out_idx[i] = si[i];
     if (PAY && out_pay) out_pay[i] = sp[i];
   }
+  // candidate lists (h != null) shorter than k -- a shard with fewer than k
+  // unlabeled rows under the sampled level 1 -- are padded with the NONE key
+  if (PAY && h) {
+    for (int64_t i = kk + tid; i < k; i += kSortThreads) {
+      if (out_keys) out_keys[i] = DAL_KEY_NONE;
+      out_idx[i] = -1;
+      if (out_pay) out_pay[i] = __builtin_nan("");
+    }
+  }
 }
 
-int run_radix(const uint64_t* keys, int64_t n, int64_t k, TopkHdr* h, hipStream_t st) {
-  if (hipMemsetAsync(h, 0, sizeof(TopkHdr), st) != hipSuccess) return DAL_ERR_HIP;
+// Zero the header with a kernel rather than hipMemsetAsync: the select is
+// replayed inside hipGraphs (engine.WarmStepGraph), where a captured memset
+// node did not clear the header on every replay (observed on gfx950 / ROCm 7).
+__global__ __launch_bounds__(256) void zero_words_kernel(uint32_t* __restrict__ p, int64_t words) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < words;
+       i += static_cast<int64_t>(gridDim.x) * 256)
+    p[i] = 0u;
+}
+
+int run_radix(const uint64_t* keys, int64_t n, int64_t k, TopkHdr* h, hipStream_t st, int passes = kPasses) {
+  static_assert(sizeof(TopkHdr) % 4 == 0, "header is whole words");
+  const int64_t words = sizeof(TopkHdr) / 4;
+  hipLaunchKernelGGL(zero_words_kernel, dim3(static_cast<unsigned>(ceil_div(words, 256 * 4))), dim3(256), 0, st,
+                     reinterpret_cast<uint32_t*>(h), words);
   int64_t blocks = ceil_div(n, kRadixThreads * 8);
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
-  for (int p = 0; p < kPasses; ++p) {
+  for (int p = 0; p < passes; ++p) {
     hipLaunchKernelGGL(radix_hist_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kRadixThreads), 0,
                        st, keys, n, k, p, h);
   }
@@ -687,10 +772,11 @@ static size_t rerank_ws_bytes(int64_t n, int64_t k, int64_t cap) {
 
 template <class Rerank>
 static int select_with_rerank(const uint64_t* keys_lo, const uint64_t* keys_hi, int64_t n, int64_t k,
-                              int64_t idx_base, int64_t cap, void* ws, size_t ws_bytes, Rerank rerank,
-                              int64_t* out_idx, double* out_scores, uint64_t* out_keys, int32_t* dev_status,
-                              hipStream_t st) {
+                              int64_t idx_base, int64_t cap, int passes, void* ws, size_t ws_bytes,
+                              Rerank rerank, int64_t* out_idx, double* out_scores, uint64_t* out_keys,
+                              int32_t* dev_status, hipStream_t st) {
   if (n < 1 || k < 1 || k > n || cap < k) return DAL_ERR_SHAPE;
+  if (passes < 0 || passes >= kPasses || (passes > 0 && cap > DAL_SORT_CAP_PAYLOAD)) return DAL_ERR_ARG;
   if (k > DAL_SORT_CAP) return DAL_ERR_CAPACITY;
   const TopkLayout L1 = topk_layout(n, cap), L2 = topk_layout(cap, k);
   if (ws_bytes < rerank_ws_bytes(n, k, cap) || (reinterpret_cast<uintptr_t>(ws) & 255)) return DAL_ERR_SHAPE;
@@ -702,11 +788,23 @@ static int select_with_rerank(const uint64_t* keys_lo, const uint64_t* keys_hi, 
   uint64_t* ckey = reinterpret_cast<uint64_t*>(base + L1.ckey);
   int64_t* cidx = reinterpret_cast<int64_t*>(base + L1.cidx);
   double* cpay = reinterpret_cast<double*>(base + L1.cpay);
-  int rc = run_radix(keys_lo, n, k, h1, st);
-  if (rc) return rc;
-  rc = run_compact<true>(keys_lo, IntervalArgs{keys_hi}, n, idx_base, k, ws, L1, dev_status, st);
-  if (rc) return rc;
-  rerank(h1, ckey, cidx, cpay, cap);  // canonical keys for every slot (NONE past the count)
+  int rc = DAL_OK;
+  if (passes > 0) {
+    rc = run_radix(keys_lo, n, k, h1, st, passes);
+    if (rc) return rc;
+    const int64_t blocks = std::min<int64_t>(ceil_div(n, kRadixThreads * 4), 1024);
+    hipLaunchKernelGGL(threshold_append_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kRadixThreads), 0, st,
+                       keys_lo, keys_hi, n, idx_base, passes, h1, cidx, cap);
+    DAL_RETURN_IF_LAUNCH_FAILED();
+  } else {
+    rc = run_radix(keys_lo, n, k, h1, st);
+    if (rc) return rc;
+    rc = run_compact<true>(keys_lo, IntervalArgs{keys_hi}, n, idx_base, k, ws, L1, dev_status, st);
+    if (rc) return rc;
+  }
+  // canonical keys for every slot (NONE past the count); with a truncated
+  // level 1 the re-rank also checks the candidate capacity (need_k = k)
+  rerank(h1, ckey, cidx, cpay, cap, passes > 0 ? k : 0);
   if (cap <= DAL_SORT_CAP_PAYLOAD) {
     // level 2 fits one block: sort the cand_count candidates (row order, so
     // ties resolve by index) by canonical key with their scores, take k
@@ -736,25 +834,26 @@ extern "C" size_t dal_dw_select_workspace_bytes(int64_t n, int64_t k, int64_t ca
 extern "C" int dal_dw_select(const uint64_t* keys_lo, const uint64_t* keys_hi, const int32_t* votes,
                              const uint8_t* row_flags, int64_t n, int64_t k, int64_t idx_base,
                              const double* lut, double beta, const float* x, int64_t d, int64_t ldx,
-                             const double* norm64, const double* colsum, int64_t cap, void* ws,
-                             size_t ws_bytes, int64_t* out_idx, double* out_scores, uint64_t* out_keys,
-                             int32_t* dev_status, dal_event_t colsum_ready, dal_stream_t stream) {
+                             const double* norm64, const double* colsum, int64_t cap, int32_t level1_passes,
+                             void* ws, size_t ws_bytes, int64_t* out_idx, double* out_scores,
+                             uint64_t* out_keys, int32_t* dev_status, dal_event_t colsum_ready,
+                             dal_stream_t stream) {
   if (!keys_lo || !keys_hi || !votes || !lut || !x || !norm64 || !colsum || !ws || !out_idx ||
       !out_scores || !dev_status)
     return DAL_ERR_ARG;
   if (d < 1 || ldx < d) return DAL_ERR_SHAPE;
   hipStream_t st = as_stream(stream);
   bool wait_failed = false;
-  auto rerank = [&](TopkHdr* h, uint64_t* ckey, int64_t* cidx, double* cpay, int64_t cp) {
+  auto rerank = [&](TopkHdr* h, uint64_t* ckey, int64_t* cidx, double* cpay, int64_t cp, int64_t need_k) {
     // the only consumer of colsum: join its producer stream here, not before the call
     if (colsum_ready && hipStreamWaitEvent(st, reinterpret_cast<hipEvent_t>(colsum_ready), 0) != hipSuccess)
       wait_failed = true;
     hipLaunchKernelGGL(rerank_kernel, dim3(static_cast<unsigned>(ceil_div(cp, 256))), dim3(256), 0, st, h,
                        idx_base, x, static_cast<int>(d), ldx, norm64, colsum, lut, votes, row_flags, beta,
-                       ckey, cidx, cpay, cp);
+                       ckey, cidx, cpay, cp, need_k, dev_status);
   };
-  const int rc = select_with_rerank(keys_lo, keys_hi, n, k, idx_base, cap, ws, ws_bytes, rerank, out_idx,
-                                    out_scores, out_keys, dev_status, st);
+  const int rc = select_with_rerank(keys_lo, keys_hi, n, k, idx_base, cap, level1_passes, ws, ws_bytes, rerank,
+                                    out_idx, out_scores, out_keys, dev_status, st);
   return rc ? rc : (wait_failed ? DAL_ERR_HIP : DAL_OK);
 }
 
@@ -771,11 +870,11 @@ extern "C" int dal_maxcos_select(const uint64_t* keys_lo, const uint64_t* keys_h
     return DAL_ERR_ARG;
   if (d < 1 || d > 256 || ld < d || m < 1) return DAL_ERR_SHAPE;
   hipStream_t st = as_stream(stream);
-  auto rerank = [&](TopkHdr* h, uint64_t* ckey, int64_t* cidx, double* cpay, int64_t cp) {
+  auto rerank = [&](TopkHdr* h, uint64_t* ckey, int64_t* cidx, double* cpay, int64_t cp, int64_t) {
     hipLaunchKernelGGL(rerank_maxcos_kernel, dim3(static_cast<unsigned>(ceil_div(cp, kRrC))), dim3(256), 0, st,
                        h, idx_base, pool, static_cast<int>(d), ld, ulab, m, ckey, cidx, cpay, cp);
   };
-  return select_with_rerank(keys_lo, keys_hi, n, k, idx_base, cap, ws, ws_bytes, rerank, out_idx, out_scores,
+  return select_with_rerank(keys_lo, keys_hi, n, k, idx_base, cap, 0, ws, ws_bytes, rerank, out_idx, out_scores,
                             out_keys, dev_status, st);
 }
 

@@ -18,6 +18,7 @@ DAL_OK = 0
 DAL_FLAG_ZERO_NORM = 1
 DAL_FLAG_CAND_OVERFLOW = 2
 DAL_FLAG_RF_SPLITS = 4
+DAL_FLAG_SAMPLE_MISS = 8
 DAL_ROW_CANDIDATE = 1
 DAL_ROW_EXCLUDED = 2
 DAL_DENSITY_NONE = 0
@@ -75,7 +76,7 @@ SIGNATURES = {
     "dal_dw_select_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
     "dal_dw_select": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64,
                               c_void_p, c_double, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
-                              c_int64, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
+                              c_int64, c_int32, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_void_p]),
     "dal_maxcos_label_rows_granule": (c_int64, [c_int64]),
     "dal_maxcos_error_bound": (c_double, [c_int64]),

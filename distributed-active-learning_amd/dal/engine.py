@@ -12,12 +12,16 @@ Reference loop body being replaced (one ``while True`` iteration):
 from __future__ import annotations
 
 
+import os
+import weakref
+
 import numpy as np
 
 from . import _lib
 from ._lib import (DAL_ASCENDING, DAL_CANON_CHUNK, DAL_DENSITY_EXACT, DAL_DENSITY_FIXED,
                    DAL_DENSITY_NONE, DAL_DESCENDING, DAL_FIXED_SCALE, DAL_FLAG_CAND_OVERFLOW,
-                   DAL_FLAG_ZERO_NORM, DAL_ROW_CANDIDATE, DAL_ROW_EXCLUDED, call)
+                   DAL_FLAG_SAMPLE_MISS, DAL_FLAG_ZERO_NORM, DAL_ROW_CANDIDATE, DAL_ROW_EXCLUDED,
+                   DAL_SORT_CAP_PAYLOAD, call)
 from .forest import Forest
 from .luts import ASCENDING, lut as make_lut
 
@@ -81,6 +85,12 @@ class Selection:
         self._votes = self._gathered(self._votes)
         return self._votes
 
+    def _detach(self):
+        """Materialise the per-row arrays now (their source buffers are about
+        to be reused: a warm-step graph replay)."""
+        self._scores = self._gathered(self._scores)
+        self._votes = self._gathered(self._votes)
+
     def __iter__(self):
         """Unpacks as the reference-shaped triple (scores, indices, selected_scores)."""
         return iter((self.scores, self.indices, self.selected_scores))
@@ -142,12 +152,16 @@ class PoolState:
         self.select_events = None  # list -> (start, end) HIP events around each dal_dw_select call
         self.cap_scale = 1  # re-rank candidate capacity multiplier, kept after an overflow
         self.cap_base = None  # initial re-rank capacity override (tests: force the overflow path)
+        self.level1_fast = True  # truncated top-k level 1 allowed (cleared after an overflow on this pool)
+        self.use_graphs = os.environ.get("DAL_GRAPHS", "1") != "0"  # hipGraph replay of warm steps
+        self._graphs = {}  # warm-step graphs by (T, depth, k, beta, cap, level-1 passes)
         self.last_status = 0     # status word read by the last synchronising select
 
     def clear_caches(self):
         """Drop normalised rows, density and column sums (forces a cold step)."""
         self._u = self._norm64 = self._density = self._colsum = self._colsum_partials = None
         self._split = self._density_exact = None
+        self._graphs = {}
 
     # ------------------------------------------------------------- caches
     def set_excluded(self, excluded):
@@ -169,6 +183,7 @@ class PoolState:
             self.flags[torch.from_numpy(local).to(self.device)] = DAL_ROW_EXCLUDED
         self._u = self._norm64 = self._density = self._colsum = self._colsum_partials = None
         self._split = self._density_exact = None
+        self._graphs = {}
 
     def n_excluded_global(self) -> int:
         return int(self.excluded.size)
@@ -315,6 +330,10 @@ class PoolState:
             self.gram_events.append(ev)
         return acc
 
+    def events_off(self) -> bool:
+        """No per-launch HIP-event timing requested (the graph path has none)."""
+        return self.forest_events is None and self.select_events is None and self.gram_events is None
+
     def set_density_fixed(self, acc):
         self._density = acc
 
@@ -374,6 +393,8 @@ class PoolState:
                              "(the reference would propagate NaN into every density)")
         if st & DAL_FLAG_CAND_OVERFLOW:
             raise _lib.DalError("density re-rank candidate set exceeded DAL_SORT_CAP_PAYLOAD")
+        if st & DAL_FLAG_SAMPLE_MISS:
+            raise _lib.DalError("truncated top-k level 1 overflowed and was not re-run")
 
 
 GRAM_KINDS = ("sym", "split", "f32")
@@ -496,6 +517,18 @@ def candidate_cap(n: int, k: int) -> int:
     return int(min(n, max(4 * k, _lib.DAL_SORT_CAP_PAYLOAD)))
 
 
+# Truncated level 1 of dal_dw_select: 2 radix digits resolve the k-th
+# pessimistic key's bucket, whose upper edge bounds the candidate search
+# (3 launches instead of 9).  DAL_LEVEL1_PASSES overrides (0 = exact radix).
+LEVEL1_PASSES = int(os.environ.get("DAL_LEVEL1_PASSES", "2"))
+
+
+def level1_passes(state, n: int, k: int, cap: int) -> int:
+    if not state.level1_fast or cap > DAL_SORT_CAP_PAYLOAD:
+        return 0
+    return LEVEL1_PASSES
+
+
 def workspace(nbytes: int, device):
     """A 256-byte aligned device workspace: (tensor, aligned pointer)."""
     torch = _torch()
@@ -520,6 +553,7 @@ def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k
     base = candidate_cap(n, k) if state.cap_base is None else max(int(k), int(state.cap_base))
     cap = int(min(n, base * cap_scale))
     while True:
+        passes = level1_passes(state, n, k, cap)
         wsb = int(lib.dal_dw_select_workspace_bytes(n, k, cap))
         ws, wsp = workspace(wsb, state.device)
         out_idx = torch.empty(k, dtype=torch.int64, device=state.device)
@@ -531,7 +565,7 @@ def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k
             ev[0].record()
         call("dal_dw_select", _ptr(keys_lo), _ptr(keys_hi), _ptr(votes), _ptr(flags), n, k,
              state.row_base, _ptr(lut_dev), float(beta), _ptr(state.x), state.d, state.d,
-             _ptr(norm64), _ptr(colsum), cap, wsp, wsb, _ptr(out_idx), _ptr(out_scores),
+             _ptr(norm64), _ptr(colsum), cap, passes, wsp, wsb, _ptr(out_idx), _ptr(out_scores),
              _ptr(out_keys), _ptr(state.status),
              0 if colsum_ready is None else colsum_ready.cuda_event, _stream(state.device))
         if ev is not None:
@@ -542,6 +576,10 @@ def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k
         # the step's one host sync: status word (zero-norm rows, candidate overflow)
         st = int(state.status.item())
         state.last_status = st
+        if st & DAL_FLAG_SAMPLE_MISS:  # truncated level 1 over capacity: exact level 1 from now on
+            state.status.bitwise_and_(~(DAL_FLAG_SAMPLE_MISS | DAL_FLAG_CAND_OVERFLOW))
+            state.level1_fast = False
+            continue
         if cap >= n or not (st & DAL_FLAG_CAND_OVERFLOW):
             return out_idx, out_scores, out_keys
         state.status.bitwise_and_(~DAL_FLAG_CAND_OVERFLOW)
@@ -596,6 +634,9 @@ def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: 
     unl = _as_index(unlabeled_idx, state.device)
     if int(unl.shape[0]) == 0:
         raise ValueError("unlabeled set is empty (the reference loop breaks here)")
+    if (state.use_graphs and density_fixed is None and state._density is not None and state._colsum is not None
+            and state.row_base == 0 and state.n == state.n_total and state.events_off()):
+        return _density_step_graph(state, unl, forest, min(int(k), int(unl.shape[0])), beta)
     # the density GEMM goes to the GPU first; the host prepares the rest while it runs
     colsum_ready = None
     if density_fixed is None and state._density is None and state._colsum is None and state.n:
@@ -627,6 +668,114 @@ def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: 
                                          state.colsum(), colsum_ready=colsum_ready)
     state.check_status(state.last_status)  # the word dw_select_local read (no second sync)
     return Selection(scores=(scores, loc), indices=idx, selected_scores=sel_scores, votes=(votes, loc))
+
+
+class WarmStepGraph:
+    """hipGraph of one warm density-weighted step (density cached -- the
+    reference's per-iteration path, density_weighting.py:133-176): forest
+    votes + score + interval keys, the candidate search, the exact fp64
+    re-rank and the final sort replay as ONE graph launch instead of ~7
+    (truncated level 1) to ~14 (exact) kernel launches from Python.  Inputs are static
+    device buffers refreshed before each replay: the forest's heap arrays
+    (copied when a different forest comes in) and the row flags (the pool's
+    base flags + the unlabeled set, marked each step)."""
+
+    def __init__(self, state: PoolState, forest: Forest, k: int, beta: float, cap: int, passes: int):
+        torch = _torch()
+        dev = state.device
+        n = state.n
+        self.state, self.k, self.cap, self.passes = state, int(k), int(cap), int(passes)
+        inner, leaf = forest.device(dev)
+        self.inner, self.leaf = inner.clone(), leaf.clone()
+        self.forest_ref = forest
+        self.n_trees, self.depth = forest.n_trees, forest.depth
+        self.flags = state.flags.clone()
+        self.lut = device_lut("entropy", forest.n_trees, dev)
+        self.votes = torch.empty(n, dtype=torch.int32, device=dev)
+        self.scores = torch.empty(n, dtype=torch.float64, device=dev)
+        self.keys_lo = torch.empty(n, dtype=torch.int64, device=dev)
+        self.keys_hi = torch.empty(n, dtype=torch.int64, device=dev)
+        # selected indices and scores side by side: one copy hands them out
+        self.out_pair = torch.empty(2 * k, dtype=torch.int64, device=dev)
+        self.out_idx = self.out_pair[:k]
+        self.out_scores = self.out_pair[k:].view(torch.float64)
+        self.out_keys = torch.empty(k, dtype=torch.int64, device=dev)
+        self._last = None  # weak reference to the Selection that still reads votes / scores
+        lib = _lib.load()
+        self.wsb = int(lib.dal_dw_select_workspace_bytes(n, k, cap))
+        self.ws, self.wsp = workspace(self.wsb, dev)
+        dens, colsum, norm64 = state.density_fixed(), state.colsum(), state.norms()
+        derr = density_error(state)
+        self.graph = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.graph(self.graph, stream=side, capture_error_mode="relaxed"):
+            st = _stream(dev)
+            state.status.zero_()
+            call("dal_forest_score", _ptr(state.x), n, state.d, state.d, _ptr(self.inner), _ptr(self.leaf),
+                 self.n_trees, self.depth, _ptr(self.lut), _ptr(dens), DAL_DENSITY_FIXED, float(derr),
+                 _ptr(self.flags), float(beta), DAL_DESCENDING, _ptr(self.votes), _ptr(self.scores),
+                 _ptr(self.keys_lo), _ptr(self.keys_hi), st)
+            call("dal_dw_select", _ptr(self.keys_lo), _ptr(self.keys_hi), _ptr(self.votes), _ptr(self.flags),
+                 n, k, state.row_base, _ptr(self.lut), float(beta), _ptr(state.x), state.d, state.d,
+                 _ptr(norm64), _ptr(colsum), cap, passes, self.wsp, self.wsb, _ptr(self.out_idx),
+                 _ptr(self.out_scores), _ptr(self.out_keys), _ptr(state.status), 0, st)
+        torch.cuda.current_stream(dev).wait_stream(side)
+
+    def run(self, forest: Forest, unl):
+        """Refresh the inputs and replay; returns (votes, scores) -- the
+        graph's buffers, valid until the next replay (copy-on-write: the
+        previous step's Selection is materialised before they are reused) --
+        and a copy of (selected indices, selected scores)."""
+        prev = self._last() if self._last is not None else None
+        if prev is not None:
+            prev._detach()
+        if forest is not self.forest_ref:
+            inner, leaf = forest.device(self.state.device)
+            self.inner.copy_(inner)
+            self.leaf.copy_(leaf)
+            self.forest_ref = forest
+        self.flags.copy_(self.state.flags)
+        call("dal_mark_rows", _ptr(unl), int(unl.shape[0]), self.state.row_base, self.state.n,
+             DAL_ROW_CANDIDATE, _ptr(self.flags), _stream(self.state.device))
+        self.graph.replay()
+        pair = self.out_pair.clone()
+        return self.votes, self.scores, pair[:self.k], pair[self.k:].view(torch_float64())
+
+
+def _density_step_graph(state: PoolState, unl, forest: Forest, kk: int, beta: float) -> Selection:
+    """Warm density step through a cached WarmStepGraph (same selection as
+    the eager path; a level-1 or re-rank capacity overflow rebuilds the graph
+    with the exact level 1 / a larger capacity and replays)."""
+    n = state.n
+    loc = state.local_positions(unl)
+    while True:
+        base = candidate_cap(n, kk) if state.cap_base is None else max(int(kk), int(state.cap_base))
+        cap = int(min(n, base * state.cap_scale))
+        passes = level1_passes(state, n, kk, cap)
+        key = (forest.n_trees, forest.depth, kk, float(beta), cap, passes)
+        g = state._graphs.get(key)
+        if g is None:
+            g = state._graphs[key] = WarmStepGraph(state, forest, kk, beta, cap, passes)
+        votes, scores, idx, sel_scores = g.run(forest, unl)
+        st = int(state.status.item())
+        state.last_status = st
+        if st & DAL_FLAG_SAMPLE_MISS:
+            state.status.bitwise_and_(~(DAL_FLAG_SAMPLE_MISS | DAL_FLAG_CAND_OVERFLOW))
+            state.level1_fast = False
+            continue
+        if (st & DAL_FLAG_CAND_OVERFLOW) and cap < n:
+            state.status.bitwise_and_(~DAL_FLAG_CAND_OVERFLOW)
+            state.cap_scale *= 4
+            continue
+        state.check_status(st)
+        sel = Selection(scores=(scores, loc), indices=idx, selected_scores=sel_scores, votes=(votes, loc))
+        g._last = weakref.ref(sel)
+        return sel
+
+
+def torch_float64():
+    return _torch().float64
 
 
 def _density_step_separable(state: PoolState, unlabeled_idx, forest: Forest, k: int,

@@ -111,12 +111,16 @@ class ShardedSelector:
         """This rank's device status word (DAL_FLAG_* bits), int32 [1]."""
         return self.state.status
 
-    def prepare_retry(self):
-        """After a re-rank capacity overflow anywhere: grow the capacity and go
-        again.  The density, operand and column-sum caches stay valid (only the
-        re-rank capacity changed), so the retry does not redo the Gram."""
+    def prepare_retry(self, sample_miss: bool = False):
+        """After a re-rank capacity overflow (or a truncated level-1
+        overflow) anywhere: grow the capacity (or fall back to the exact radix
+        level 1) and go again.  The density, operand and column-sum caches stay valid,
+        so the retry does not redo the Gram."""
         self.state.status.zero_()
-        self.cap_scale *= 4
+        if sample_miss:
+            self.state.level1_fast = False
+        else:
+            self.cap_scale *= 4
 
     def clear_caches(self):
         """Drop the shard's normalised rows, density and column sums (cold step)."""
@@ -397,8 +401,8 @@ def select(sel: ShardedSelector, comm, unlabeled_idx, forest, k: int, mode: str 
     if st & _lib.DAL_FLAG_ZERO_NORM:
         raise ValueError("pool contains a zero-norm row: cosine similarity is undefined "
                          "(the reference would propagate NaN into every density)")
-    if st & _lib.DAL_FLAG_CAND_OVERFLOW:  # rare: grow the re-rank capacity everywhere and redo
-        sel.prepare_retry()
+    if st & (_lib.DAL_FLAG_CAND_OVERFLOW | _lib.DAL_FLAG_SAMPLE_MISS):  # rare: redo on every rank
+        sel.prepare_retry(sample_miss=bool(st & _lib.DAL_FLAG_SAMPLE_MISS))
         return select(sel, comm, unlabeled_idx, forest, k, mode, strategy, beta, sort_fn, density_mode)
     return out
 
@@ -451,6 +455,13 @@ def emulate(selectors, unlabeled_idx, forest, k: int, mode: str = "dw",
     n_unl = int(np.asarray(unlabeled_idx).reshape(-1).shape[0]) if not hasattr(unlabeled_idx, "shape") \
         else int(unlabeled_idx.shape[0])
     out = merge_topk(keys_all, idx_all, sc_all, k, sort_fn, all_valid=n_unl >= k)
+    st = 0
+    for s in selectors:
+        st |= int(s.state.status.item())
+    if st & (_lib.DAL_FLAG_SAMPLE_MISS | _lib.DAL_FLAG_CAND_OVERFLOW):  # as select(): redo on every shard
+        for s in selectors:
+            s.prepare_retry(sample_miss=bool(st & _lib.DAL_FLAG_SAMPLE_MISS))
+        return emulate(selectors, unlabeled_idx, forest, k, mode, strategy, beta, sort_fn, density_mode)
     for s in selectors:
         s.state.check_status()
     return out

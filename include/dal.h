@@ -55,6 +55,7 @@ enum dal_status {
 #define DAL_FLAG_ZERO_NORM 1      /* a pool row has ||x|| == 0 (cosine undefined) */
 #define DAL_FLAG_CAND_OVERFLOW 2  /* re-rank candidate set exceeded capacity */
 #define DAL_FLAG_RF_SPLITS 4      /* a feature produced more than num_splits + 1 thresholds */
+#define DAL_FLAG_SAMPLE_MISS 8    /* truncated top-k level 1 over capacity: re-run with level1_passes = 0 */
 
 /* per-row flags (uint8 per pool row) */
 #define DAL_ROW_CANDIDATE 1 /* row is in the unlabeled set and may be selected */
@@ -241,12 +242,19 @@ int dal_topk(const uint64_t* keys, int64_t n, int64_t k, int64_t idx_base, void*
  * colsum_ready (nullable): an event recorded after ``colsum`` was written on
  * another stream; the call makes ``stream`` wait for it just before the
  * re-rank (the radix select and compaction run without it), so a cold step's
- * canonical column sum overlaps the candidate search. */
+ * canonical column sum overlaps the candidate search.
+ * level1_passes = p in 1..5 (cap <= DAL_SORT_CAP_PAYLOAD): level 1 resolves
+ * only the first p radix digits of K; tau = the upper edge of K's bucket
+ * (tau >= K) and the candidates are every row whose optimistic key is <= tau
+ * -- a superset of the exact candidates, found in p + 1 launches instead of 9
+ * (the engine uses p = 2: ~2^-11 relative, about a density interval's width).
+ * More than cap candidates sets DAL_FLAG_SAMPLE_MISS: re-run with
+ * level1_passes = 0.  The selection is the same either way. */
 size_t dal_dw_select_workspace_bytes(int64_t n, int64_t k, int64_t cap);
 int dal_dw_select(const uint64_t* keys_lo, const uint64_t* keys_hi, const int32_t* votes,
                   const uint8_t* row_flags, int64_t n, int64_t k, int64_t idx_base,
                   const double* lut, double beta, const float* x, int64_t d, int64_t ldx,
-                  const double* norm64, const double* colsum, int64_t cap, void* ws,
+                  const double* norm64, const double* colsum, int64_t cap, int32_t level1_passes, void* ws,
                   size_t ws_bytes, int64_t* out_idx, double* out_scores, uint64_t* out_keys,
                   int32_t* dev_status, dal_event_t colsum_ready, dal_stream_t stream);
 

@@ -1,6 +1,8 @@
 """One cold config-2 density step, repeated, for a kernel timeline under
 rocprofv3 --kernel-trace (analyse with scripts/step_timeline.py --analyse DIR).
-usage: rocprofv3 --kernel-trace -d gpurun_out/tl -o tl --output-format csv -- python scripts/step_timeline.py"""
+usage: rocprofv3 --kernel-trace -d gpurun_out/tl -o tl --output-format csv -- python scripts/step_timeline.py [warm]
+"warm": the density stays cached (the reference's per-iteration path); the
+analysis then starts at the last step's mark_rows launch."""
 import glob
 import os
 import sys
@@ -8,13 +10,13 @@ import sys
 REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 
 
-def analyse(d):
+def analyse(d, first="normalize_split"):
     import csv
     f = sorted(glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True))[-1]
     rows = list(csv.DictReader(open(f)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     # the last step: from the last Gram launch's predecessor normalize_split
-    starts = [i for i, r in enumerate(rows) if "normalize_split" in r["Kernel_Name"]]
+    starts = [i for i, r in enumerate(rows) if first in r["Kernel_Name"]]
     i0 = starts[-1]
     t0 = int(rows[i0]["Start_Timestamp"])
     prev_end = t0
@@ -30,7 +32,7 @@ def analyse(d):
 
 if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--analyse":
-        analyse(sys.argv[2])
+        analyse(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "normalize_split")
         sys.exit(0)
     sys.path.insert(0, os.path.join(REPO, "distributed-active-learning_amd"))
     sys.path.insert(0, REPO)
@@ -46,8 +48,10 @@ if __name__ == "__main__":
     forest = Forest.synthetic(10, 4, d, seed=1, dist="uniform")
     unl = torch.arange(10, n, device=dev, dtype=torch.int64)
     state = engine.PoolState(x, excluded=np.arange(10), device=dev)
+    warm = len(sys.argv) > 1 and sys.argv[1] == "warm"
     for _ in range(6):
-        state.clear_caches()
+        if not warm:
+            state.clear_caches()
         r = engine.density_step(state, unl, forest, 100)
     torch.cuda.synchronize()
     print("ok", r.indices[:5].tolist())
