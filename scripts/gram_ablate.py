@@ -16,7 +16,7 @@ from dal.engine import PoolState, _ptr, _stream  # noqa: E402
 dev = torch.device("cuda:0")
 libs = {"full": _lib.load()}
 for a in os.environ.get("AB_LIBS", "abl1,abl2").split(","):
-    p = os.path.join(REPO, "build", a, "libdal.so")
+    p = os.path.join(REPO, os.environ.get("AB_DIR", "build"), a, "libdal.so")
     if os.path.exists(p):
         libs[a] = ctypes.CDLL(p)
 # variants of the current library selected by environment knobs: name=VAR:VAL
