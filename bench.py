@@ -499,6 +499,40 @@ def bench_div(args, steps, warmup, world, rank, dev, dist, backend):
     return res
 
 
+def bench_rf_train(dev, n: int = 5000, d: int = 64, trees: int = 10, reps: int = 20):
+    """Per-iteration model fit (uncertainty_sampling.py:71-76): GPU
+    RandomForest.trainClassifier on an AL-sized labeled set vs scikit-learn's
+    fit on the host.  Synthetic labeled rows (U[0,1), label = thresholded row
+    sum), seeded bagging draws."""
+    import torch
+    from sklearn.ensemble import RandomForestClassifier
+
+    from dal.random_forest import bagging_inputs, train_classifier
+
+    rng = np.random.default_rng(7)
+    X = rng.random((n, d), dtype=np.float32)
+    y = (X[:, : d // 8].sum(axis=1) > d // 16).astype(np.int64)
+    w, s = bagging_inputs(n, d, trees, 4, seed=1)
+    xd = torch.from_numpy(X).to(dev)
+    for _ in range(3):
+        train_classifier(xd, y, trees, weights=w, feature_subsets=s, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        train_classifier(xd, y, trees, weights=w, feature_subsets=s, device=dev)
+    torch.cuda.synchronize()
+    gpu_ms = (time.perf_counter() - t0) / reps * 1e3
+    t0 = time.perf_counter()
+    RandomForestClassifier(n_estimators=trees, max_depth=4, max_features="sqrt", bootstrap=True,
+                           random_state=0, n_jobs=-1).fit(X, y)
+    cpu_ms = (time.perf_counter() - t0) * 1e3
+    return {"workload": f"RandomForest.trainClassifier on {n} x {d} labeled rows, T={trees}, depth 4, "
+                        "32 bins, sqrt features (MLlib 2.1 algorithm)",
+            "gpu_ms_per_fit": gpu_ms, "sklearn_host_ms_per_fit": cpu_ms, "cores": _cores(),
+            "note": "wall per fit incl. the host's bagging draws and the forest's copy back; sklearn is "
+                    "a different (midpoint-threshold) algorithm timed for scale"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -551,6 +585,8 @@ def main():
             out["extra"][f"config{c}"] = {kk: r[kk] for kk in (
                 "value", "unit", "steps", "ms_per_step", "config", "warm_selection_latency_ms", "self_check",
                 "roofline", "roofline_forest", "roofline_topk") if kk in r}
+    if world == 1 and CONFIGS[args.config].get("mode") != "div":
+        out.setdefault("extra", {})["rf_train"] = bench_rf_train(dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

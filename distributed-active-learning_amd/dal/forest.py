@@ -15,7 +15,11 @@ Shallower leaves are padded with always-left splits (threshold = +inf) whose
 whole subtree carries the leaf's class, so every root-to-leaf walk is exactly
 D steps (wave-uniform trip count on the GPU).  Thresholds are rounded toward
 -inf to fp32: for every fp32 x,  x <= t32  <=>  (double)x <= t64, so votes are
-bit-exact against MLlib (fp64) and scikit-learn (fp32 X, fp64 thresholds).
+bit-exact against scikit-learn (fp32 X, fp64 thresholds) and against MLlib's
+fp64 comparison FOR fp32-REPRESENTABLE FEATURE VALUES (the pool is fp32 here;
+text features that are not fp32-representable are rounded on ingest, and a
+value within that rounding of an fp64 MLlib threshold can fall on the other
+side -- parity unpinned for such data: no reference-held model covers it).
 """
 from __future__ import annotations
 
