@@ -240,18 +240,25 @@ def forest_roofline(n_rows, d, trees, forest_ms, config, world):
     return out
 
 
-def topk_roofline(n_rows, select_ms, config, world):
-    """K3 (dal_dw_select: radix select of the k-th pessimistic key, ordered
-    compaction of the interval candidates, exact fp64 re-rank, one-block
-    sort).  Algorithmic bytes per call = 8 B per row per radix pass + 2 x 16 B
-    per row (both interval keys, count and write passes); the re-rank and sort
-    touch O(candidates) bytes."""
+def topk_roofline(n_rows, select_ms, config, world, level1_passes=0):
+    """K3 (dal_dw_select).  Exact level 1: radix select of the k-th
+    pessimistic key (6 passes x 8 B per row) + ordered compaction (count and
+    write: both interval keys, 2 x 16 B per row).  Truncated level 1 (the
+    engine default on pools whose candidates fit 4,096 slots): 2 radix passes
+    (2 x 8 B) + one append pass over both keys (16 B).  The exact fp64 re-rank
+    and the one-block sort touch O(candidates) bytes."""
     if not select_ms:
         return None
-    per_row = 8 * TOPK_RADIX_PASSES + 32
+    if level1_passes:
+        per_row = 8 * level1_passes + 16
+        kernel = (f"dal_dw_select ({level1_passes}-digit radix bound + candidate append + fp64 re-rank + "
+                  "sort)")
+    else:
+        per_row = 8 * TOPK_RADIX_PASSES + 32
+        kernel = "dal_dw_select (radix select + interval compaction + fp64 re-rank + sort)"
     nbytes = float(n_rows) * per_row
     gbs = nbytes / (select_ms * 1e-3) / 1e9
-    return {"bound": "hbm", "kernel": "dal_dw_select (radix select + interval compaction + fp64 re-rank + sort)",
+    return {"bound": "hbm", "kernel": kernel,
             "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
             "traffic": _traffic(config, "dw_select_bytes_per_launch", world), "launch_ms": select_ms,
             "algorithmic_bytes_per_launch": nbytes, "bytes_per_row": per_row,
@@ -406,15 +413,16 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
         "warm_rows_per_s": (n_scored / (warm_ms * 1e-3)) if warm_ms else None,
         "self_check": {"gram_selection_equals_separable_selection": same,
                        "warm_selection_equals_cold_selection": warm_same, "k": k,
-                       "note": "last timed step vs the exact O(N*D) density path, and the last warm "
-                               "(graph-replayed) step vs the cold one: indices + fp64 score bits"},
+                       "note": "last timed step vs the exact O(N*D) density path, and the last warm step "
+                               "vs the cold one: indices + fp64 score bits"},
         "separable": ({"cold_selection_latency_ms": sep_ms, "rows_per_s": n_scored / (sep_ms * 1e-3),
                        "note": "density via the exact O(N*D) identity sum_j<u_i,u_j> = <u_i, sum_j u_j> "
                                "(canonical fp64, same selection); HBM-bound, not the MFMA path"}
                       if sep_ms else None),
         "roofline": gram_roofline(state.gram, achieved, traffic, gram_ms, gram_ms_max, flops),
         "roofline_forest": forest_roofline(state.n, d, cfg["trees"], forest_ms, config, world),
-        "roofline_topk": topk_roofline(state.n, select_ms, config, world),
+        "roofline_topk": topk_roofline(state.n, select_ms, config, world,
+                                       engine.LEVEL1_PASSES if state.level1_fast else 0),
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and cpu and not args.no_cpu_baseline:

@@ -169,14 +169,39 @@ __global__ __launch_bounds__(kRadixThreads) void radix_hist_kernel(const uint64_
   const int shift = digit_shift(pass);
   const unsigned long long dmask = static_cast<unsigned long long>(digit_bins(pass) - 1);
   const unsigned long long hmask = pass == 0 ? 0ull : (~0ull << (64 - kDigitBits * pass));
+  // scores cluster (DW keys share their sign/exponent digit, LC keys take
+  // T+1 values): the wave's most common bin -- the first valid lane's -- is
+  // counted with ONE atomic, the other lanes add theirs (no 64-way LDS
+  // same-address serialisation on the heavy bin)
+  const int lane = tid & 63;
+  auto count = [&](bool valid, unsigned bin) {
+    const unsigned long long vm = __ballot(valid);
+    if (!vm) return;
+    const int first = __ffsll(static_cast<long long>(vm)) - 1;
+    const unsigned b0 = __shfl(bin, first);
+    const unsigned long long m0 = __ballot(valid && bin == b0);
+    if (lane == first) atomicAdd(&hist[b0], static_cast<unsigned>(__popcll(m0)));
+    if (valid && bin != b0) atomicAdd(&hist[bin], 1u);
+  };
 #pragma unroll
   for (int j = 0; j < kPre; ++j) {
     const unsigned long long key = pre[j];
-    if (i0 + j * stride < n && (key & hmask) == prefix) atomicAdd(&hist[(key >> shift) & dmask], 1u);
+    count(i0 + j * stride < n && (key & hmask) == prefix, static_cast<unsigned>((key >> shift) & dmask));
   }
-  for (int64_t i = i0 + kPre * stride; i < n; i += stride) {
-    const unsigned long long key = keys[i];
-    if ((key & hmask) == prefix) atomicAdd(&hist[(key >> shift) & dmask], 1u);
+  // the rest in batches of kPre keys, each batch's loads in flight together
+  // (wave-uniform trip count: the ballots see every lane)
+  for (int64_t i0b = i0 - tid + kPre * stride; i0b < n; i0b += kPre * stride) {
+    unsigned long long kb[kPre];
+#pragma unroll
+    for (int j = 0; j < kPre; ++j) {
+      const int64_t i = i0b + j * stride + tid;
+      kb[j] = i < n ? keys[i] : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < kPre; ++j) {
+      const int64_t i = i0b + j * stride + tid;
+      count(i < n && (kb[j] & hmask) == prefix, static_cast<unsigned>((kb[j] >> shift) & dmask));
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -403,23 +428,41 @@ __global__ __launch_bounds__(kRadixThreads) void threshold_append_kernel(
   const int tid = threadIdx.x, lane = tid & 63;
   if (blockIdx.x == 0 && tid == 0) h->kstar = tau;
   unsigned long long below = 0;
-  for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * kRadixThreads; i0 < n;
-       i0 += static_cast<int64_t>(gridDim.x) * kRadixThreads) {
-    const int64_t i = i0 + tid;
-    bool cand = false;
-    if (i < n) {
-      below += keys_lo[i] <= tau;
-      const unsigned long long hi = keys_hi[i];
-      cand = hi <= tau && hi != DAL_KEY_NONE;
+  constexpr int kIlp = 8;  // keys per thread per sweep: their loads go out together
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kRadixThreads;
+  for (int64_t b0 = static_cast<int64_t>(blockIdx.x) * kRadixThreads; b0 < n; b0 += kIlp * stride) {
+    unsigned long long lo[kIlp], hi[kIlp];
+#pragma unroll
+    for (int j = 0; j < kIlp; ++j) {
+      const int64_t i = b0 + j * stride + tid;
+      lo[j] = i < n ? keys_lo[i] : DAL_KEY_NONE;
+      hi[j] = i < n ? keys_hi[i] : DAL_KEY_NONE;
     }
-    const unsigned long long m = __ballot(cand);
-    if (!m) continue;
+    bool cand[kIlp];
+    unsigned int nc = 0;
+#pragma unroll
+    for (int j = 0; j < kIlp; ++j) {
+      below += b0 + j * stride + tid < n && lo[j] <= tau;
+      cand[j] = hi[j] <= tau && hi[j] != DAL_KEY_NONE;
+      nc += cand[j];
+    }
+    // one slot reservation per wave and sweep for all its candidates
+    unsigned int incl = nc;
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned int y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    const unsigned int tot = __shfl(incl, 63);
+    if (!tot) continue;
     unsigned int base = 0;
-    if (lane == 0) base = atomicAdd(&h->cand_count, static_cast<unsigned int>(__popcll(m)));
-    base = __shfl(base, 0);
-    if (cand) {
-      const int64_t pos = base + __popcll(m & ((1ull << lane) - 1ull));
-      if (pos < cap) cidx[pos] = idx_base + i;
+    if (lane == 0) base = atomicAdd(&h->cand_count, tot);
+    int64_t pos = static_cast<int64_t>(__shfl(base, 0)) + (incl - nc);
+#pragma unroll
+    for (int j = 0; j < kIlp; ++j) {
+      if (cand[j]) {
+        if (pos < cap) cidx[pos] = idx_base + b0 + j * stride + tid;
+        ++pos;
+      }
     }
   }
   for (int o = 32; o > 0; o >>= 1) below += __shfl_xor(below, o);
@@ -464,7 +507,21 @@ __global__ __launch_bounds__(256) void rerank_kernel(const TopkHdr* __restrict__
   const double nr = norm64[i];
   const float* xr = x + i * ldx;
   double acc = 0.0;
-  for (int f = 0; f < d; ++f) {
+  // the row's features are fetched 64 at a time (all loads in flight before
+  // the sequential canonical chain consumes them), not one dependent load per step
+  constexpr int kChunk = 64;
+  int f0 = 0;
+  for (; f0 + kChunk <= d; f0 += kChunk) {
+    float xv[kChunk];
+#pragma unroll
+    for (int q = 0; q < kChunk; ++q) xv[q] = xr[f0 + q];
+#pragma unroll
+    for (int q = 0; q < kChunk; ++q) {
+      const double u = static_cast<double>(xv[q]) / nr;
+      acc = acc + u * colsum[f0 + q];
+    }
+  }
+  for (int f = f0; f < d; ++f) {
     const double u = static_cast<double>(xr[f]) / nr;
     acc = acc + u * colsum[f];
   }
@@ -705,8 +762,11 @@ int run_radix(const uint64_t* keys, int64_t n, int64_t k, TopkHdr* h, hipStream_
   const int64_t words = sizeof(TopkHdr) / 4;
   hipLaunchKernelGGL(zero_words_kernel, dim3(static_cast<unsigned>(ceil_div(words, 256 * 4))), dim3(256), 0, st,
                      reinterpret_cast<uint32_t*>(h), words);
+  // each block flushes up to 2048 bins with global atomics: beyond ~256
+  // blocks the flush, not the key stream, sets a pass's time (2M keys: 977
+  // blocks -> 2M atomics)
   int64_t blocks = ceil_div(n, kRadixThreads * 8);
-  if (blocks > 2048) blocks = 2048;
+  if (blocks > 256) blocks = 256;
   if (blocks < 1) blocks = 1;
   for (int p = 0; p < passes; ++p) {
     hipLaunchKernelGGL(radix_hist_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kRadixThreads), 0,

@@ -23,7 +23,7 @@ def analyse(d, first="normalize_split"):
     tot = 0
     for r in rows[i0:]:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-        name = r["Kernel_Name"].split("(")[0][-60:]
+        name = r["Kernel_Name"].replace("dal::(anonymous namespace)::", "").split("(")[0][-60:]
         print(f"{(s - t0) / 1e3:9.1f} us  gap {(s - prev_end) / 1e3:7.1f}  dur {(e - s) / 1e3:8.1f}  {name}")
         prev_end = e
         tot = e - t0
@@ -43,7 +43,7 @@ if __name__ == "__main__":
     import bench
 
     dev = torch.device("cuda:0")
-    n, d = 100000, 64
+    n, d = (int(v) for v in os.environ.get("TL_SHAPE", "100000x64").split("x"))
     x = bench.upload(bench.host_pool(0, n, d, "uniform"), dev)
     forest = Forest.synthetic(10, 4, d, seed=1, dist="uniform")
     unl = torch.arange(10, n, device=dev, dtype=torch.int64)
