@@ -169,3 +169,51 @@ def test_gpu_trained_forest_votes_and_predict(cuda):
     assert np.array_equal(votes.cpu().numpy(), ref_votes)
     assert np.array_equal(labels.cpu().numpy(), (2 * ref_votes > 10).astype(np.uint8))
     assert (labels.cpu().numpy() == y).mean() > 0.5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["min_instances", "min_gain", "bins4", "bins100", "depth1", "constant_feature",
+                                  "one_class", "sampled_thresholds", "heavy_weights"])
+def test_gpu_train_edge_cases_match_oracle(cuda, case):
+    """MLlib's strategy knobs and degenerate inputs: minInstancesPerNode,
+    minInfoGain, maxBins, depth 1, a constant feature, a single-class label
+    set, thresholds fitted on a row sample (n > max(maxBins^2, 10000)), and
+    large bootstrap counts."""
+    from dal.random_forest import bagging_inputs, split_sample_rows, train_classifier
+
+    rng = np.random.default_rng(17)
+    n, d, T, depth = 3000, 12, 10, 4
+    kw, okw, max_bins = {}, {}, 32
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    y = (X[:, 0] + 0.3 * X[:, 1] > 0).astype(np.int64)
+    if case == "min_instances":
+        kw, okw = dict(min_instances_per_node=25), dict(min_instances=25)
+    elif case == "min_gain":
+        kw, okw = dict(min_info_gain=0.01), dict(min_info_gain=0.01)
+    elif case == "bins4":
+        max_bins = 4
+    elif case == "bins100":
+        max_bins = 100
+    elif case == "depth1":
+        depth = 1
+    elif case == "constant_feature":
+        X[:, 0] = 0.5
+        X[:, 3] = -2.0
+    elif case == "one_class":
+        y = np.ones(n, dtype=np.int64)
+    elif case == "sampled_thresholds":
+        n = 20000
+        X = rng.random((n, d), dtype=np.float32)
+        y = (X[:, 2] > 0.4).astype(np.int64)
+    w, s = bagging_inputs(n, d, T, depth, seed=5)
+    if case == "heavy_weights":
+        w = (w * 37).astype(np.int32)
+    F = train_classifier(X, y, T, max_depth=depth, max_bins=max_bins, weights=w, feature_subsets=s,
+                         device=cuda, seed=3, **kw)
+    rows = split_sample_rows(n, max_bins, seed=3)
+    if case == "sampled_thresholds":
+        assert rows is not None and 0 < rows.size <= 16384
+    _, sf, st, lc = R.train_classifier(X, y, w, s, max_depth=depth, max_bins=max_bins, split_rows=rows, **okw)
+    inner, leaf = _oracle_heap(sf, st, lc)
+    assert np.array_equal(F.inner, inner)
+    assert np.array_equal(F.leaf, leaf)
