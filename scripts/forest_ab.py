@@ -47,13 +47,16 @@ for n, d, t, dist in SHAPES:
     dens = torch.zeros(st.n_pad, dtype=torch.int64, device=dev)
     err = 1e-3
     res = {}
-    variants = (("default", None), ("tpr1", "1"), ("tpr2", "2"), ("tpr4", "4"))
-    for name, tpr in variants:
-        if tpr is None:
-            os.environ.pop("DAL_FOREST_TPR", None)
+    knob = os.environ.get("AB_KNOB", "DAL_FOREST_TPR")
+    vals = os.environ.get("AB_VALS", "1,2,4").split(",")
+    variants = (("default", None),) + tuple((f"{knob}={v}", v) for v in vals)
+    for name, val in variants:
+        if val is None:
+            os.environ.pop(knob, None)
         else:
-            os.environ["DAL_FOREST_TPR"] = tpr
+            os.environ[knob] = val
         res[name] = timed(st, forest, lut, flags, dens, err)
+    os.environ.pop(knob, None)
     # scores hold NaN for excluded rows: compare bit patterns
     bits = lambda o: [a.view(torch.int64) if a.dtype == torch.float64 else a for a in o]
     ref = bits(res["default"][1])
@@ -63,4 +66,3 @@ for n, d, t, dist in SHAPES:
         same = all(torch.equal(a, b) for a, b in zip(ref, bits(out)))
         print(f"n={n} d={d} T={t} kernel={name}: {ms * 1e3:.1f} us "
               f"({n * row_bytes / ms / 1e6:.0f} GB/s algorithmic) identical={same}", flush=True)
-os.environ.pop("DAL_FOREST_TPR", None)
