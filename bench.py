@@ -493,7 +493,7 @@ def bench_div(args, steps, warmup, world, rank, dev, dist, backend):
         "scaling": "strong", "vs_baseline": None, "dtype": "bf16", "data": DATA_NOTE,
         "config": {"workload": cfg["workload"], "pool_rows": n, "features": d, "labeled": m, "k": k,
                    "parallelism": f"row-shard dp{world}" if world > 1 else "single GPU"},
-        "roofline": {"bound": "mfma", "kernel": "dal_max_cosine (v_mfma_f32_32x32x16_bf16)",
+        "roofline": {"bound": "mfma", "kernel": "dal_max_cosine (v_mfma_f32_16x16x32_bf16)",
                      "achieved": achieved, "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / BF16_MFMA_PEAK_TFLOPS,
                      "traffic": _traffic("5", "maxcos_bytes_per_launch", world), "launch_ms": kms,

@@ -7,37 +7,36 @@
 //   m_i = max_{l in L} cos(x_i, x_l)
 // and selects the k rows least similar to the labeled set.
 //
-// MI355X design: v_mfma_f32_32x32x16_bf16 (fp32 accumulate; bf16 x bf16
+// MI355X design: v_mfma_f32_16x16x32_bf16 (fp32 accumulate; bf16 x bf16
 // products are exact in fp32).  A block = 4 waves x 64 pool rows held as A
 // fragments in VGPRs (loaded once from HBM: the pool is streamed exactly
 // once); the labeled rows stream through a 2-stage LDS ring by LDS-DMA
-// (source-address XOR swizzle -> conflict-free ds_read_b128, SQ_LDS_BANK_
-// CONFLICT = 0).  Each 32x32 output tile is scaled by 1/||x_l|| (per lane =
-// per column) and max-reduced into a running per-lane maximum; a recursive-
-// halving max over the 32 column lanes and the row's 1/||x_i|| (computed
-// in-kernel from the resident fragments) finish the row.  The similarity
-// matrix is never stored.
+// (source-address XOR swizzle -> conflict-free ds_read_b128).  Each 16x16
+// output tile is scaled by 1/||x_l|| (per lane = per column) and max-reduced
+// into a running per-lane maximum (one v_max3 per two products); a recursive-
+// halving max over the 16 column lanes and the row's 1/||x_i|| (the diagonal
+// of the resident fragments' own Gram, four MFMAs per row tile) finish the
+// row.  The similarity matrix is never stored.
 //
-// Measured at 8M x 128, m = 1024 (scripts/maxcos_ab.py, bit-identical
-// outputs): one wave per SIMD with 64 KiB stages 2.78 ms (30% of dense bf16
-// peak; exposed per-block A fetch, 5-step butterfly reduction); two waves per
-// SIMD 2.04 ms; + v_max3 pairs, hoisted DMA offsets, halving reduction
-// 1.80 ms; + immediate-offset B reads 1.75 ms (48%, MFMA busy 61% at the
-// 1.89 GHz the chip holds under this load).
+// The kernel is bound by vector ISSUE, not by the matrix pipe: an MFMA holds
+// its SIMD's issue for 8 cycles (of 16 for this shape) and each product costs
+// 1.5 VALU in the epilogue, so what paid was taking VALU out (fp64 norms ->
+// MFMA norms) and putting more waves beside it (three per SIMD: 16 KiB
+// stages, 152 VGPRs at d = 128).
+// Measured at 8M x 128, m = 1024 (scripts/maxcos_ab.py, same process): the
+// previous 32x32x16 kernel (two waves per SIMD, fp64 norms) 1.97 ms; this one
+// 1.57 ms (53 % of the dense bf16 peak); with the arg-max 9.30 -> 3.14 ms.
 #include <type_traits>
-
-#include <stdlib.h>
 
 #include "common.hpp"
 
 namespace dal {
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 #define AS3 __attribute__((address_space(3)))
 
-constexpr int kMcThreads = 256;
 constexpr int kMcRows = 256;     // pool rows per block (64 per wave)
 constexpr int kMaxLab = 4096;    // labeled rows whose 1/||x|| fit the LDS table
 
@@ -45,55 +44,50 @@ __device__ __forceinline__ float bf16_to_f32(uint16_t b) {
   return __uint_as_float(static_cast<unsigned>(b) << 16);
 }
 
-// Two waves per SIMD (OCC = 2: 32 KiB stages, 1/||x_l|| table in dynamic LDS
-// so two blocks fit a CU): one wave's A-fragment fetch, norm and epilogue VALU
-// run under the other wave's MFMAs.  Column tiles in pairs so the running max
-// takes one v_max3 per two products; branch-free A loads (rows clamped to
-// n-1, never stored); the stage-0 DMA is issued before the A fetch so both are
-// in flight together; d = 128 unrolls the stage loop twice so every B-fragment
-// address is a per-lane base plus an immediate.
-template <int DK, int OCC, int NW = 4>
-struct Mc2Cfg {
-  static constexpr int STAGE = (OCC == 2 || NW == 8) ? 32768 : 65536;
-  static constexpr int F4 = STAGE / 16;
-  static constexpr int ROWB = DK * 2;
-  static constexpr int SLOTS = ROWB / 16;
-  static constexpr int SR = STAGE / ROWB;
-  static constexpr int NCT = SR / 32;
-  static constexpr int NKS = DK / 16;
-  static constexpr int SWZ = (SLOTS < 16 ? SLOTS : 16) - 1;
-  static constexpr int PIECES = STAGE / (NW * 1024);  // 1 KiB LDS-DMA pieces per wave per stage
-};
-
-// NW = waves per block (64 pool rows each).  NW = 8 (one 512-thread block per
-// CU, still two waves per SIMD, half the DMA issue per MFMA) measured 12 %
-// slower than NW = 4 at 8M x 128 (barriers over 8 waves), so NW = 4 is used.
+// Lane layout: A/B fragments hold row/column li = lane & 15, k = 8 (lane >> 4)
+// .. +7 of a 32-wide k-step; the 16x16 output holds column li, rows
+// 4 (lane >> 4) + i.  The running maximum keeps 4 x 4 values per lane.
 //
 // ARG: also the arg-max (labeled-row position l) of every pool row.  Each lane
 // keeps, per accumulator slot, its best value b1 (first l on equal values: l
 // grows along a lane's columns and only a strictly larger value replaces b1),
-// that value's l, and the runner-up b2; a butterfly over the 32 column lanes
+// that value's l, and the runner-up b2; a butterfly over the 16 column lanes
 // merges the triples.  When the scaled top two are more than 2 x the error
 // bound apart the fp32 arg-max is the canonical one (|m_gpu - m_canon| <= err
 // per entry); otherwise the row gets -1 - l and dal_maxcos_argmax_resolve
 // recomputes it in canonical fp64.
-template <int DK, int OCC, int NW, bool ARG = false>
-__global__ __launch_bounds__(64 * NW, OCC) void maxcos2_kernel(
+
+template <int DK, int STAGE_ = 32768>
+struct McCfg {
+  static constexpr int STAGE = STAGE_;
+  static constexpr int F4 = STAGE / 16;
+  static constexpr int ROWB = DK * 2;
+  static constexpr int SLOTS = ROWB / 16;
+  static constexpr int SR = STAGE / ROWB;   // labeled rows per stage
+  static constexpr int NCT = SR / 16;       // 16-column tiles per stage (even)
+  static constexpr int NKS = DK / 32;
+  static constexpr int RT = 4;              // 16-row tiles per wave
+  static constexpr int SWZ = (SLOTS < 16 ? SLOTS : 16) - 1;
+  static constexpr int PIECES = STAGE / (4 * 1024);
+  static_assert(NCT % 2 == 0, "column tiles go in pairs");
+};
+
+template <int DK, bool ARG, int OCC>
+__global__ __launch_bounds__(256, OCC) void maxcos_kernel(
     const uint16_t* __restrict__ pool, int64_t n, const uint16_t* __restrict__ lab, int64_t m_pad,
     const float* __restrict__ inv_lab, const float* __restrict__ inv_pool, float* __restrict__ out,
     int32_t* __restrict__ out_arg, double gap, int32_t* __restrict__ status) {
-  using C = Mc2Cfg<DK, OCC, NW>;
+  using C = McCfg<DK, OCC == 3 ? 16384 : 32768>;
   extern __shared__ __attribute__((aligned(16))) float4 mc_dyn[];
   float4* lds = mc_dyn;
   float* invl = reinterpret_cast<float*>(mc_dyn + 2 * C::F4);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int li = lane & 31, lh = lane >> 5;
-  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * (64 * NW) + wave * 64;
+  const int li = lane & 15, lq = lane >> 4;
+  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * 256 + wave * 64;
   const int n_stages = static_cast<int>(m_pad / C::SR);
 
-  for (int i = tid; i < m_pad; i += 64 * NW) invl[i] = inv_lab[i];
+  for (int i = tid; i < m_pad; i += 256) invl[i] = inv_lab[i];
 
-  // per-piece source offsets (swizzled) and the wave's LDS base, computed once
   unsigned voff[C::PIECES];
 #pragma unroll
   for (int q = 0; q < C::PIECES; ++q) {
@@ -118,51 +112,55 @@ __global__ __launch_bounds__(64 * NW, OCC) void maxcos2_kernel(
           : "memory");
     }
   };
-  // stage 0 first: the compiler's own waits for the (younger) A loads then
-  // also cover it, which is conservative and correct
   issue(0, 0);
 
-  bf16x8 a[2][C::NKS];
+  bf16x8 a[C::RT][C::NKS];
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt) {
-    int64_t row = row0 + rt * 32 + li;
+  for (int rt = 0; rt < C::RT; ++rt) {
+    int64_t row = row0 + rt * 16 + li;
     row = row < n ? row : n - 1;
 #pragma unroll
     for (int s = 0; s < C::NKS; ++s)
-      a[rt][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pool + row * DK + 16 * s + 8 * lh));
+      a[rt][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pool + row * DK + 32 * s + 8 * lq));
   }
 
-  // 1/||x_i||: fp64 sum of squares of the register-resident fragments; v*v is
-  // exact in fp64, so fma(v, v, s) == s + v*v (dal_inv_norms_bf16's value)
-  float inv_row[2];
+  // 1/||x_i|| from the resident fragments: ||x_i||^2 is the diagonal of the
+  // tile's own Gram A A^T (an A fragment is also the B fragment of the same
+  // rows), NKS MFMAs per row tile instead of d fp64 conversions and FMAs per
+  // row -- this kernel is vector-issue-bound, not MFMA-bound.  Exact products,
+  // fp32 sums: the norm's error is part of dal_maxcos_error_bound.  Diagonal
+  // (r, r) sits on lane r + 16 (r >> 2), element r & 3.
+  float inv_row[C::RT];
+  {
+    const int src = li + 16 * (li >> 2);
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt) {
-    double s2 = 0.0;
+    for (int rt = 0; rt < C::RT; ++rt) {
+      f32x4 g = {};
 #pragma unroll
-    for (int s = 0; s < C::NKS; ++s) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const double v = static_cast<double>(static_cast<float>(a[rt][s][e]));
-        s2 = __builtin_fma(v, v, s2);
-      }
+      for (int s = 0; s < C::NKS; ++s) g = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rt][s], a[rt][s], g, 0, 0, 0);
+      const int j = li & 3;
+      const float mine = j == 0 ? g[0] : j == 1 ? g[1] : j == 2 ? g[2] : g[3];
+      const float n2 = __shfl(mine, src);
+      inv_row[rt] = static_cast<float>(1.0 / __builtin_sqrt(static_cast<double>(n2)));
     }
-    s2 = s2 + __shfl_xor(s2, 32);
-    inv_row[rt] = static_cast<float>(1.0 / __builtin_sqrt(s2));
   }
 
-  float mx0[16], mx1[16];
-  float sb0[ARG ? 16 : 1], sb1[ARG ? 16 : 1];  // runner-up values (ARG)
-  int ag0[ARG ? 16 : 1], ag1[ARG ? 16 : 1];    // arg of mx (ARG)
+  float mx[C::RT][4];
+  float sb[ARG ? C::RT : 1][4];
+  int ag[ARG ? C::RT : 1][4];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) mx0[r] = mx1[r] = -__builtin_inff();
+  for (int rt = 0; rt < C::RT; ++rt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) mx[rt][i] = -__builtin_inff();
   if constexpr (ARG) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      sb0[r] = sb1[r] = -__builtin_inff();
-      ag0[r] = ag1[r] = 0x7FFFFFFF;
-    }
+    for (int rt = 0; rt < C::RT; ++rt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        sb[rt][i] = -__builtin_inff();
+        ag[rt][i] = 0x7FFFFFFF;
+      }
   }
-  // (b1, l, b2) <- v at column l; NaN (padding) never replaces b1 or b2
   auto upd = [](float& b1, float& b2, int& a, float v, int l) {
     if (v > b1) {
       b2 = b1;
@@ -172,14 +170,56 @@ __global__ __launch_bounds__(64 * NW, OCC) void maxcos2_kernel(
       b2 = fmaxf(b2, v);
     }
   };
-  const f32x16 zero = {};
-
-  // per-lane LDS offsets of the B fragment of each k-step (float4 units);
-  // column-tile and ring-buffer offsets are compile-time immediates
+  const f32x4 zero = {};
   int boff[C::NKS];
 #pragma unroll
-  for (int s = 0; s < C::NKS; ++s) boff[s] = li * C::SLOTS + ((2 * s + lh) ^ (li & C::SWZ));
+  for (int s = 0; s < C::NKS; ++s) boff[s] = li * C::SLOTS + ((4 * s + lq) ^ (li & C::SWZ));
 
+  // a pair of column tiles (ct, ct + 1): MFMAs into (c, e), then the scaled
+  // running max; a scheduling fence per pair keeps the compiler from hoisting
+  // a whole stage's B reads (registers decide the occupancy here)
+  constexpr int NP = C::NCT / 2;
+  f32x4 acc[2][C::RT];
+  auto mfma_pair = [&](const float4* B, int ct, f32x4 (&c)[2][C::RT]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int s = 0; s < C::NKS; ++s) {
+        const bf16x8 b = __builtin_bit_cast(bf16x8, B[(ct + h) * 16 * C::SLOTS + boff[s]]);
+#pragma unroll
+        for (int rt = 0; rt < C::RT; ++rt)
+          c[h][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rt][s], b, s == 0 ? zero : c[h][rt], 0, 0, 0);
+      }
+    }
+  };
+  auto epi_pair = [&](int col, const f32x4 (&c)[2][C::RT]) {
+    const float ila = invl[col + li], ilb = invl[col + 16 + li];
+    if constexpr (ARG) {
+#pragma unroll
+      for (int rt = 0; rt < C::RT; ++rt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          upd(mx[rt][i], sb[rt][i], ag[rt][i], c[0][rt][i] * ila, col + li);
+          upd(mx[rt][i], sb[rt][i], ag[rt][i], c[1][rt][i] * ilb, col + 16 + li);
+        }
+    } else {
+#pragma unroll
+      for (int rt = 0; rt < C::RT; ++rt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mx[rt][i] = fmaxf(fmaxf(mx[rt][i], c[0][rt][i] * ila), c[1][rt][i] * ilb);
+    }
+  };
+  // materialise a stage's maxima at its end: otherwise the compiler sinks the
+  // epilogue past the next barrier and keeps every accumulator alive (spills)
+  auto pin = [&]() {
+#pragma unroll
+    for (int rt = 0; rt < C::RT; ++rt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        asm volatile("" : "+v"(mx[rt][i]));
+        if constexpr (ARG) asm volatile("" : "+v"(sb[rt][i]), "+v"(ag[rt][i]));
+      }
+  };
   auto stage_body = [&](auto bufc, int st) {
     constexpr int buf = decltype(bufc)::value;
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -187,140 +227,66 @@ __global__ __launch_bounds__(64 * NW, OCC) void maxcos2_kernel(
     if (st + 1 < n_stages) issue(buf ^ 1, st + 1);
     const float4* B = lds + buf * C::F4;
 #pragma unroll
-    for (int ct = 0; ct < C::NCT; ct += 2) {
-      f32x16 c0, c1, d0, d1;
-#pragma unroll
-      for (int s = 0; s < C::NKS; ++s) {
-        const bf16x8 b = __builtin_bit_cast(bf16x8, B[ct * 32 * C::SLOTS + boff[s]]);
-        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][s], b, s == 0 ? zero : c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][s], b, s == 0 ? zero : c1, 0, 0, 0);
-      }
-#pragma unroll
-      for (int s = 0; s < C::NKS; ++s) {
-        const bf16x8 b = __builtin_bit_cast(bf16x8, B[(ct + 1) * 32 * C::SLOTS + boff[s]]);
-        d0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][s], b, s == 0 ? zero : d0, 0, 0, 0);
-        d1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][s], b, s == 0 ? zero : d1, 0, 0, 0);
-      }
-      // padded labeled rows carry NaN -> ignored by fmaxf
-      const float ila = invl[st * C::SR + ct * 32 + li], ilb = invl[st * C::SR + ct * 32 + 32 + li];
-      if constexpr (ARG) {
-        const int la = st * C::SR + ct * 32 + li;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          upd(mx0[r], sb0[r], ag0[r], c0[r] * ila, la);
-          upd(mx0[r], sb0[r], ag0[r], d0[r] * ilb, la + 32);
-          upd(mx1[r], sb1[r], ag1[r], c1[r] * ila, la);
-          upd(mx1[r], sb1[r], ag1[r], d1[r] * ilb, la + 32);
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          mx0[r] = fmaxf(fmaxf(mx0[r], c0[r] * ila), d0[r] * ilb);  // one v_max3
-          mx1[r] = fmaxf(fmaxf(mx1[r], c1[r] * ila), d1[r] * ilb);
-        }
-      }
+    for (int p = 0; p < NP; ++p) {
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_pair(B, 2 * p, acc);
+      epi_pair(st * C::SR + 2 * p * 16, acc);
     }
+    pin();
   };
-  auto stage_body_rt = [&](int st) {
-    const int buf = st & 1;
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (st + 1 < n_stages) issue(buf ^ 1, st + 1);
-    const float4* B = lds + buf * C::F4;
+  // the label granule (65536 / (2d) rows) is two 32 KiB stages: n_stages is even
+  for (int st = 0; st < n_stages; st += 2) {
+    stage_body(std::integral_constant<int, 0>{}, st);
+    stage_body(std::integral_constant<int, 1>{}, st + 1);
+  }
+  // slot j = 4 rt + i holds row 16 rt + 4 lq + i; lane li finishes slot j = li
+  const int rl = 16 * (li >> 2) + 4 * lq + (li & 3);
+  const int64_t row = row0 + rl;
+  // inv_row[rt] of row 16 rt + r lives on the lanes with li = r
+  float iv_reg = 0.0f;
 #pragma unroll
-    for (int ct = 0; ct < C::NCT; ct += 2) {
-      f32x16 c0, c1, d0, d1;
-#pragma unroll
-      for (int s = 0; s < C::NKS; ++s) {
-        const bf16x8 b = __builtin_bit_cast(bf16x8, B[ct * 32 * C::SLOTS + boff[s]]);
-        c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][s], b, s == 0 ? zero : c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][s], b, s == 0 ? zero : c1, 0, 0, 0);
-      }
-#pragma unroll
-      for (int s = 0; s < C::NKS; ++s) {
-        const bf16x8 b = __builtin_bit_cast(bf16x8, B[(ct + 1) * 32 * C::SLOTS + boff[s]]);
-        d0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][s], b, s == 0 ? zero : d0, 0, 0, 0);
-        d1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][s], b, s == 0 ? zero : d1, 0, 0, 0);
-      }
-      // padded labeled rows carry NaN -> ignored by fmaxf
-      const float ila = invl[st * C::SR + ct * 32 + li], ilb = invl[st * C::SR + ct * 32 + 32 + li];
-      if constexpr (ARG) {
-        const int la = st * C::SR + ct * 32 + li;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          upd(mx0[r], sb0[r], ag0[r], c0[r] * ila, la);
-          upd(mx0[r], sb0[r], ag0[r], d0[r] * ilb, la + 32);
-          upd(mx1[r], sb1[r], ag1[r], c1[r] * ila, la);
-          upd(mx1[r], sb1[r], ag1[r], d1[r] * ilb, la + 32);
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          mx0[r] = fmaxf(fmaxf(mx0[r], c0[r] * ila), d0[r] * ilb);  // one v_max3
-          mx1[r] = fmaxf(fmaxf(mx1[r], c1[r] * ila), d1[r] * ilb);
-        }
-      }
-    }
-  };
-  if constexpr (DK == 128 && (OCC == 2 || NW == 8)) {
-    // the label granule (65536 / (2d) rows) is two 32 KiB stages: n_stages is even
-    if ((n_stages & 1) == 0) {
-      for (int st = 0; st < n_stages; st += 2) {
-        stage_body(std::integral_constant<int, 0>{}, st);
-        stage_body(std::integral_constant<int, 1>{}, st + 1);
-      }
-    } else {
-      for (int st = 0; st < n_stages; ++st) stage_body_rt(st);
-    }
-  } else {
-    // d = 64 unrolled twice exceeds the 256-register budget: keep one body
-    for (int st = 0; st < n_stages; ++st) stage_body_rt(st);
+  for (int rt = 0; rt < C::RT; ++rt) {
+    const float t = __shfl(inv_row[rt], rl & 15);
+    if ((li >> 2) == rt) iv_reg = t;
   }
   if constexpr (ARG) {
-    // butterfly over the 32 column lanes, every slot j: merge (b1, l, b2)
-    float b1[32], b2[32];
-    int ag[32];
+    float b1[16], b2[16];
+    int av[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      b1[r] = mx0[r];
-      b1[16 + r] = mx1[r];
-      b2[r] = sb0[r];
-      b2[16 + r] = sb1[r];
-      ag[r] = ag0[r];
-      ag[16 + r] = ag1[r];
-    }
+    for (int rt = 0; rt < C::RT; ++rt)
 #pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
+      for (int i = 0; i < 4; ++i) {
+        b1[4 * rt + i] = mx[rt][i];
+        b2[4 * rt + i] = sb[rt][i];
+        av[4 * rt + i] = ag[rt][i];
+      }
 #pragma unroll
-      for (int j = 0; j < 32; ++j) {
+    for (int o = 1; o < 16; o <<= 1) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
         const float ob1 = __shfl_xor(b1[j], o), ob2 = __shfl_xor(b2[j], o);
-        const int oa = __shfl_xor(ag[j], o);
-        if (ob1 > b1[j] || (ob1 == b1[j] && oa < ag[j])) {
+        const int oa = __shfl_xor(av[j], o);
+        if (ob1 > b1[j] || (ob1 == b1[j] && oa < av[j])) {
           b2[j] = fmaxf(b1[j], ob2);
           b1[j] = ob1;
-          ag[j] = oa;
+          av[j] = oa;
         } else {
           b2[j] = fmaxf(b2[j], ob1);
         }
       }
     }
-    // lane li finishes slot j = li: row tile li>>4, accumulator element li&15
     float v1 = b1[0], v2 = b2[0];
-    int va = ag[0];
+    int va = av[0];
 #pragma unroll
-    for (int j = 1; j < 32; ++j) {
+    for (int j = 1; j < 16; ++j) {
       if (li == j) {
         v1 = b1[j];
         v2 = b2[j];
-        va = ag[j];
+        va = av[j];
       }
     }
-    const int r = li & 15;
-    const int rl = (li >> 4) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-    const float inv0 = __shfl(inv_row[0], rl & 31), inv1 = __shfl(inv_row[1], rl & 31);
-    const int64_t row = row0 + rl;
     if (row < n) {
-      const float iv = inv_pool ? inv_pool[row] : ((rl >> 5) ? inv1 : inv0);
+      const float iv = inv_pool ? inv_pool[row] : iv_reg;
       if (!(iv < __builtin_inff())) atomicOr(status, DAL_FLAG_ZERO_NORM);
       const float m1 = v1 * iv, m2 = v2 * iv;
       out[row] = m1;
@@ -329,20 +295,14 @@ __global__ __launch_bounds__(64 * NW, OCC) void maxcos2_kernel(
     }
     return;
   }
-  // max over the 32 column lanes by recursive halving: at mask m a lane keeps
-  // the half of its 2m values selected by (li & m) and folds in the partner's
-  // copy of that half (31 shuffles).  Lane li ends with value j = li, i.e.
-  // row tile li>>4, accumulator element r = li&15.
-  float v[32];
+  float v[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    v[r] = mx0[r];
-    v[16 + r] = mx1[r];
-  }
+  for (int rt = 0; rt < C::RT; ++rt)
 #pragma unroll
-  for (int step = 0; step < 5; ++step) {
-    const int m = 16 >> step;
-    // bit-mask selects (a ternary on array elements becomes dynamic indexing)
+    for (int i = 0; i < 4; ++i) v[4 * rt + i] = mx[rt][i];
+#pragma unroll
+  for (int step = 0; step < 4; ++step) {
+    const int m = 8 >> step;
     const unsigned upm = (li & m) ? 0xFFFFFFFFu : 0u;
 #pragma unroll
     for (int j = 0; j < m; ++j) {
@@ -352,15 +312,10 @@ __global__ __launch_bounds__(64 * NW, OCC) void maxcos2_kernel(
       v[j] = fmaxf(keep, __shfl_xor(send, m));
     }
   }
-  const float mine = v[0];
-  const int r = li & 15;
-  const int rl = (li >> 4) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-  const float inv0 = __shfl(inv_row[0], rl & 31), inv1 = __shfl(inv_row[1], rl & 31);
-  const int64_t row = row0 + rl;
   if (row < n) {
-    const float iv = inv_pool ? inv_pool[row] : ((rl >> 5) ? inv1 : inv0);
+    const float iv = inv_pool ? inv_pool[row] : iv_reg;
     if (!(iv < __builtin_inff())) atomicOr(status, DAL_FLAG_ZERO_NORM);
-    out[row] = mine * iv;
+    out[row] = v[0] * iv;
   }
 }
 
@@ -478,18 +433,17 @@ __global__ __launch_bounds__(256) void maxcos_argmax_resolve_kernel(const uint16
   }
 }
 
-template <int DK, bool ARG>
+template <int DK, bool ARG, int OCC>
 int launch_maxcos_t(const uint16_t* pool, int64_t n, const uint16_t* lab, int64_t m_pad, const float* inv_lab,
-                    const float* inv_pool, float* out, int32_t* out_arg, double gap, int32_t* status,
-                    hipStream_t st) {
+                      const float* inv_pool, float* out, int32_t* out_arg, double gap, int32_t* status,
+                      hipStream_t st) {
   const int64_t blocks = ceil_div(n, kMcRows);
-  constexpr int OCC = DK <= 128 ? 2 : 1;
-  const size_t shm = 2 * Mc2Cfg<DK, OCC>::STAGE + static_cast<size_t>(m_pad) * 4;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(maxcos2_kernel<DK, OCC, 4, ARG>),
+  const size_t shm = 2 * McCfg<DK, OCC == 3 ? 16384 : 32768>::STAGE + static_cast<size_t>(m_pad) * 4;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(maxcos_kernel<DK, ARG, OCC>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm)) != hipSuccess)
     return DAL_ERR_HIP;
-  hipLaunchKernelGGL((maxcos2_kernel<DK, OCC, 4, ARG>), dim3(static_cast<unsigned>(blocks)), dim3(kMcThreads), shm,
-                     st, pool, n, lab, m_pad, inv_lab, inv_pool, out, out_arg, gap, status);
+  hipLaunchKernelGGL((maxcos_kernel<DK, ARG, OCC>), dim3(static_cast<unsigned>(blocks)), dim3(256), shm, st, pool, n,
+                     lab, m_pad, inv_lab, inv_pool, out, out_arg, gap, status);
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
 }
@@ -497,8 +451,12 @@ int launch_maxcos_t(const uint16_t* pool, int64_t n, const uint16_t* lab, int64_
 template <int DK>
 int launch_maxcos(const uint16_t* pool, int64_t n, const uint16_t* lab, int64_t m_pad, const float* inv_lab,
                   const float* inv_pool, float* out, int32_t* out_arg, double gap, int32_t* status, hipStream_t st) {
-  if (out_arg) return launch_maxcos_t<DK, true>(pool, n, lab, m_pad, inv_lab, inv_pool, out, out_arg, gap, status, st);
-  return launch_maxcos_t<DK, false>(pool, n, lab, m_pad, inv_lab, inv_pool, out, nullptr, 0.0, status, st);
+  // three waves per SIMD where the registers allow it (16 KiB stages so three
+  // blocks' rings fit the LDS): d <= 128, or d = 64 with the arg-max state
+  constexpr int OCC = DK <= 128 ? 3 : 2, OCC_ARG = DK <= 64 ? 3 : 2;
+  if (out_arg)
+    return launch_maxcos_t<DK, true, OCC_ARG>(pool, n, lab, m_pad, inv_lab, inv_pool, out, out_arg, gap, status, st);
+  return launch_maxcos_t<DK, false, OCC>(pool, n, lab, m_pad, inv_lab, inv_pool, out, nullptr, 0.0, status, st);
 }
 
 }  // namespace
@@ -528,9 +486,16 @@ extern "C" int dal_canon_unit_rows_bf16(const uint16_t* x, int64_t n, int64_t d,
   return DAL_OK;
 }
 
+// Relative to ||x_i|| ||x_l|| (Cauchy-Schwarz; the cosine is <= 1): the
+// d-term dot product of exact bf16 products, summed in fp32 in any order with
+// up to 2u per add, 2 (d - 1) u; the fp32 scalings by 1/||x_l|| (an fp32
+// rounding of the fp64 value) and by 1/||x_i|| with their two products, 4u;
+// the in-kernel ||x_i||^2 (the same kind of d-term fp32 sum, 2 (d - 1) u,
+// halved by the square root) plus the fp64 -> fp32 rounding of 1/||x_i||,
+// (d - 1) u + u.  Total < (3d + 6) u.
 extern "C" double dal_maxcos_error_bound(int64_t d) {
   const double u = 1.0 / 16777216.0;
-  const double k = 2.0 * static_cast<double>(d) + 4.0;
+  const double k = 3.0 * static_cast<double>(d) + 6.0;
   return k * u / (1.0 - k * u) * 1.01 + 1e-12;
 }
 

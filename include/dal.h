@@ -265,8 +265,8 @@ int dal_dw_select(const uint64_t* keys_lo, const uint64_t* keys_hi, const int32_
  * real m carry inv_lab = NaN (ignored).  bf16 MFMA (v_mfma_f32_32x32x16_bf16),
  * fp32 accumulate, row-max epilogue; the n x m matrix is never stored.
  * m_pad % dal_maxcos_label_rows_granule(d) == 0, m_pad <= 4096.  inv_pool
- * (nullable): per-row 1/||x_i||; NULL computes it in-kernel (fp64 sum of
- * squares from the register-resident row fragments).
+ * (nullable): per-row 1/||x_i||; NULL computes it in-kernel (the diagonal of
+ * the register-resident row fragments' own Gram, fp32 sums of exact products).
  * |m_gpu - m_canonical| <= dal_maxcos_error_bound(d) (Cauchy-Schwarz). */
 int64_t dal_maxcos_label_rows_granule(int64_t d);
 double dal_maxcos_error_bound(int64_t d);

@@ -10,6 +10,7 @@
 #   bench[=ARGS]          python bench.py ARGS (',' = space)  -> gpurun_out/bench_<n>.log
 #   stats=TAG[=ARGS]      rocprofv3 --kernel-trace --stats of bench.py ARGS -> gpurun_out/prof_TAG/
 #   pmc=TAG=CTRS[=ARGS]   rocprofv3 --pmc CTRS (',' = space) of bench.py ARGS -> gpurun_out/pmc_TAG/
+#   pmcpy=TAG=CTRS=SCRIPT[=ARGS]  rocprofv3 --pmc CTRS of python SCRIPT ARGS -> gpurun_out/pmc_TAG/
 #   py=SCRIPT[=ARGS]      python SCRIPT ARGS                  -> gpurun_out/py_<n>.log
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -61,6 +62,19 @@ for step in "$@"; do
         python3 -u bench.py ${args//,/ } > gpurun_out/pmc_$tag.log 2>&1
       rc=$?
       echo "[$n] pmc $tag rc=$rc"
+      ;;
+    pmcpy)
+      tag=${rest%%=*}
+      r2=${rest#*=}
+      ctrs=${r2%%=*}
+      r3=${r2#*=}
+      scr=${r3%%=*}
+      args=""
+      [[ "$r3" == *=* ]] && args=${r3#*=}
+      timeout -s KILL 240 rocprofv3 --pmc ${ctrs//,/ } --output-format csv -d gpurun_out/pmc_$tag -o run -- \
+        python3 -u $scr ${args//,/ } > gpurun_out/pmc_$tag.log 2>&1
+      rc=$?
+      echo "[$n] pmcpy $tag rc=$rc"
       ;;
     py)
       scr=${rest%%=*}
