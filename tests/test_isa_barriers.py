@@ -93,7 +93,7 @@ def test_every_gram_barrier_waits_for_lds():
 
 def test_every_maxcos_barrier_waits_for_lds():
     funcs = _functions(_disassemble())
-    ks = {k: v for k, v in funcs.items() if "maxcos2_kernel" in k}
+    ks = {k: v for k, v in funcs.items() if "maxcos_kernel" in k}
     assert ks
     for name, body in ks.items():
         n, bad = _check(body)
