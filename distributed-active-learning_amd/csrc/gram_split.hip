@@ -712,13 +712,23 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym_kernel(
 #ifndef DAL_SYM2_ABL
 #define DAL_SYM2_ABL 0
 #endif
+// Column sums of a pair (P, J) from ONE row per block: 1^T (U_P U_J^T) =
+// sigma_P U_J^T with sigma_P = sum of P's 512 operand rows, formed once per
+// row unit from the resident A fragments.  For each 16-column tile one wave
+// (round robin) issues 3 NKS extra MFMAs with sigma_P as the A operand (all
+// 16 A rows equal, so any output row is the column sum) and stores one value
+// per column: +3 % MFMAs instead of a per-element VALU add and four same-
+// address LDS atomics per column per wave (those cost 7-12 %).
+#ifndef DAL_SYM2_SIGMA
+#define DAL_SYM2_SIGMA 1  // 1: at KS = 32 (measured faster there only), 2: always, 0: never (A/B builds)
+#endif
 
 // One step of a reduce-scatter over the 16 lanes of a DPP row: lanes whose
 // select bit is clear keep v[k] (k < H) summed with their partner's, lanes
 // whose bit is set keep v[k + H]; CTRL is a DPP permutation pairing each lane
 // with a lane of the opposite bit (row_mirror, row_half_mirror, quad swaps).
-template <int H, int CTRL>
-__device__ __forceinline__ void row_reduce_scatter_step(float (&v)[32], bool hi) {
+template <int H, int CTRL, int N = 32>
+__device__ __forceinline__ void row_reduce_scatter_step(float (&v)[N], bool hi) {
 #pragma unroll
   for (int k = 0; k < H; ++k) {
     const float keep = hi ? v[k + H] : v[k];
@@ -726,6 +736,23 @@ __device__ __forceinline__ void row_reduce_scatter_step(float (&v)[32], bool hi)
     v[k] = keep + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, send), CTRL,
                                                                         0xF, 0xF, false));
   }
+}
+
+// Reduce-scatter of N values over the 16 lanes of a DPP row (N = 16: lane li
+// ends with the 16-lane sum of value li; N = 8: of value li & 7).
+template <int N>
+__device__ __forceinline__ void row_sum_scatter(float (&v)[N], int li) {
+  if constexpr (N == 16) {
+    row_reduce_scatter_step<8, 0x140, 16>(v, li & 8);
+  } else {
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+      v[k] += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v[k]), 0x140, 0xF,
+                                                                   0xF, false));
+  }
+  row_reduce_scatter_step<4, 0x141, N>(v, li & 4);
+  row_reduce_scatter_step<2, 0x4E, N>(v, li & 2);
+  row_reduce_scatter_step<1, 0xB1, N>(v, li & 1);
 }
 
 // Lane id recomputed at the point of use (asm volatile: never hoisted out of
@@ -770,11 +797,17 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
     int ns_active, int64_t ldh, int slice_off, int chunk_j, int n_chunks,
     unsigned long long* __restrict__ acc_out, int a_nt, int contig) {
   using C = Sym2Cfg<KS>;
+  constexpr bool SIG = DAL_SYM2_SIGMA == 2 || (DAL_SYM2_SIGMA == 1 && KS == 32);
   using A = SpAcc<16>;
   using acc_t = A::type;
   __shared__ __attribute__((aligned(16))) float4 lds[2 * C::F4];
   __shared__ double colacc[2][256];
   __shared__ double rowacc[C::SB];
+  // sigma_P: per-wave partial sums, then the split row (H' | L', fp16 at 2^-6
+  // of the operand's scale) read as an A fragment (every lane of a DPP row
+  // reads the same 16 B: broadcast)
+  __shared__ float sig_part[SIG ? 4 : 1][SIG ? KS : 1];
+  __shared__ f16x8 sig_row[SIG ? 2 * C::HI : 1];
 
   const int tid = threadIdx.x;
   const int wave = DAL_SYM2_FRESH ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6, lane = tid & 63;
@@ -885,6 +918,41 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
       }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);
+    if constexpr (SIG) {
+      // this wave's 128 rows summed per feature: in lane order over the row
+      // tiles (H then L of each), then over the 16 lanes of the DPP row
+      constexpr int V = C::NKS * 8;
+      float sp[V];
+#pragma unroll
+      for (int c = 0; c < C::NKS; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float t = 0.0f;
+#pragma unroll
+          for (int rt = 0; rt < C::RT; ++rt) {
+            t += static_cast<float>(ah[rt][c][e]);
+            t += static_cast<float>(al[rt][c][e]);
+          }
+          sp[c * 8 + e] = t;
+        }
+      const int fl = static_cast<int>(fresh_lane()), fli = fl & 15, flq = fl >> 4;
+      row_sum_scatter<V>(sp, fli);
+      if (fli < V) sig_part[wave][(fli >> 3) * 32 + flq * 8 + (fli & 7)] = sp[0];
+    }
+  };
+  // after a block_sync that follows load_a: sigma_P = the four waves' partials
+  // (fixed order), scaled by 2^-6 (exact) and split into two fp16 terms
+  auto build_sigma = [&]() {
+    if constexpr (SIG) {
+      if (tid < KS) {
+        const float sg = ((sig_part[0][tid] + sig_part[1][tid]) + sig_part[2][tid]) + sig_part[3][tid];
+        const float s6 = sg * 0x1p-6f;
+        const _Float16 h = static_cast<_Float16>(s6);
+        const _Float16 l = static_cast<_Float16>(s6 - static_cast<float>(h));
+        reinterpret_cast<_Float16*>(sig_row)[tid] = h;
+        reinterpret_cast<_Float16*>(sig_row)[KS + tid] = l;
+      }
+    }
   };
   constexpr float kFold = 0x1p8f;  // units of 2^-24 -> multiples of 2^-32
 
@@ -895,8 +963,12 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
     bol[c] = li * C::SLOTS + ((C::HI + c * C::LG + lq) ^ (li & C::SWZ));
   }
 
-  acc_t mc[2][C::RT];
+  // row-sum chains: two (even / odd column tiles, whose growth gives the
+  // column sums) or, with sigma, one per row tile
+  constexpr int NCH = SIG ? 1 : 2;
+  acc_t mc[NCH][C::RT];
   float tprev[2];
+  f16x8 sgh[SIG ? C::NKS : 1], sgl[SIG ? C::NKS : 1];  // sigma_P fragments
   // one 128-column stage; fresh = first stage after a fold (chains restart)
   // (LDS operands are addressed by index, never through generic pointers:
   // 64-bit flat addresses would cost registers this kernel does not have)
@@ -914,8 +986,11 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
     for (int ct = 0; ct <= C::NCT; ++ct) {
       __builtin_amdgcn_sched_barrier(0);
       if (ct < C::NCT) {
-        const int ch = ct & 1;
-        const bool fresh = fresh_stage && ct < 2;
+        const int ch = ct % NCH;
+        const bool fresh = fresh_stage && ct < NCH;
+        // column tile ct's sums: this wave's turn (wave-uniform branch)
+        const bool sig = SIG && (ct & 3) == wave;
+        acc_t sg = {};
 #pragma unroll
         for (int c = 0; c < C::NKS; ++c) {
           const acc_t zero = {};
@@ -926,18 +1001,25 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
           for (int rt = 0; rt < C::RT; ++rt) mc[ch][rt] = A::mfma(ah[rt][c], bl[c], mc[ch][rt]);
 #pragma unroll
           for (int rt = 0; rt < C::RT; ++rt) mc[ch][rt] = A::mfma(al[rt][c], bh[c], mc[ch][rt]);
+          if (sig) {
+            sg = A::mfma(sgh[c], bh[c], sg);
+            sg = A::mfma(sgh[c], bl[c], sg);
+            sg = A::mfma(sgl[c], bh[c], sg);
+          }
           if (ct + 1 < C::NCT) load_b(c, ct + 1);
         }
+        // every output row of the sigma tile is the column sum (units 2^-18)
+        if (sig && lq == 0) colacc[cbuf][col0 + ct * 16 + li] = static_cast<double>(__builtin_rintf(sg[0] * cmul * 64.0f));
       }
-      if (ct > 0) {
+      if (!SIG && ct > 0 && DAL_SYM2_ABL != 6) {
         const int ch = (ct - 1) & 1;
-        float t0 = mc[ch][0][0], t1 = mc[ch][0][1];
+        float t0 = mc[ch % NCH][0][0], t1 = mc[ch % NCH][0][1];
 #pragma unroll
         for (int rt = 0; rt < C::RT; ++rt) {
 #pragma unroll
           for (int r = rt == 0 ? 2 : 0; r < C::NV; r += 2) {
-            t0 += mc[ch][rt][r];
-            t1 += mc[ch][rt][r + 1];
+            t0 += mc[ch % NCH][rt][r];
+            t1 += mc[ch % NCH][rt][r + 1];
           }
         }
         const float T = t0 + t1;
@@ -953,7 +1035,8 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
 #pragma unroll
           for (int i = 0; i < NM; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // VALU (previous tile's epilogue)
+            if constexpr (!SIG)
+              __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // VALU (previous tile's epilogue)
           }
           __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);    // next tile's B, k-step c
         }
@@ -973,7 +1056,7 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
 #pragma unroll
     for (int rt = 0; rt < C::RT; ++rt)
 #pragma unroll
-      for (int q = 0; q < C::NV; ++q) v[rt * 4 + q] = mc[0][rt][q] + mc[1][rt][q];
+      for (int q = 0; q < C::NV; ++q) v[rt * 4 + q] = NCH == 1 ? mc[0][rt][q] : mc[0][rt][q] + mc[NCH - 1][rt][q];
     row_reduce_scatter_step<16, 0x140>(v, li & 8);  // row_mirror: lane i <-> 15 - i
     row_reduce_scatter_step<8, 0x141>(v, li & 4);   // row_half_mirror: i <-> i ^ 7
     row_reduce_scatter_step<4, 0x4E>(v, li & 2);    // quad_perm [2,3,0,1]: i <-> i ^ 2
@@ -1010,6 +1093,7 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
   int J = jmap(r);
   issue(0, J, 0);
   load_a(P);
+  bool sig_fresh = true;  // sigma_P must be rebuilt (A fragments reloaded)
   int cb = 0;        // colacc buffer of the current pair
   int buf = 0;       // LDS stage of the pair's first stage (alternates per pair when SPP == 1)
   int flushJ = -1;   // column block whose sums wait in colacc[cb ^ 1]
@@ -1029,12 +1113,25 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
     if (flushJ >= 0) flush_cols(cb ^ 1, flushJ);
     if (flushP >= 0) flush_rows(flushP);
     flushP = -1;
+    if (SIG && sig_fresh) {
+      build_sigma();
+      block_sync();
+      sig_fresh = false;
+#pragma unroll
+      for (int c = 0; c < (SIG ? C::NKS : 0); ++c) {
+        const int flq = static_cast<int>(fresh_lane()) >> 4;
+        sgh[c] = sig_row[c * C::LG + flq];
+        sgl[c] = sig_row[C::HI + c * C::LG + flq];
+      }
+    }
     if constexpr (C::SPP == 2) {  // KS 64: two 128-column stages
       issue(1, J, 1);
       compute(0, cmul, cb, 0, true);
+      // one chain: fold per 128-column stage (chain length = two chains per pair)
+      if constexpr (NCH == 1) fold_rows();
       block_sync();
       if (has_next) issue(0, nJ, 0);
-      compute(1, cmul, cb, 128, false);
+      compute(1, cmul, cb, 128, NCH == 1);
     } else {                      // KS 32: one 256-column stage, buffers alternate per pair
       if (has_next) issue(buf ^ 1, nJ, 0);
       compute(buf, cmul, cb, 0, true);
@@ -1051,6 +1148,7 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
     if (new_rows) {
       P = nP;
       if constexpr (DAL_SYM2_ABL != 5) load_a(P);
+      sig_fresh = true;
     }
     r = nr;
     J = nJ;
@@ -1467,7 +1565,11 @@ extern "C" double dal_density_error_bound_sym(int64_t n_cols) {
   //              gamma_1541 * c per column
   //   column side  a tile's column partial is T_k - T_{k-1}, T = sum of the
   //              lane's 16 chain values (k <= 8 tiles into the chain):
-  //              (8 gamma_192 + 15 gamma_15 + u) * c per row
+  //              (8 gamma_192 + 15 gamma_15 + u) * c per row; or (sigma form,
+  //              KS 32: one chain of 16 tiles x 96 products per row, so the
+  //              same row side) <sigma_P, u_j> from sigma_P summed in fp32
+  //              (<= 22 adds) and split in two fp16 terms, one MFMA chain of
+  //              96 products: (gamma_22 + gamma_96 + 3 * 2^-22) * c per row
   //   split + fp32 unit rows  5 * 2^-22;  fixed-point roundings <= 2^-33 each
   // Every column j of a row's density lies on exactly one side of its pair.
   const double u = 1.0 / 8388608.0;  // 2^-23
