@@ -553,13 +553,17 @@ __global__ __launch_bounds__(256) void rerank_maxcos_kernel(const TopkHdr* __res
                                                             int64_t ld, const double* __restrict__ ulabT,
                                                             int64_t m, uint64_t* __restrict__ ckey,
                                                             const int64_t* __restrict__ cidx,
-                                                            double* __restrict__ cpay, int64_t cap) {
+                                                            double* __restrict__ cpay, int64_t cap,
+                                                            int64_t need_k, int32_t* __restrict__ status) {
   __shared__ double su[256][kRrC];  // [f][candidate]
   __shared__ double rb[4][kRrC];
   __shared__ long long ra[4][kRrC];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t c0 = static_cast<int64_t>(blockIdx.x) * kRrC;
   const int64_t count = h->cand_count;
+  if (need_k && c0 == 0 && tid == 0 &&
+      (h->total_lt < static_cast<unsigned long long>(need_k) || h->cand_count > cap))
+    atomicOr(status, DAL_FLAG_SAMPLE_MISS);  // truncated level 1 over capacity: the caller re-runs exactly
   if (c0 >= count) {
     if (tid < kRrC && c0 + tid < cap) ckey[c0 + tid] = DAL_KEY_NONE;
     return;
@@ -923,19 +927,21 @@ extern "C" size_t dal_maxcos_select_workspace_bytes(int64_t n, int64_t k, int64_
 
 extern "C" int dal_maxcos_select(const uint64_t* keys_lo, const uint64_t* keys_hi, int64_t n, int64_t k,
                                  int64_t idx_base, const uint16_t* pool, int64_t d, int64_t ld,
-                                 const double* ulab, int64_t m, int64_t cap, void* ws, size_t ws_bytes,
+                                 const double* ulab, int64_t m, int64_t cap, int32_t level1_passes, void* ws,
+                                 size_t ws_bytes,
                                  int64_t* out_idx, double* out_scores, uint64_t* out_keys,
                                  int32_t* dev_status, dal_stream_t stream) {
   if (!keys_lo || !keys_hi || !pool || !ulab || !ws || !out_idx || !out_scores || !dev_status)
     return DAL_ERR_ARG;
   if (d < 1 || d > 256 || ld < d || m < 1) return DAL_ERR_SHAPE;
   hipStream_t st = as_stream(stream);
-  auto rerank = [&](TopkHdr* h, uint64_t* ckey, int64_t* cidx, double* cpay, int64_t cp, int64_t) {
+  auto rerank = [&](TopkHdr* h, uint64_t* ckey, int64_t* cidx, double* cpay, int64_t cp, int64_t need_k) {
     hipLaunchKernelGGL(rerank_maxcos_kernel, dim3(static_cast<unsigned>(ceil_div(cp, kRrC))), dim3(256), 0, st,
-                       h, idx_base, pool, static_cast<int>(d), ld, ulab, m, ckey, cidx, cpay, cp);
+                       h, idx_base, pool, static_cast<int>(d), ld, ulab, m, ckey, cidx, cpay, cp, need_k,
+                       dev_status);
   };
-  return select_with_rerank(keys_lo, keys_hi, n, k, idx_base, cap, 0, ws, ws_bytes, rerank, out_idx, out_scores,
-                            out_keys, dev_status, st);
+  return select_with_rerank(keys_lo, keys_hi, n, k, idx_base, cap, level1_passes, ws, ws_bytes, rerank, out_idx,
+                            out_scores, out_keys, dev_status, st);
 }
 
 // Interval keys of fp32 values: lo/hi = keys of the pessimistic/optimistic

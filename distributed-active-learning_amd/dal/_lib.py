@@ -93,7 +93,7 @@ SIGNATURES = {
                                       c_void_p, c_void_p]),
     "dal_maxcos_select_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
     "dal_maxcos_select": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64,
-                                  c_int64, c_void_p, c_int64, c_int64, c_void_p, c_size_t, c_void_p,
+                                  c_int64, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_size_t, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p]),
     "dal_sort_pairs": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
                                c_void_p, c_void_p]),

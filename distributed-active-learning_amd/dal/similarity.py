@@ -113,8 +113,8 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
     import torch
 
     from . import _lib
-    from ._lib import DAL_ASCENDING, DAL_FLAG_CAND_OVERFLOW, DAL_ROW_CANDIDATE
-    from .engine import Selection, _as_index, _ptr, _stream, candidate_cap, workspace
+    from ._lib import DAL_ASCENDING, DAL_FLAG_CAND_OVERFLOW, DAL_FLAG_SAMPLE_MISS, DAL_ROW_CANDIDATE
+    from .engine import LEVEL1_PASSES, Selection, _as_index, _ptr, _stream, candidate_cap, workspace
 
     lib = _lib.load()
     x, dev = _bf16_pool(pool, device)
@@ -128,6 +128,7 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
     mx = torch.empty(n, dtype=torch.float32, device=dev)
     _lib.call("dal_max_cosine", _ptr(x), n, d, _ptr(lab.rows), lab.m_pad, _ptr(lab.inv), 0,
               _ptr(mx), 0, _ptr(status), _stream(dev))
+    in_range = None  # device count of the candidates inside this shard (read with the status)
     if candidates is None:
         flags = torch.full((n,), DAL_ROW_CANDIDATE, dtype=torch.uint8, device=dev)
         cand = torch.arange(n, device=dev)
@@ -137,9 +138,11 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
         gidx = _as_index(candidates, dev)
         _lib.call("dal_mark_rows", _ptr(gidx), int(gidx.shape[0]), int(row_base), n, DAL_ROW_CANDIDATE,
                   _ptr(flags), _stream(dev))
-        cand = gidx - row_base
-        cand = cand[(cand >= 0) & (cand < n)]  # global candidates of other shards are not ours
+        cand = gidx - row_base if row_base else gidx
+        # an upper bound until the status read: global candidates of other
+        # shards are not ours (filtered below, off the common path)
         n_cand = int(cand.shape[0])
+        in_range = ((cand >= 0) & (cand < n)).sum(dtype=torch.int32).reshape(1)
         if n_cand == 0:
             return Selection(scores=mx[cand], indices=torch.empty(0, dtype=torch.int64, device=dev),
                              selected_scores=torch.empty(0, dtype=torch.float64, device=dev))
@@ -149,21 +152,43 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
     _lib.call("dal_interval_keys_f32", _ptr(mx), n, float(lib.dal_maxcos_error_bound(d)), _ptr(flags),
               DAL_ASCENDING, _ptr(lo), _ptr(hi), _stream(dev))
     cap = candidate_cap(n, kk)
+    passes = LEVEL1_PASSES if cap <= _lib.DAL_SORT_CAP_PAYLOAD else 0
     while True:
         wsb = int(lib.dal_maxcos_select_workspace_bytes(n, kk, cap))
         ws, wsp = workspace(wsb, dev)
         out_idx = torch.empty(kk, dtype=torch.int64, device=dev)
         out_sc = torch.empty(kk, dtype=torch.float64, device=dev)
         _lib.call("dal_maxcos_select", _ptr(lo), _ptr(hi), n, kk, int(row_base), _ptr(x), d, d,
-                  _ptr(lab.unit64_t), lab.m, cap, wsp, wsb, _ptr(out_idx), _ptr(out_sc), 0,
+                  _ptr(lab.unit64_t), lab.m, cap, passes, wsp, wsb, _ptr(out_idx), _ptr(out_sc), 0,
                   _ptr(status), _stream(dev))
-        st = int(status.item()) | int(lab.status.item())
+        # one host read for the status words (and the shard's candidate count)
+        words = [status, lab.status] + ([in_range] if in_range is not None else [])
+        vals = torch.cat(words).tolist()
+        st = vals[0] | vals[1]
         if st & 1:
             raise ValueError("zero-norm row: cosine undefined")
+        if in_range is not None and vals[2] < n_cand:
+            # candidates outside this shard: filter and redo with the true count
+            # (kk must not exceed it, or key-NONE rows would fill the list)
+            cand = cand[(cand >= 0) & (cand < n)]
+            n_cand, in_range = int(cand.shape[0]), None
+            if n_cand == 0:
+                return Selection(scores=mx[cand], indices=torch.empty(0, dtype=torch.int64, device=dev),
+                                 selected_scores=torch.empty(0, dtype=torch.float64, device=dev))
+            kk = min(int(k), n_cand)
+            cap = candidate_cap(n, kk)
+            passes = LEVEL1_PASSES if cap <= _lib.DAL_SORT_CAP_PAYLOAD else 0
+            status.zero_()
+            continue
+        if st & DAL_FLAG_SAMPLE_MISS:  # the truncated level 1 overflowed: exact level 1
+            passes = 0
+            status.zero_()
+            continue
         if cap >= n or not (st & DAL_FLAG_CAND_OVERFLOW):
             break
         status.zero_()
         cap = min(n, cap * 4)
+        passes = 0
     return Selection(scores=mx[cand], indices=out_idx, selected_scores=out_sc)
 
 

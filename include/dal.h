@@ -298,11 +298,14 @@ int dal_interval_keys_f32(const float* values, int64_t n, double err, const uint
 /* Diversity selection: the k rows with the smallest canonical fp64 max-cosine
  * (ties -> lower index), from interval keys of dal_max_cosine's output;
  * ulab = canonical fp64 unit rows of the m labeled rows, feature-major
- * [d][m] (dal_canon_unit_rows_bf16 with feature_major = 1); d <= 256.  Same candidate/re-rank contract as dal_dw_select. */
+ * [d][m] (dal_canon_unit_rows_bf16 with feature_major = 1); d <= 256.  Same candidate/re-rank contract
+ * as dal_dw_select, including level1_passes (0 = exact radix level 1; 1-5 =
+ * truncated, DAL_FLAG_SAMPLE_MISS when its candidates overflow cap <= 4096). */
 size_t dal_maxcos_select_workspace_bytes(int64_t n, int64_t k, int64_t cap);
 int dal_maxcos_select(const uint64_t* keys_lo, const uint64_t* keys_hi, int64_t n, int64_t k,
                       int64_t idx_base, const uint16_t* pool, int64_t d, int64_t ld,
-                      const double* ulab, int64_t m, int64_t cap, void* ws, size_t ws_bytes,
+                      const double* ulab, int64_t m, int64_t cap, int32_t level1_passes, void* ws,
+                      size_t ws_bytes,
                       int64_t* out_idx, double* out_scores, uint64_t* out_keys,
                       int32_t* dev_status, dal_stream_t stream);
 

@@ -5,7 +5,7 @@
 #
 # STEP (run in order, each under its own time limit; the first failure ends
 # the call -- no GPU step runs after a fault, abort or timeout):
-#   tests[=EXPR]          pytest -m gpu (optionally -k EXPR)  -> gpurun_out/pytest_gpu.log
+#   tests[=EXPR]          pytest -m gpu (optionally -k EXPR, ',' = space) -> gpurun_out/pytest_gpu.log
 #   smoke                 __graft_entry__.smoke()             -> gpurun_out/smoke.log
 #   bench[=ARGS]          python bench.py ARGS (',' = space)  -> gpurun_out/bench_<n>.log
 #   stats=TAG[=ARGS]      rocprofv3 --kernel-trace --stats of bench.py ARGS -> gpurun_out/prof_TAG/
@@ -25,7 +25,7 @@ for step in "$@"; do
   case "$kind" in
     tests)
       k=()
-      [ -n "$rest" ] && k=(-k "$rest")
+      [ -n "$rest" ] && k=(-k "${rest//,/ }")
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread "${k[@]}" \
         > gpurun_out/pytest_gpu.log 2>&1
       rc=$?

@@ -86,3 +86,29 @@ def test_diversity_select_scale(cuda):
     ref_idx, ref_sc = O.diversity_select_canonical(X, L, k, candidates=cand)
     assert np.array_equal(_np(sel.indices), ref_idx)
     assert np.array_equal(_np(sel.selected_scores), ref_sc)
+
+
+@pytest.mark.parametrize("case", ["bucket_overflow", "foreign_candidates"])
+def test_diversity_select_fallbacks(cuda, case):
+    """The truncated level 1 overflowing its 4,096 slots (5,000 identical
+    least-similar rows: DAL_FLAG_SAMPLE_MISS, exact re-run), and candidate
+    lists holding indices outside the pool (filtered after the status read,
+    then re-selected with the true count)."""
+    from dal import similarity as sim
+
+    n, d, m, k = 12000, 64, 256, 100
+    X = O.bf16_round(O.synthetic_pool(n, d, seed=11))
+    L = np.arange(m)
+    cand = np.arange(m, n)
+    if case == "bucket_overflow":
+        far = np.zeros(d, dtype=np.float32)
+        far[0] = 1.0  # a corner of the positive orthant: every copy has the same, smallest max-cosine
+        X[3000:8000] = O.bf16_round(far[None, :])
+    else:
+        cand = np.concatenate([cand, np.arange(n, n + 500)])  # not rows of this pool
+    sel = sim.diversity_select(X, L, k, candidates=cand, device=cuda)
+    ref_idx, ref_sc = O.diversity_select_canonical(X, L, k, candidates=cand[cand < n])
+    assert np.array_equal(_np(sel.indices), ref_idx)
+    assert np.array_equal(_np(sel.selected_scores), ref_sc)
+    if case == "bucket_overflow":
+        assert (ref_idx == np.arange(3000, 3100)).all()  # ties -> lower index
