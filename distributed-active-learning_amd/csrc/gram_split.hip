@@ -1073,6 +1073,10 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
     slot = 0.0;
   };
   auto flush_cols = [&](int cbuf, int Jf) {
+    if constexpr (DAL_SYM2_ABL == 7) {  // no global column flush
+      colacc[cbuf][tid] = 0.0;
+      return;
+    }
     flush_one(colacc[cbuf][tid], static_cast<int64_t>(Jf) * 256 + tid);
   };
   auto flush_rows = [&](int Pf) {
