@@ -68,7 +68,8 @@ __device__ __forceinline__ double density_pow_err(double d, double derr, double 
 
 template <bool X_LDS, bool F_LDS>
 __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs A, int R, int tpr,
-                                                                      int x_floats, bool vec4) {
+                                                                      int x_floats, bool vec4, bool pad4,
+                                                                      bool pre) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* xs = reinterpret_cast<float*>(smem);
   const int n_inner = (1 << A.depth) - 1;
@@ -84,8 +85,22 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
     inner = fs;
     leaf = ls;
   }
-  const int xstride = A.d + 1;
+  // row stride in LDS: d + 1 words for scalar staging; with 16-B staging
+  // d + 4 (rows stay 16-B aligned, one ds_write_b128 per load, consecutive
+  // lanes on consecutive banks; rows of a wave start 4 banks apart)
+  const int xstride = A.d + (pad4 ? 4 : 1);
   const int64_t row0 = static_cast<int64_t>(blockIdx.x) * R;
+  const int r = tid / tpr, sub = tid - r * tpr;
+  const int64_t row = row0 + r;
+  const bool live = r < R && row < A.n;
+  // the row leader's epilogue inputs are loaded with the tile (one HBM
+  // latency per block instead of two)
+  uint8_t fl_pre = DAL_ROW_CANDIDATE;
+  long long dens_pre = 0;
+  if (pre && live && sub == 0) {
+    if (A.flags) fl_pre = A.flags[row];
+    if (A.dkind) dens_pre = static_cast<const long long*>(A.density)[row];
+  }
   if (X_LDS) {
     const int rows_here = static_cast<int>(min(static_cast<int64_t>(R), A.n - row0));
     if (vec4) {
@@ -110,10 +125,14 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
           if (e < total) {
             const int r = e / q, c = e - r * q;
             float* dst = xs + r * xstride + 4 * c;
-            dst[0] = v[j].x;
-            dst[1] = v[j].y;
-            dst[2] = v[j].z;
-            dst[3] = v[j].w;
+            if (pad4) {
+              *reinterpret_cast<v4f*>(dst) = v[j];
+            } else {
+              dst[0] = v[j].x;
+              dst[1] = v[j].y;
+              dst[2] = v[j].z;
+              dst[3] = v[j].w;
+            }
           }
         }
       }
@@ -126,9 +145,6 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
   }
   __syncthreads();
 
-  const int r = tid / tpr, sub = tid - r * tpr;
-  const int64_t row = row0 + r;
-  const bool live = r < R && row < A.n;
   const float* xrow = X_LDS ? xs + r * xstride : A.x + (live ? row : 0) * A.ldx;
 
   int v = 0;
@@ -162,12 +178,12 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
   for (int o = 1; o < tpr; o <<= 1) v += __shfl_xor(v, o);
   if (!live || sub != 0) return;
 
-  const uint8_t fl = A.flags ? A.flags[row] : DAL_ROW_CANDIDATE;
+  const uint8_t fl = pre ? fl_pre : A.flags ? A.flags[row] : DAL_ROW_CANDIDATE;
   const double e = A.lut[v];
   double s, err = 0.0;
   if (A.dkind) {
-    double d = A.dkind == 1 ? from_fixed(static_cast<const long long*>(A.density)[row])
-                            : static_cast<const double*>(A.density)[row];
+    const long long draw = pre ? dens_pre : static_cast<const long long*>(A.density)[row];
+    double d = A.dkind == 1 ? from_fixed(draw) : __builtin_bit_cast(double, draw);
     if (fl & DAL_ROW_EXCLUDED) d = __builtin_nan("");
     s = e * density_pow(d, A.beta);
     if (A.dkind == 1 && e == e && e != 0.0 && d == d) {
@@ -227,7 +243,12 @@ extern "C" int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ld
     while (R > 1 && kForestThreads / R < tpr_min) R >>= 1;
   }
   const int tpr = kForestThreads / R;
-  const int x_floats = x_lds ? R * static_cast<int>(d + 1) : 0;
+  const bool vec4 = (d % 4 == 0) && (ldx % 4 == 0) && (reinterpret_cast<uintptr_t>(x) % 16 == 0);
+  bool pad4 = vec4;
+  if (const char* e = getenv("DAL_FOREST_PAD4")) pad4 = vec4 && atoi(e) != 0;  // timing knob (A/B runs)
+  bool pre = true;
+  if (const char* e = getenv("DAL_FOREST_PREFETCH")) pre = atoi(e) != 0;  // timing knob (A/B runs)
+  const int x_floats = x_lds ? R * static_cast<int>(d + (pad4 ? 4 : 1)) : 0;
   const int64_t n_inner = (int64_t{1} << depth) - 1, n_leaf = int64_t{1} << depth;
   const int64_t f_bytes = n_trees * (n_inner * 8 + n_leaf);
   const bool f_lds = f_bytes <= 65536;
@@ -235,7 +256,6 @@ extern "C" int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ld
   size_t smem = static_cast<size_t>(xf) * 4 + (f_lds ? static_cast<size_t>(f_bytes) : 0);
   if (smem == 0) smem = 16;
   const dim3 grid(static_cast<unsigned>(ceil_div(n, R)));
-  const bool vec4 = (d % 4 == 0) && (ldx % 4 == 0) && (reinterpret_cast<uintptr_t>(x) % 16 == 0);
   hipStream_t st = as_stream(stream);
 #define DAL_FOREST_LAUNCH(XL, FL)                                                                   \
   do {                                                                                              \
@@ -244,7 +264,7 @@ extern "C" int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ld
         hipSuccess)                                                                                 \
       return DAL_ERR_HIP;                                                                           \
     hipLaunchKernelGGL((forest_score_kernel<XL, FL>), grid, dim3(kForestThreads), smem, st, A, R,  \
-                       tpr, xf, vec4);                                                              \
+                       tpr, xf, vec4, pad4, pre);                                                              \
   } while (0)
   if (x_lds && f_lds) DAL_FOREST_LAUNCH(true, true);
   else if (x_lds) DAL_FOREST_LAUNCH(true, false);
