@@ -51,4 +51,28 @@ __device__ __forceinline__ double from_fixed(long long a) {
   return static_cast<double>(a) * (1.0 / DAL_FIXED_SCALE);
 }
 
+// Internal hook of dal_dw_step into dal_forest_score's kernel (forest.hip):
+// status_reset (nullable) is zeroed by the first thread, before any later
+// kernel of the step can raise a flag (a replayed step starts clean).
+struct ForestStepHooks {
+  int32_t* status_reset = nullptr;
+};
+
+int forest_score_launch(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
+                        const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
+                        const void* density, int density_kind, double density_err, const uint8_t* row_flags,
+                        double beta, int order, int32_t* votes, double* scores, uint64_t* keys,
+                        uint64_t* keys_hi, const ForestStepHooks& hooks, hipStream_t st);
+
+// dal_dw_step with the plan's publishing hooks (topk.hip, SortTail): the
+// selection is also written to *out_slot (a host-mapped word holding a device
+// address; nullable) and the final status word to *status_mirror (host-mapped).
+int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner, const uint8_t* leaf,
+                 int32_t n_trees, int32_t depth, const double* lut, const int64_t* density_fixed, double density_err,
+                 const uint8_t* row_flags, double beta, int64_t idx_base, const double* norm64, const double* colsum,
+                 int64_t k, int64_t cap, int32_t level1_passes, uint32_t step_flags, void* ws, size_t ws_bytes,
+                 int32_t* votes, double* scores, uint64_t* keys_lo, uint64_t* keys_hi, int64_t* out_idx,
+                 double* out_scores, uint64_t* out_keys, int32_t* dev_status, dal_event_t colsum_ready,
+                 dal_stream_t stream, int64_t* const* out_slot, int32_t* status_mirror);
+
 }  // namespace dal

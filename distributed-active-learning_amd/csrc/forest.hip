@@ -51,7 +51,9 @@ struct ForestArgs {
   double* scores;
   uint64_t* keys;
   uint64_t* keys_hi;
+  ForestStepHooks hooks;  // dal_dw_step only (common.hpp)
 };
+
 
 __device__ __forceinline__ double density_pow(double d, double beta) {
   return beta == 1.0 ? d : pow(d, beta);
@@ -72,6 +74,7 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
                                                                       bool pre) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* xs = reinterpret_cast<float*>(smem);
+  if (A.hooks.status_reset && blockIdx.x == 0 && threadIdx.x == 0) *A.hooks.status_reset = 0;
   const int n_inner = (1 << A.depth) - 1;
   const int n_leaf = 1 << A.depth;
   const int2* inner = A.inner;
@@ -204,14 +207,13 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
 }  // namespace
 }  // namespace dal
 
-using namespace dal;
+namespace dal {
 
-extern "C" int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
-                                const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
-                                const void* density, int density_kind, double density_err,
-                                const uint8_t* row_flags,
-                                double beta, int order, int32_t* votes, double* scores, uint64_t* keys,
-                                uint64_t* keys_hi, dal_stream_t stream) {
+int forest_score_launch(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
+                        const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
+                        const void* density, int density_kind, double density_err, const uint8_t* row_flags,
+                        double beta, int order, int32_t* votes, double* scores, uint64_t* keys,
+                        uint64_t* keys_hi, const ForestStepHooks& hooks_in, hipStream_t st) {
   if (!x || !inner || !leaf || !lut || !votes || !scores || !keys) return DAL_ERR_ARG;
   if (order != DAL_ASCENDING && order != DAL_DESCENDING) return DAL_ERR_ARG;
   if (density_kind < 0 || density_kind > 2 || (density_kind && !density)) return DAL_ERR_ARG;
@@ -220,7 +222,7 @@ extern "C" int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ld
   if (n == 0) return DAL_OK;
   ForestArgs A{x, n, static_cast<int>(d), ldx, reinterpret_cast<const int2*>(inner), leaf, n_trees,
                depth, lut, density_kind ? density : nullptr, density_kind, density_err, row_flags, beta,
-               order, votes, scores, keys, keys_hi};
+               order, votes, scores, keys, keys_hi, hooks_in};
   // rows per block: stage up to ~16 KiB of pool rows in LDS.  Small tiles keep
   // more blocks (and their loads) resident per CU: at 2M x 256 a 16 KiB tile
   // runs 0.52 ms vs 0.60 (32 KiB) / 0.85 (96 KiB) / 0.75 (8 KiB); neutral at
@@ -254,9 +256,9 @@ extern "C" int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ld
   const bool f_lds = f_bytes <= 65536;
   const int xf = static_cast<int>(round_up(x_floats, 4));  // forest region 16-B aligned
   size_t smem = static_cast<size_t>(xf) * 4 + (f_lds ? static_cast<size_t>(f_bytes) : 0);
+  const int64_t blocks = ceil_div(n, R);
   if (smem == 0) smem = 16;
-  const dim3 grid(static_cast<unsigned>(ceil_div(n, R)));
-  hipStream_t st = as_stream(stream);
+  const dim3 grid(static_cast<unsigned>(blocks));
 #define DAL_FOREST_LAUNCH(XL, FL)                                                                   \
   do {                                                                                              \
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(forest_score_kernel<XL, FL>),             \
@@ -264,7 +266,7 @@ extern "C" int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ld
         hipSuccess)                                                                                 \
       return DAL_ERR_HIP;                                                                           \
     hipLaunchKernelGGL((forest_score_kernel<XL, FL>), grid, dim3(kForestThreads), smem, st, A, R,  \
-                       tpr, xf, vec4, pad4, pre);                                                              \
+                       tpr, xf, vec4, pad4, pre);                                                            \
   } while (0)
   if (x_lds && f_lds) DAL_FOREST_LAUNCH(true, true);
   else if (x_lds) DAL_FOREST_LAUNCH(true, false);
@@ -273,4 +275,19 @@ extern "C" int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ld
 #undef DAL_FOREST_LAUNCH
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
+}
+
+}  // namespace dal
+
+using namespace dal;
+
+extern "C" int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
+                                const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
+                                const void* density, int density_kind, double density_err,
+                                const uint8_t* row_flags,
+                                double beta, int order, int32_t* votes, double* scores, uint64_t* keys,
+                                uint64_t* keys_hi, dal_stream_t stream) {
+  return forest_score_launch(x, n, d, ldx, inner, leaf, n_trees, depth, lut, density, density_kind, density_err,
+                             row_flags, beta, order, votes, scores, keys, keys_hi, ForestStepHooks{},
+                             as_stream(stream));
 }

@@ -1,0 +1,146 @@
+// Warm-step plan: one density-weighted AL iteration (dal_dw_step) captured
+// once as a hipGraph over caller-owned static buffers and replayed by
+// dal_dw_plan_run, which also does the per-step refresh (base flags -> step
+// flags, mark the unlabeled rows); the graph's last kernel writes the
+// selection into the caller's fresh buffer and the status word into
+// host-mapped memory -- the host side of a warm step is ONE call and nothing
+// but the stream sync follows the replay.
+//
+// Reference: the body of density_weighting.py:133-176 (per iteration: T x
+// predict, entropy x density, sortBy, take(window_size)) with the proximity
+// matrix of :58-100 cached across iterations, as the reference does.
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <new>
+
+#include "common.hpp"
+
+// Host-mapped words the graph's last kernel publishes into: the selection's
+// destination (a fresh tensor each step, set by the host before the replay)
+// and the final status word.  No copy launches follow the graph.
+struct PlanSlot {
+  int64_t* out;
+  int32_t status;
+  int32_t pad;
+};
+
+struct dal_dw_plan {
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  const uint8_t* base_flags = nullptr;
+  uint8_t* flags = nullptr;
+  int64_t n = 0, row_base = 0, k = 0;
+  const int64_t* out_pair = nullptr;  // device [2k]: selected indices | selected score bits
+  int32_t* dev_status = nullptr;
+  PlanSlot* slot = nullptr;       // host view
+  PlanSlot* slot_dev = nullptr;   // the same words as the device addresses them
+  bool timing = false;            // DAL_PLAN_TIMING=1: host time per phase, printed by destroy
+  double t_refresh = 0, t_launch = 0, t_sync = 0;
+  int64_t runs = 0;
+};
+
+static double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+using namespace dal;
+
+extern "C" int dal_dw_plan_create(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
+                                  const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
+                                  const int64_t* density_fixed, double density_err, const uint8_t* base_flags,
+                                  uint8_t* flags, double beta, int64_t idx_base, const double* norm64,
+                                  const double* colsum, int64_t k, int64_t cap, int32_t level1_passes, void* ws,
+                                  size_t ws_bytes, int32_t* votes, double* scores, uint64_t* keys_lo,
+                                  uint64_t* keys_hi, int64_t* out_pair, uint64_t* out_keys, int32_t* dev_status,
+                                  dal_stream_t stream, dal_dw_plan_t** plan_out) {
+  if (!plan_out || !base_flags || !flags || !out_pair || !ws) return DAL_ERR_ARG;
+  *plan_out = nullptr;
+  if (n < 1 || k < 1) return DAL_ERR_SHAPE;
+  hipStream_t st = as_stream(stream);
+  // the fused step leaves its level-1 header zero after every replay: zero it once
+  if (hipMemsetAsync(ws, 0, ws_bytes, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+    return DAL_ERR_HIP;
+  dal_dw_plan* p = new (std::nothrow) dal_dw_plan;
+  if (!p) return DAL_ERR_HIP;
+  hipStream_t cs = nullptr;
+  int rc = DAL_OK;
+  if (hipHostMalloc(reinterpret_cast<void**>(&p->slot), sizeof(PlanSlot), hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&p->slot_dev), p->slot, 0) != hipSuccess)
+    rc = DAL_ERR_HIP;
+  if (!rc) {
+    p->slot->out = nullptr;
+    p->slot->status = 0;
+  }
+  if (!rc && hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) rc = DAL_ERR_HIP;
+  if (!rc && hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) != hipSuccess) rc = DAL_ERR_HIP;
+  if (!rc) {
+    const int step_rc = dw_step_impl(x, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, density_err,
+                                     flags, beta, idx_base, norm64, colsum, k, cap, level1_passes,
+                                     DAL_STEP_RESET_STATUS | DAL_STEP_WS_CLEAN, ws, ws_bytes, votes, scores, keys_lo,
+                                     keys_hi, out_pair, reinterpret_cast<double*>(out_pair + k), out_keys,
+                                     dev_status, nullptr, cs, &p->slot_dev->out, &p->slot_dev->status);
+    const hipError_t end = hipStreamEndCapture(cs, &p->graph);
+    rc = step_rc ? step_rc : (end != hipSuccess ? DAL_ERR_HIP : DAL_OK);
+  }
+  if (!rc && hipGraphInstantiate(&p->exec, p->graph, nullptr, nullptr, 0) != hipSuccess) rc = DAL_ERR_HIP;
+  if (cs) (void)hipStreamDestroy(cs);
+  if (rc) {
+    dal_dw_plan_destroy(p);
+    return rc;
+  }
+  p->base_flags = base_flags;
+  p->flags = flags;
+  p->n = n;
+  p->row_base = idx_base;
+  p->k = k;
+  p->out_pair = out_pair;
+  p->dev_status = dev_status;
+  const char* tm = getenv("DAL_PLAN_TIMING");
+  p->timing = tm && atoi(tm) != 0;
+  *plan_out = p;
+  return DAL_OK;
+}
+
+extern "C" int dal_dw_plan_run(dal_dw_plan_t* p, const int64_t* unl, int64_t n_unl, int64_t* out_copy,
+                               int32_t* status_out, dal_stream_t stream) {
+  if (!p || !status_out || (!unl && n_unl)) return DAL_ERR_ARG;
+  hipStream_t st = as_stream(stream);
+  const double t0 = p->timing ? now_us() : 0.0;
+  if (hipMemcpyAsync(p->flags, p->base_flags, static_cast<size_t>(p->n), hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return DAL_ERR_HIP;
+  int rc = dal_mark_rows(unl, n_unl, p->row_base, p->n, DAL_ROW_CANDIDATE, p->flags, stream);
+  if (rc) return rc;
+  volatile PlanSlot* slot = p->slot;
+  slot->out = out_copy;
+  slot->status = -1;  // overwritten by the graph's last kernel
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  const double t1 = p->timing ? now_us() : 0.0;
+  if (hipGraphLaunch(p->exec, st) != hipSuccess) return DAL_ERR_HIP;
+  const double t2 = p->timing ? now_us() : 0.0;
+  if (hipStreamSynchronize(st) != hipSuccess) return DAL_ERR_HIP;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  if (p->timing) {
+    const double t3 = now_us();
+    p->t_refresh += t1 - t0;
+    p->t_launch += t2 - t1;
+    p->t_sync += t3 - t2;
+    ++p->runs;
+  }
+  const int32_t v = slot->status;
+  if (v < 0) return DAL_ERR_HIP;  // the step did not publish its status
+  *status_out = v;
+  return DAL_OK;
+}
+
+extern "C" void dal_dw_plan_destroy(dal_dw_plan_t* p) {
+  if (!p) return;
+  if (p->timing && p->runs)
+    fprintf(stderr, "dal_dw_plan: %lld runs, host us per run: refresh %.1f, graph launch %.1f, sync %.1f\n",
+            static_cast<long long>(p->runs), p->t_refresh / p->runs, p->t_launch / p->runs, p->t_sync / p->runs);
+  if (p->exec) (void)hipGraphExecDestroy(p->exec);
+  if (p->graph) (void)hipGraphDestroy(p->graph);
+  if (p->slot) (void)hipHostFree(p->slot);
+  delete p;
+}

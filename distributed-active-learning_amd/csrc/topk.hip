@@ -415,7 +415,72 @@ __global__ __launch_bounds__(kRadixThreads) void compact_write_kernel(
   }
 }
 
+// ------------------------------------------------------------- re-rank ----
+// Canonical fp64 density-weighted score of a row (bit-identical to
+// oracle.density_canonical: x/norm, then sequential mul+add over features;
+// the library is compiled with -ffp-contract=off).
+struct DwRerank {
+  const float* x;
+  int d;
+  int64_t ldx;
+  const double* norm64;
+  const double* colsum;
+  const double* lut;
+  const int32_t* votes;
+  const uint8_t* flags;
+  double beta;
+};
+
+// The canonical score of local row i, computed by a whole wave (every lane
+// calls it with the same row): lane f forms the rounded product
+// (x_f / norm) * s_f -- the divisions and loads run in parallel -- and the
+// sequential sum over f takes the products from the lanes in order (the
+// oracle's operations in the oracle's order).  false (NONE key, NaN payload)
+// when the row is not an unlabeled candidate (a shard with < k candidates).
+__device__ __forceinline__ double readlane_f64(double v, int l) {  // l wave-uniform
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(b), l));
+  const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(b >> 32), l));
+  return __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
+}
+
+__device__ __forceinline__ bool dw_canonical_score_wave(const DwRerank& R, int64_t i, double& s,
+                                                        double lut_lane = 0.0, int n_lut = 0) {
+  const int lane = threadIdx.x & 63;
+  const uint8_t fl = R.flags ? R.flags[i] : DAL_ROW_CANDIDATE;
+  const double nr = R.norm64[i];
+  const int v = R.votes[i];
+  const float* xr = R.x + i * R.ldx;
+  double acc = 0.0;
+  for (int f0 = 0; f0 < R.d; f0 += 64) {
+    const int f = f0 + lane;
+    double p = 0.0;
+    if (f < R.d) {
+      const double u = static_cast<double>(xr[f]) / nr;
+      p = u * R.colsum[f];
+    }
+    const int m = R.d - f0 < 64 ? R.d - f0 : 64;
+    for (int q = 0; q < m; ++q) acc = acc + readlane_f64(p, q);  // v_readlane: no LDS round trip
+  }
+  if (!(fl & DAL_ROW_CANDIDATE)) {
+    s = __builtin_nan("");
+    return false;
+  }
+  if (fl & DAL_ROW_EXCLUDED) acc = __builtin_nan("");
+  // n_lut > 0: lane l holds lut[l] (T < 64), no dependent load on the vote
+  const double e = v < n_lut ? readlane_f64(lut_lane, v) : R.lut[v];
+  s = e * (R.beta == 1.0 ? acc : pow(acc, R.beta));
+  return true;
+}
+
 // ---------------------------------------------------- truncated level 1 ----
+// dal_dw_step's fused re-rank target (append_rerank_kernel).
+struct AppendRerank {
+  DwRerank R;
+  uint64_t* ckey;
+  double* cpay;
+};
+
 __global__ __launch_bounds__(kRadixThreads) void threshold_append_kernel(
     const uint64_t* __restrict__ keys_lo, const uint64_t* __restrict__ keys_hi, int64_t n, int64_t idx_base,
     int passes, TopkHdr* __restrict__ h, int64_t* __restrict__ cidx, int64_t cap) {
@@ -475,61 +540,93 @@ __global__ __launch_bounds__(kRadixThreads) void threshold_append_kernel(
   }
 }
 
-// ------------------------------------------------------------- re-rank ----
-// Canonical fp64 density-weighted score of each candidate (bit-identical to
-// oracle.density_canonical: x/norm, then sequential mul+add over features;
-// the library is compiled with -ffp-contract=off).
-__global__ __launch_bounds__(256) void rerank_kernel(const TopkHdr* __restrict__ h, int64_t idx_base,
-                                                     const float* __restrict__ x, int d, int64_t ldx,
-                                                     const double* __restrict__ norm64,
-                                                     const double* __restrict__ colsum,
-                                                     const double* __restrict__ lut,
-                                                     const int32_t* __restrict__ votes,
-                                                     const uint8_t* __restrict__ flags, double beta,
+// dal_dw_step's candidate search + re-rank: one key per thread (grid-stride),
+// the first keys and the LUT fetched before the level-1 state is resolved,
+// each wave's slot reservation issued before it scores its candidates (the
+// atomic's round trip overlaps the candidate loads), each candidate scored by
+// the whole wave and stored by its own lane.
+__global__ __launch_bounds__(kRadixThreads) void append_rerank_kernel(
+    const uint64_t* __restrict__ keys_lo, const uint64_t* __restrict__ keys_hi, int64_t n, int64_t idx_base,
+    int passes, TopkHdr* __restrict__ h, int64_t* __restrict__ cidx, int64_t cap, AppendRerank AR, int n_lut) {
+  __shared__ uint32_t scan[kRadixThreads / 64];
+  __shared__ unsigned long long red[kRadixThreads / 64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kRadixThreads;
+  int64_t i = static_cast<int64_t>(blockIdx.x) * kRadixThreads + tid;
+  unsigned long long lo = i < n ? keys_lo[i] : DAL_KEY_NONE;
+  unsigned long long hi = i < n ? keys_hi[i] : DAL_KEY_NONE;
+  const double lut_lane = lane < n_lut ? AR.R.lut[lane] : 0.0;
+  unsigned long long prefix, krem;
+  resolve_digit(h, passes - 1, prefix, krem, scan);
+  const int sh = digit_shift(passes - 1);
+  const unsigned long long tau = prefix | (sh ? ((1ull << sh) - 1ull) : 0ull);
+  if (blockIdx.x == 0 && tid == 0) h->kstar = tau;
+  unsigned long long below = 0;
+  const unsigned long long lt_mask = (1ull << lane) - 1ull;
+  for (;;) {  // wave-uniform: a wave's lanes hold consecutive rows
+    const bool valid = i < n;
+    below += valid && lo <= tau;
+    const bool cand = valid && hi <= tau && hi != DAL_KEY_NONE;
+    const unsigned long long cm = __ballot(cand);
+    if (cm) {
+      unsigned int base = 0;
+      if (lane == 0) base = atomicAdd(&h->cand_count, static_cast<unsigned>(__popcll(cm)));
+      double my_s = 0.0;
+      bool my_ok = false;
+      for (unsigned long long t = cm; t;) {
+        const int l = __ffsll(static_cast<long long>(t)) - 1;
+        t &= t - 1;
+        double sc;
+        const bool ok = dw_canonical_score_wave(AR.R, i - lane + l, sc, lut_lane, n_lut);
+        if (lane == l) {
+          my_s = sc;
+          my_ok = ok;
+        }
+      }
+      const int64_t pos = static_cast<int64_t>(__shfl(base, 0)) + __popcll(cm & lt_mask);
+      if (cand && pos < cap) {
+        cidx[pos] = idx_base + i;
+        AR.cpay[pos] = my_s;
+        AR.ckey[pos] = my_ok ? score_key(my_s, DAL_DESCENDING) : DAL_KEY_NONE;
+      }
+    }
+    i += stride;
+    if (i - lane >= n) break;
+    lo = i < n ? keys_lo[i] : DAL_KEY_NONE;
+    hi = i < n ? keys_hi[i] : DAL_KEY_NONE;
+  }
+  for (int o = 32; o > 0; o >>= 1) below += __shfl_xor(below, o);
+  if (lane == 0) red[tid >> 6] = below;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kRadixThreads / 64; ++w) t += red[w];
+    atomicAdd(&h->total_lt, t);
+  }
+}
+
+// One wave per candidate slot (dw_canonical_score_wave).
+__global__ __launch_bounds__(256) void rerank_kernel(const TopkHdr* __restrict__ h, int64_t idx_base, DwRerank R,
                                                      uint64_t* __restrict__ ckey,
                                                      const int64_t* __restrict__ cidx,
                                                      double* __restrict__ cpay, int64_t cap,
                                                      int64_t need_k, int32_t* __restrict__ status) {
-  const int64_t c = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (need_k && c == 0 && (h->total_lt < static_cast<unsigned long long>(need_k) || h->cand_count > cap))
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const bool lead = (threadIdx.x & 63) == 0;
+  if (need_k && c == 0 && lead &&
+      (h->total_lt < static_cast<unsigned long long>(need_k) || h->cand_count > cap))
     atomicOr(status, DAL_FLAG_SAMPLE_MISS);  // truncated level 1 over capacity: the caller re-runs exactly
   if (c >= cap) return;
   if (c >= h->cand_count) {
-    ckey[c] = DAL_KEY_NONE;
+    if (lead) ckey[c] = DAL_KEY_NONE;
     return;
   }
-  const int64_t i = cidx[c] - idx_base;
-  if (flags && !(flags[i] & DAL_ROW_CANDIDATE)) {  // filler when a shard has < k candidates
-    cpay[c] = __builtin_nan("");
-    ckey[c] = DAL_KEY_NONE;
-    return;
+  double s;
+  const bool ok = dw_canonical_score_wave(R, cidx[c] - idx_base, s);
+  if (lead) {
+    cpay[c] = s;
+    ckey[c] = ok ? score_key(s, DAL_DESCENDING) : DAL_KEY_NONE;
   }
-  const double nr = norm64[i];
-  const float* xr = x + i * ldx;
-  double acc = 0.0;
-  // the row's features are fetched 64 at a time (all loads in flight before
-  // the sequential canonical chain consumes them), not one dependent load per step
-  constexpr int kChunk = 64;
-  int f0 = 0;
-  for (; f0 + kChunk <= d; f0 += kChunk) {
-    float xv[kChunk];
-#pragma unroll
-    for (int q = 0; q < kChunk; ++q) xv[q] = xr[f0 + q];
-#pragma unroll
-    for (int q = 0; q < kChunk; ++q) {
-      const double u = static_cast<double>(xv[q]) / nr;
-      acc = acc + u * colsum[f0 + q];
-    }
-  }
-  for (int f = f0; f < d; ++f) {
-    const double u = static_cast<double>(xr[f]) / nr;
-    acc = acc + u * colsum[f];
-  }
-  if (flags && (flags[i] & DAL_ROW_EXCLUDED)) acc = __builtin_nan("");
-  const double e = lut[votes[i]];
-  const double s = e * (beta == 1.0 ? acc : pow(acc, beta));
-  cpay[c] = s;
-  ckey[c] = score_key(s, DAL_DESCENDING);
 }
 
 // Canonical fp64 max-cosine of each candidate: one wave per candidate, lanes
@@ -681,6 +778,53 @@ __global__ __launch_bounds__(256) void gather_selected_kernel(const int64_t* __r
 }
 
 // ---------------------------------------------------------------- sort ----
+// Fused-step tail (dal_dw_step): the truncated level 1's capacity check
+// (need_k > 0: fewer than k pessimistic keys <= tau or more than cap
+// candidates -> DAL_FLAG_SAMPLE_MISS), the candidate count clamped to cap, and
+// the level-1 header cleared once every thread has read it, so the next call
+// (a replayed hipGraph) starts from a zero header without a memset launch.
+// Plan publishing (dal_dw_plan_run): out_slot is a host-mapped word holding
+// the device address the selection is also written to (a fresh tensor per
+// step; NULL: none), status_mirror a host-mapped copy of the status word
+// written last -- the host reads both after its stream sync, with no copy
+// launches after the graph.
+struct SortTail {
+  int64_t cap = 0;
+  int64_t need_k = 0;
+  int32_t* status = nullptr;
+  uint32_t* clear = nullptr;
+  int64_t clear_words = 0;
+  int64_t* const* out_slot = nullptr;
+  int32_t* status_mirror = nullptr;
+};
+
+__device__ __forceinline__ int64_t* load_out_slot(int64_t* const* slot) {
+  return slot ? __hip_atomic_load(const_cast<int64_t**>(slot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : nullptr;
+}
+
+__device__ __forceinline__ void publish_status(int32_t* status, int32_t* mirror) {
+  const int32_t v = __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(mirror, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Exact-level-1 plans: the same publishing as a separate one-block launch.
+__global__ __launch_bounds__(256) void publish_kernel(const int64_t* __restrict__ out_idx,
+                                                      const double* __restrict__ out_scores, int64_t k,
+                                                      int64_t* const* out_slot, int32_t* status,
+                                                      int32_t* status_mirror) {
+  int64_t* dest = load_out_slot(out_slot);
+  if (dest) {
+    for (int64_t i = threadIdx.x; i < k; i += 256) {
+      dest[i] = out_idx[i];
+      dest[k + i] = __double_as_longlong(out_scores[i]);
+    }
+  }
+  if (status_mirror) {
+    __syncthreads();
+    if (threadIdx.x == 0) publish_status(status, status_mirror);
+  }
+}
+
 template <bool PAY>
 __global__ __launch_bounds__(kSortThreads) void sort_kernel(const uint64_t* __restrict__ keys,
                                                             const int64_t* __restrict__ idx,
@@ -689,13 +833,19 @@ __global__ __launch_bounds__(kSortThreads) void sort_kernel(const uint64_t* __re
                                                             int64_t n_static, int64_t k,
                                                             uint64_t* __restrict__ out_keys,
                                                             int64_t* __restrict__ out_idx,
-                                                            double* __restrict__ out_pay) {
+                                                            double* __restrict__ out_pay, SortTail tail) {
   constexpr int CAP = PAY ? DAL_SORT_CAP_PAYLOAD : DAL_SORT_CAP;
   __shared__ unsigned long long sk[CAP];
   __shared__ long long si[CAP];
   __shared__ double sp[PAY ? CAP : 1];
+  __shared__ int64_t* s_dest;
   const int tid = threadIdx.x;
+  if (tid == 0) s_dest = load_out_slot(tail.out_slot);  // one host round trip, overlapping the sort
   int64_t m = h ? static_cast<int64_t>(h->cand_count) : n_static;
+  if (tail.need_k && tid == 0 &&
+      (h->total_lt < static_cast<unsigned long long>(tail.need_k) || m > tail.cap))
+    atomicOr(tail.status, DAL_FLAG_SAMPLE_MISS);
+  if (tail.cap && m > tail.cap) m = tail.cap;
   if (m > CAP) m = CAP;
   int mp = 2;
   while (mp < m) mp <<= 1;
@@ -735,11 +885,19 @@ __global__ __launch_bounds__(kSortThreads) void sort_kernel(const uint64_t* __re
       __syncthreads();
     }
   }
+  if (tail.clear) {  // every thread read the header before the first barrier above
+    for (int64_t w = tid; w < tail.clear_words; w += kSortThreads) tail.clear[w] = 0u;
+  }
+  int64_t* const dest = s_dest;  // written before the first barrier
   const int64_t kk = k < m ? k : m;
   for (int i = tid; i < kk; i += kSortThreads) {
     if (out_keys) out_keys[i] = sk[i];
     out_idx[i] = si[i];
     if (PAY && out_pay) out_pay[i] = sp[i];
+    if (PAY && dest) {
+      dest[i] = si[i];
+      dest[k + i] = __double_as_longlong(sp[i]);
+    }
   }
   // candidate lists (h != null) shorter than k -- a shard with fewer than k
   // unlabeled rows under the sampled level 1 -- are padded with the NONE key
@@ -748,7 +906,15 @@ __global__ __launch_bounds__(kSortThreads) void sort_kernel(const uint64_t* __re
       if (out_keys) out_keys[i] = DAL_KEY_NONE;
       out_idx[i] = -1;
       if (out_pay) out_pay[i] = __builtin_nan("");
+      if (dest) {
+        dest[i] = -1;
+        dest[k + i] = __double_as_longlong(__builtin_nan(""));
+      }
     }
+  }
+  if (tail.status_mirror) {  // last: every status writer of the step has finished
+    __syncthreads();
+    if (tid == 0) publish_status(tail.status, tail.status_mirror);
   }
 }
 
@@ -761,11 +927,18 @@ __global__ __launch_bounds__(256) void zero_words_kernel(uint32_t* __restrict__ 
     p[i] = 0u;
 }
 
-int run_radix(const uint64_t* keys, int64_t n, int64_t k, TopkHdr* h, hipStream_t st, int passes = kPasses) {
-  static_assert(sizeof(TopkHdr) % 4 == 0, "header is whole words");
-  const int64_t words = sizeof(TopkHdr) / 4;
-  hipLaunchKernelGGL(zero_words_kernel, dim3(static_cast<unsigned>(ceil_div(words, 256 * 4))), dim3(256), 0, st,
-                     reinterpret_cast<uint32_t*>(h), words);
+constexpr int64_t kHdrWords = sizeof(TopkHdr) / 4;
+static_assert(sizeof(TopkHdr) % 4 == 0, "header is whole words");
+
+void zero_header(TopkHdr* h, hipStream_t st) {
+  hipLaunchKernelGGL(zero_words_kernel, dim3(static_cast<unsigned>(ceil_div(kHdrWords, 256 * 4))), dim3(256), 0, st,
+                     reinterpret_cast<uint32_t*>(h), kHdrWords);
+}
+
+// Radix passes 0 .. passes-1 (zero: clear the header first).
+int run_radix(const uint64_t* keys, int64_t n, int64_t k, TopkHdr* h, hipStream_t st, int passes = kPasses,
+              bool zero = true) {
+  if (zero) zero_header(h, st);
   // each block flushes up to 2048 bins with global atomics: beyond ~256
   // blocks the flush, not the key stream, sets a pass's time (2M keys: 977
   // blocks -> 2M atomics)
@@ -823,7 +996,7 @@ extern "C" int dal_topk(const uint64_t* keys, int64_t n, int64_t k, int64_t idx_
   hipLaunchKernelGGL(sort_kernel<false>, dim3(1), dim3(kSortThreads), 0, st,
                      reinterpret_cast<const uint64_t*>(base + L.ckey),
                      reinterpret_cast<const int64_t*>(base + L.cidx), nullptr, h, int64_t{0}, k,
-                     out_keys, out_idx, nullptr);
+                     out_keys, out_idx, nullptr, SortTail{});
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
 }
@@ -873,7 +1046,7 @@ static int select_with_rerank(const uint64_t* keys_lo, const uint64_t* keys_hi, 
     // level 2 fits one block: sort the cand_count candidates (row order, so
     // ties resolve by index) by canonical key with their scores, take k
     hipLaunchKernelGGL(sort_kernel<true>, dim3(1), dim3(kSortThreads), 0, st, ckey, cidx, cpay, h1, int64_t{0},
-                       k, out_keys, out_idx, out_scores);
+                       k, out_keys, out_idx, out_scores, SortTail{});
     DAL_RETURN_IF_LAUNCH_FAILED();
     return DAL_OK;
   }
@@ -884,7 +1057,7 @@ static int select_with_rerank(const uint64_t* keys_lo, const uint64_t* keys_hi, 
   uint64_t* pkeys = reinterpret_cast<uint64_t*>(base2 + L2.ckey);
   hipLaunchKernelGGL(sort_kernel<false>, dim3(1), dim3(kSortThreads), 0, st, pkeys,
                      reinterpret_cast<const int64_t*>(base2 + L2.cidx), nullptr, h2, int64_t{0}, k, pkeys,
-                     pos, nullptr);
+                     pos, nullptr, SortTail{});
   hipLaunchKernelGGL(gather_selected_kernel, dim3(static_cast<unsigned>(ceil_div(k, 256))), dim3(256), 0, st,
                      pos, pkeys, k, cidx, cpay, out_idx, out_scores, out_keys);
   DAL_RETURN_IF_LAUNCH_FAILED();
@@ -912,13 +1085,115 @@ extern "C" int dal_dw_select(const uint64_t* keys_lo, const uint64_t* keys_hi, c
     // the only consumer of colsum: join its producer stream here, not before the call
     if (colsum_ready && hipStreamWaitEvent(st, reinterpret_cast<hipEvent_t>(colsum_ready), 0) != hipSuccess)
       wait_failed = true;
-    hipLaunchKernelGGL(rerank_kernel, dim3(static_cast<unsigned>(ceil_div(cp, 256))), dim3(256), 0, st, h,
-                       idx_base, x, static_cast<int>(d), ldx, norm64, colsum, lut, votes, row_flags, beta,
+    hipLaunchKernelGGL(rerank_kernel, dim3(static_cast<unsigned>(ceil_div(cp, 4))), dim3(256), 0, st, h,
+                       idx_base, DwRerank{x, static_cast<int>(d), ldx, norm64, colsum, lut, votes, row_flags, beta},
                        ckey, cidx, cpay, cp, need_k, dev_status);
   };
   const int rc = select_with_rerank(keys_lo, keys_hi, n, k, idx_base, cap, level1_passes, ws, ws_bytes, rerank,
                                     out_idx, out_scores, out_keys, dev_status, st);
   return rc ? rc : (wait_failed ? DAL_ERR_HIP : DAL_OK);
+}
+
+extern "C" size_t dal_dw_step_workspace_bytes(int64_t n, int64_t k, int64_t cap) {
+  return rerank_ws_bytes(n, k, cap);
+}
+
+// One density-weighted iteration: dal_forest_score (DAL_DENSITY_FIXED,
+// DAL_DESCENDING, interval keys) + dal_dw_select in one call.  With a
+// truncated level 1 (level1_passes > 0, cap <= DAL_SORT_CAP_PAYLOAD) the
+// launches are fused: the threshold append re-ranks the candidates it appends
+// (a wave per candidate), and the one-block sort checks the capacity and
+// clears the level-1 header -- 5 launches instead of 7 (no header zero with
+// DAL_STEP_WS_CLEAN, no status memset with DAL_STEP_RESET_STATUS).  Same bits
+// as the two calls.
+namespace dal {
+
+int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner, const uint8_t* leaf,
+                 int32_t n_trees, int32_t depth, const double* lut, const int64_t* density_fixed, double density_err,
+                 const uint8_t* row_flags, double beta, int64_t idx_base, const double* norm64, const double* colsum,
+                 int64_t k, int64_t cap, int32_t level1_passes, uint32_t step_flags, void* ws, size_t ws_bytes,
+                 int32_t* votes, double* scores, uint64_t* keys_lo, uint64_t* keys_hi, int64_t* out_idx,
+                 double* out_scores, uint64_t* out_keys, int32_t* dev_status, dal_event_t colsum_ready,
+                 dal_stream_t stream, int64_t* const* out_slot, int32_t* status_mirror) {
+  if (!x || !inner || !leaf || !lut || !density_fixed || !norm64 || !colsum || !ws || !votes || !scores ||
+      !keys_lo || !keys_hi || !out_idx || !out_scores || !dev_status)
+    return DAL_ERR_ARG;
+  if (step_flags & ~static_cast<uint32_t>(DAL_STEP_RESET_STATUS | DAL_STEP_WS_CLEAN)) return DAL_ERR_ARG;
+  if (n < 1 || d < 1 || ldx < d || k < 1 || k > n || cap < k) return DAL_ERR_SHAPE;
+  if (level1_passes < 0 || level1_passes >= kPasses || (level1_passes > 0 && cap > DAL_SORT_CAP_PAYLOAD))
+    return DAL_ERR_ARG;
+  if (k > DAL_SORT_CAP) return DAL_ERR_CAPACITY;
+  if (ws_bytes < rerank_ws_bytes(n, k, cap) || (reinterpret_cast<uintptr_t>(ws) & 255)) return DAL_ERR_SHAPE;
+  hipStream_t st = as_stream(stream);
+  const bool clean = step_flags & DAL_STEP_WS_CLEAN;
+  ForestStepHooks hooks;
+  if (step_flags & DAL_STEP_RESET_STATUS) hooks.status_reset = dev_status;
+  const TopkLayout L1 = topk_layout(n, cap);
+  char* base = static_cast<char*>(ws);
+  TopkHdr* h1 = reinterpret_cast<TopkHdr*>(base + L1.hdr);
+  if (level1_passes == 0) {  // exact level 1: the two calls as they are
+    int rc = forest_score_launch(x, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, DAL_DENSITY_FIXED,
+                                 density_err, row_flags, beta, DAL_DESCENDING, votes, scores, keys_lo, keys_hi,
+                                 hooks, st);
+    if (rc) return rc;
+    rc = dal_dw_select(keys_lo, keys_hi, votes, row_flags, n, k, idx_base, lut, beta, x, d, ldx, norm64, colsum,
+                       cap, 0, ws, ws_bytes, out_idx, out_scores, out_keys, dev_status, colsum_ready, stream);
+    if (rc) return rc;
+    if (clean) zero_header(h1, st);  // keep the contract: the header is left zero
+    if (out_slot || status_mirror)
+      hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(256), 0, st, out_idx, out_scores, k, out_slot, dev_status,
+                         status_mirror);
+    DAL_RETURN_IF_LAUNCH_FAILED();
+    return DAL_OK;
+  }
+  if (!clean) zero_header(h1, st);
+  int rc = forest_score_launch(x, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, DAL_DENSITY_FIXED,
+                               density_err, row_flags, beta, DAL_DESCENDING, votes, scores, keys_lo, keys_hi, hooks,
+                               st);
+  if (rc) return rc;
+  rc = run_radix(keys_lo, n, k, h1, st, level1_passes, false);
+  if (rc) return rc;
+  if (colsum_ready && hipStreamWaitEvent(st, reinterpret_cast<hipEvent_t>(colsum_ready), 0) != hipSuccess)
+    return DAL_ERR_HIP;
+  uint64_t* ckey = reinterpret_cast<uint64_t*>(base + L1.ckey);
+  int64_t* cidx = reinterpret_cast<int64_t*>(base + L1.cidx);
+  double* cpay = reinterpret_cast<double*>(base + L1.cpay);
+  const DwRerank R{x, static_cast<int>(d), ldx, norm64, colsum, lut, votes, row_flags, beta};
+  // one key per thread where possible: a wave scores its candidates one after
+  // another, so the fewer rows a wave sweeps, the shorter its longest chain
+  const int64_t blocks = std::min<int64_t>(ceil_div(n, kRadixThreads), 2048);
+  const int n_lut = n_trees < 64 ? n_trees + 1 : 0;  // LUT held in lanes when it fits a wave
+  hipLaunchKernelGGL(append_rerank_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kRadixThreads), 0, st, keys_lo,
+                     keys_hi, n, idx_base, static_cast<int>(level1_passes), h1, cidx, cap, AppendRerank{R, ckey, cpay},
+                     n_lut);
+  SortTail tail;
+  tail.cap = cap;
+  tail.need_k = k;
+  tail.status = dev_status;
+  tail.clear = reinterpret_cast<uint32_t*>(h1);
+  tail.clear_words = kHdrWords;
+  tail.out_slot = out_slot;
+  tail.status_mirror = status_mirror;
+  hipLaunchKernelGGL(sort_kernel<true>, dim3(1), dim3(kSortThreads), 0, st, ckey, cidx, cpay, h1, int64_t{0}, k,
+                     out_keys, out_idx, out_scores, tail);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}
+
+}  // namespace dal
+
+extern "C" int dal_dw_step(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
+                           const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
+                           const int64_t* density_fixed, double density_err, const uint8_t* row_flags, double beta,
+                           int64_t idx_base, const double* norm64, const double* colsum, int64_t k, int64_t cap,
+                           int32_t level1_passes, uint32_t step_flags, void* ws, size_t ws_bytes, int32_t* votes,
+                           double* scores, uint64_t* keys_lo, uint64_t* keys_hi, int64_t* out_idx,
+                           double* out_scores, uint64_t* out_keys, int32_t* dev_status, dal_event_t colsum_ready,
+                           dal_stream_t stream) {
+  return dw_step_impl(x, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, density_err, row_flags, beta,
+                      idx_base, norm64, colsum, k, cap, level1_passes, step_flags, ws, ws_bytes, votes, scores,
+                      keys_lo, keys_hi, out_idx, out_scores, out_keys, dev_status, colsum_ready, stream, nullptr,
+                      nullptr);
 }
 
 extern "C" size_t dal_maxcos_select_workspace_bytes(int64_t n, int64_t k, int64_t cap) {
@@ -978,11 +1253,11 @@ extern "C" int dal_sort_pairs(const uint64_t* keys, const int64_t* idx, const do
   if (payload) {
     if (n > DAL_SORT_CAP_PAYLOAD) return DAL_ERR_CAPACITY;
     hipLaunchKernelGGL(sort_kernel<true>, dim3(1), dim3(kSortThreads), 0, st, keys, idx, payload,
-                       nullptr, n, k, out_keys, out_idx, out_payload);
+                       nullptr, n, k, out_keys, out_idx, out_payload, SortTail{});
   } else {
     if (n > DAL_SORT_CAP) return DAL_ERR_CAPACITY;
     hipLaunchKernelGGL(sort_kernel<false>, dim3(1), dim3(kSortThreads), 0, st, keys, idx, nullptr,
-                       nullptr, n, k, out_keys, out_idx, nullptr);
+                       nullptr, n, k, out_keys, out_idx, nullptr, SortTail{});
   }
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;

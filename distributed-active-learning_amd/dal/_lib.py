@@ -34,6 +34,8 @@ DAL_CANON_CHUNK = 256
 DAL_MAX_TREE_DEPTH = 16
 DAL_SORT_CAP = 8192
 DAL_SORT_CAP_PAYLOAD = 4096
+DAL_STEP_RESET_STATUS = 1
+DAL_STEP_WS_CLEAN = 2
 DAL_RF_MAX_SPLITS = 255
 DAL_RF_MAX_SPLIT_SAMPLE = 16384
 DAL_RF_MAX_DEPTH = 10
@@ -78,6 +80,17 @@ SIGNATURES = {
                               c_void_p, c_double, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
                               c_int64, c_int32, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_void_p]),
+    "dal_dw_step_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
+    "dal_dw_step": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32, c_int32, c_void_p,
+                            c_void_p, c_double, c_void_p, c_double, c_int64, c_void_p, c_void_p, c_int64, c_int64,
+                            c_int32, ctypes.c_uint32, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
+                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "dal_dw_plan_create": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32, c_int32,
+                                   c_void_p, c_void_p, c_double, c_void_p, c_void_p, c_double, c_int64, c_void_p,
+                                   c_void_p, c_int64, c_int64, c_int32, c_void_p, c_size_t, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "dal_dw_plan_run": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    "dal_dw_plan_destroy": (None, [c_void_p]),
     "dal_maxcos_label_rows_granule": (c_int64, [c_int64]),
     "dal_maxcos_error_bound": (c_double, [c_int64]),
     "dal_inv_norms_bf16": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p, c_void_p,

@@ -21,7 +21,7 @@ from . import _lib
 from ._lib import (DAL_ASCENDING, DAL_CANON_CHUNK, DAL_DENSITY_EXACT, DAL_DENSITY_FIXED,
                    DAL_DENSITY_NONE, DAL_DESCENDING, DAL_FIXED_SCALE, DAL_FLAG_CAND_OVERFLOW,
                    DAL_FLAG_SAMPLE_MISS, DAL_FLAG_ZERO_NORM, DAL_ROW_CANDIDATE, DAL_ROW_EXCLUDED,
-                   DAL_SORT_CAP_PAYLOAD, call)
+                   DAL_SORT_CAP_PAYLOAD, DAL_STEP_RESET_STATUS, DAL_STEP_WS_CLEAN, call)
 from .forest import Forest
 from .luts import ASCENDING, lut as make_lut
 
@@ -587,6 +587,49 @@ def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k
         state.cap_scale *= 4  # later steps (same pool, same score spread) start here
 
 
+def dw_step_local(state: PoolState, forest: Forest, flags, dens, lut_dev, k: int, beta: float, colsum,
+                  colsum_ready=None):
+    """dal_dw_step on this (single-GPU) pool: votes, scores and interval keys
+    of every row, then the exact canonical top-k -- one C call with fused
+    launches (the truncated level 1).  Same retries as dw_select_local.
+    Returns (votes, scores, indices, selected scores)."""
+    torch = _torch()
+    lib = _lib.load()
+    n = state.n
+    inner, leaf = forest.device(state.device)
+    norm64 = state.norms()
+    derr = float(density_error(state))
+    dev = state.device
+    votes = torch.empty(n, dtype=torch.int32, device=dev)
+    scores = torch.empty(n, dtype=torch.float64, device=dev)
+    keys_lo = torch.empty(n, dtype=torch.int64, device=dev)
+    keys_hi = torch.empty(n, dtype=torch.int64, device=dev)
+    base = candidate_cap(n, k) if state.cap_base is None else max(int(k), int(state.cap_base))
+    cap = int(min(n, base * state.cap_scale))
+    while True:
+        passes = level1_passes(state, n, k, cap)
+        wsb = int(lib.dal_dw_step_workspace_bytes(n, k, cap))
+        ws, wsp = workspace(wsb, dev)
+        out_idx = torch.empty(k, dtype=torch.int64, device=dev)
+        out_scores = torch.empty(k, dtype=torch.float64, device=dev)
+        call("dal_dw_step", _ptr(state.x), n, state.d, state.d, _ptr(inner), _ptr(leaf), forest.n_trees,
+             forest.depth, _ptr(lut_dev), _ptr(dens), derr, _ptr(flags), float(beta), state.row_base,
+             _ptr(norm64), _ptr(colsum), k, cap, passes, 0, wsp, wsb, _ptr(votes), _ptr(scores), _ptr(keys_lo),
+             _ptr(keys_hi), _ptr(out_idx), _ptr(out_scores), 0, _ptr(state.status),
+             0 if colsum_ready is None else colsum_ready.cuda_event, _stream(dev))
+        st = int(state.status.item())  # the step's one host sync
+        state.last_status = st
+        if st & DAL_FLAG_SAMPLE_MISS:  # truncated level 1 over capacity: exact level 1 from now on
+            state.status.bitwise_and_(~(DAL_FLAG_SAMPLE_MISS | DAL_FLAG_CAND_OVERFLOW))
+            state.level1_fast = False
+            continue
+        if cap >= n or not (st & DAL_FLAG_CAND_OVERFLOW):
+            return votes, scores, out_idx, out_scores
+        state.status.bitwise_and_(~DAL_FLAG_CAND_OVERFLOW)
+        cap = min(n, cap * 4)
+        state.cap_scale *= 4
+
+
 def sort_pairs(keys, idx, k: int, payload=None):
     """Sort (key, idx) pairs (with an optional fp64 payload) and keep k."""
     torch = _torch()
@@ -660,6 +703,13 @@ def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: 
     kk = min(int(k), n_cand)
     loc = state.local_positions(unl)
     lut_dev = device_lut("entropy", forest.n_trees, state.device)
+    if (state.forest_events is None and state.select_events is None and state.row_base == 0
+            and state.n == state.n_total):
+        # one C call, fused launches (the per-kernel timing path below keeps K2 / K3 apart)
+        votes, scores, idx, sel_scores = dw_step_local(state, forest, flags, dens, lut_dev, kk, beta,
+                                                       state.colsum(), colsum_ready)
+        state.check_status(state.last_status)
+        return Selection(scores=(scores, loc), indices=idx, selected_scores=sel_scores, votes=(votes, loc))
     votes, scores, keys_lo, keys_hi = forest_score(
         state, forest, lut_dev, flags, DAL_DESCENDING, density=dens,
         density_err=density_error(state), beta=beta, want_hi=True)
@@ -671,16 +721,19 @@ def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: 
 
 
 class WarmStepGraph:
-    """hipGraph of one warm density-weighted step (density cached -- the
-    reference's per-iteration path, density_weighting.py:133-176): forest
-    votes + score + interval keys, the candidate search, the exact fp64
-    re-rank and the final sort replay as ONE graph launch instead of ~7
-    (truncated level 1) to ~14 (exact) kernel launches from Python.  Inputs are static
-    device buffers refreshed before each replay: the forest's heap arrays
-    (copied when a different forest comes in) and the row flags (the pool's
-    base flags + the unlabeled set, marked each step)."""
+    """One warm density-weighted step (density cached -- the reference's
+    per-iteration path, density_weighting.py:133-176) as a libdal plan
+    (dal_dw_plan_create): dal_dw_step -- forest votes + score + interval
+    keys, the candidate search, the exact fp64 re-rank and the final sort,
+    fused into 5 launches -- captured once as a hipGraph over static device
+    buffers.  Per step ONE C call (dal_dw_plan_run) rebuilds the row flags
+    from the pool's base flags and the unlabeled list, replays the graph,
+    copies the selection out and reads the status word.  A different forest
+    is copied into the static heap arrays first."""
 
     def __init__(self, state: PoolState, forest: Forest, k: int, beta: float, cap: int, passes: int):
+        import ctypes
+
         torch = _torch()
         dev = state.device
         n = state.n
@@ -697,36 +750,31 @@ class WarmStepGraph:
         self.keys_hi = torch.empty(n, dtype=torch.int64, device=dev)
         # selected indices and scores side by side: one copy hands them out
         self.out_pair = torch.empty(2 * k, dtype=torch.int64, device=dev)
-        self.out_idx = self.out_pair[:k]
-        self.out_scores = self.out_pair[k:].view(torch.float64)
         self.out_keys = torch.empty(k, dtype=torch.int64, device=dev)
         self._last = None  # weak reference to the Selection that still reads votes / scores
         lib = _lib.load()
-        self.wsb = int(lib.dal_dw_select_workspace_bytes(n, k, cap))
+        self.wsb = int(lib.dal_dw_step_workspace_bytes(n, k, cap))
         self.ws, self.wsp = workspace(self.wsb, dev)
-        dens, colsum, norm64 = state.density_fixed(), state.colsum(), state.norms()
-        derr = density_error(state)
-        self.graph = torch.cuda.CUDAGraph()
-        side = torch.cuda.Stream(device=dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.graph(self.graph, stream=side, capture_error_mode="relaxed"):
-            st = _stream(dev)
-            state.status.zero_()
-            call("dal_forest_score", _ptr(state.x), n, state.d, state.d, _ptr(self.inner), _ptr(self.leaf),
-                 self.n_trees, self.depth, _ptr(self.lut), _ptr(dens), DAL_DENSITY_FIXED, float(derr),
-                 _ptr(self.flags), float(beta), DAL_DESCENDING, _ptr(self.votes), _ptr(self.scores),
-                 _ptr(self.keys_lo), _ptr(self.keys_hi), st)
-            call("dal_dw_select", _ptr(self.keys_lo), _ptr(self.keys_hi), _ptr(self.votes), _ptr(self.flags),
-                 n, k, state.row_base, _ptr(self.lut), float(beta), _ptr(state.x), state.d, state.d,
-                 _ptr(norm64), _ptr(colsum), cap, passes, self.wsp, self.wsb, _ptr(self.out_idx),
-                 _ptr(self.out_scores), _ptr(self.out_keys), _ptr(state.status), 0, st)
-        torch.cuda.current_stream(dev).wait_stream(side)
+        self._keep = (state.density_fixed(), state.colsum(), state.norms(), state.flags, state.x)
+        dens, colsum, norm64 = self._keep[:3]
+        plan = ctypes.c_void_p()
+        call("dal_dw_plan_create", _ptr(state.x), n, state.d, state.d, _ptr(self.inner), _ptr(self.leaf),
+             self.n_trees, self.depth, _ptr(self.lut), _ptr(dens), float(density_error(state)), _ptr(state.flags),
+             _ptr(self.flags), float(beta), state.row_base, _ptr(norm64), _ptr(colsum), k, cap, passes, self.wsp,
+             self.wsb, _ptr(self.votes), _ptr(self.scores), _ptr(self.keys_lo), _ptr(self.keys_hi),
+             _ptr(self.out_pair), _ptr(self.out_keys), _ptr(state.status), _stream(dev), ctypes.byref(plan))
+        self.plan = plan
+        self._status = ctypes.c_int32()
+        self._status_ref = ctypes.byref(self._status)
+        self._finalizer = weakref.finalize(self, lib.dal_dw_plan_destroy, plan)
 
     def run(self, forest: Forest, unl):
-        """Refresh the inputs and replay; returns (votes, scores) -- the
-        graph's buffers, valid until the next replay (copy-on-write: the
-        previous step's Selection is materialised before they are reused) --
-        and a copy of (selected indices, selected scores)."""
+        """Refresh the inputs, replay, read the status: returns (votes,
+        scores, selection pair, status).  votes / scores are the plan's
+        buffers, valid until the next replay (copy-on-write: the previous
+        step's Selection is materialised before they are reused); the pair
+        (indices | score bits) is a fresh tensor."""
+        torch = _torch()
         prev = self._last() if self._last is not None else None
         if prev is not None:
             prev._detach()
@@ -735,17 +783,15 @@ class WarmStepGraph:
             self.inner.copy_(inner)
             self.leaf.copy_(leaf)
             self.forest_ref = forest
-        self.flags.copy_(self.state.flags)
-        call("dal_mark_rows", _ptr(unl), int(unl.shape[0]), self.state.row_base, self.state.n,
-             DAL_ROW_CANDIDATE, _ptr(self.flags), _stream(self.state.device))
-        self.graph.replay()
-        pair = self.out_pair.clone()
-        return self.votes, self.scores, pair[:self.k], pair[self.k:].view(torch_float64())
+        pair = torch.empty(2 * self.k, dtype=torch.int64, device=self.state.device)
+        call("dal_dw_plan_run", self.plan, _ptr(unl), int(unl.shape[0]), _ptr(pair), self._status_ref,
+             _stream(self.state.device))
+        return self.votes, self.scores, pair, int(self._status.value)
 
 
 def _density_step_graph(state: PoolState, unl, forest: Forest, kk: int, beta: float) -> Selection:
     """Warm density step through a cached WarmStepGraph (same selection as
-    the eager path; a level-1 or re-rank capacity overflow rebuilds the graph
+    the eager path; a level-1 or re-rank capacity overflow rebuilds the plan
     with the exact level 1 / a larger capacity and replays)."""
     n = state.n
     loc = state.local_positions(unl)
@@ -757,8 +803,7 @@ def _density_step_graph(state: PoolState, unl, forest: Forest, kk: int, beta: fl
         g = state._graphs.get(key)
         if g is None:
             g = state._graphs[key] = WarmStepGraph(state, forest, kk, beta, cap, passes)
-        votes, scores, idx, sel_scores = g.run(forest, unl)
-        st = int(state.status.item())
+        votes, scores, pair, st = g.run(forest, unl)
         state.last_status = st
         if st & DAL_FLAG_SAMPLE_MISS:
             state.status.bitwise_and_(~(DAL_FLAG_SAMPLE_MISS | DAL_FLAG_CAND_OVERFLOW))
@@ -769,7 +814,8 @@ def _density_step_graph(state: PoolState, unl, forest: Forest, kk: int, beta: fl
             state.cap_scale *= 4
             continue
         state.check_status(st)
-        sel = Selection(scores=(scores, loc), indices=idx, selected_scores=sel_scores, votes=(votes, loc))
+        sel = Selection(scores=(scores, loc), indices=pair[:kk], selected_scores=pair[kk:].view(torch_float64()),
+                        votes=(votes, loc))
         g._last = weakref.ref(sel)
         return sel
 

@@ -258,6 +258,62 @@ int dal_dw_select(const uint64_t* keys_lo, const uint64_t* keys_hi, const int32_
                   size_t ws_bytes, int64_t* out_idx, double* out_scores, uint64_t* out_keys,
                   int32_t* dev_status, dal_event_t colsum_ready, dal_stream_t stream);
 
+/* ---- one density-weighted iteration in one call (a5-a11) ----------------
+ * The body of density_weighting.py:133-176 for a cached density: equivalent to
+ * dal_forest_score(x, ..., density_fixed, DAL_DENSITY_FIXED, density_err,
+ * row_flags, beta, DAL_DESCENDING, votes, scores, keys_lo, keys_hi) followed by
+ * dal_dw_select(keys_lo, keys_hi, votes, row_flags, n, k, idx_base, lut, beta,
+ * x, d, ldx, norm64, colsum, cap, level1_passes, ...) -- same outputs, same
+ * bits -- with the launches fused when level1_passes > 0 (and cap <=
+ * DAL_SORT_CAP_PAYLOAD): the score kernel counts the first radix digit
+ * itself, the threshold append computes each candidate's canonical score, and
+ * the final sort checks the capacity (DAL_FLAG_SAMPLE_MISS) and clears the
+ * level-1 header.  step_flags:
+ *   DAL_STEP_RESET_STATUS  *dev_status is zeroed at the start of the step (on
+ *                          the device: a replayed hipGraph needs no memset node);
+ *   DAL_STEP_WS_CLEAN      the workspace header is zero on entry (a previous
+ *                          dal_dw_step left it so, or the caller zeroed the
+ *                          workspace once): no zeroing launch.  The header is
+ *                          left zero on exit whenever this flag is given.
+ * Workspace: dal_dw_step_workspace_bytes (== dal_dw_select's). */
+#define DAL_STEP_RESET_STATUS 1u
+#define DAL_STEP_WS_CLEAN 2u
+size_t dal_dw_step_workspace_bytes(int64_t n, int64_t k, int64_t cap);
+int dal_dw_step(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner, const uint8_t* leaf,
+                int32_t n_trees, int32_t depth, const double* lut, const int64_t* density_fixed,
+                double density_err, const uint8_t* row_flags, double beta, int64_t idx_base,
+                const double* norm64, const double* colsum, int64_t k, int64_t cap, int32_t level1_passes,
+                uint32_t step_flags, void* ws, size_t ws_bytes, int32_t* votes, double* scores,
+                uint64_t* keys_lo, uint64_t* keys_hi, int64_t* out_idx, double* out_scores,
+                uint64_t* out_keys, int32_t* dev_status, dal_event_t colsum_ready, dal_stream_t stream);
+
+/* ---- warm-step plan: a replayed dal_dw_step with a one-call host side -----
+ * dal_dw_plan_create captures dal_dw_step (DAL_STEP_RESET_STATUS |
+ * DAL_STEP_WS_CLEAN, no colsum event) over the given caller-owned buffers as a
+ * hipGraph (the workspace is zeroed once, synchronously on ``stream``).
+ * ``flags`` is the step's row-flag buffer, rebuilt by every run from
+ * ``base_flags`` (the pool's EXCLUDED bits) and the unlabeled list; the
+ * selection lands in out_pair[0..k) (indices) and out_pair[k..2k) (fp64
+ * score bits).  dal_dw_plan_run(plan, unl, n_unl, out_copy, status, stream):
+ * flags <- base_flags, mark unl as DAL_ROW_CANDIDATE, replay (the graph's
+ * last kernel also writes the selection to out_copy -- nullable, 2k int64 --
+ * and the final status word to host-mapped memory), synchronise ``stream``
+ * and return the status in *status -- the density_weighting.py:133-176
+ * iteration in one call.  Buffers must outlive the plan; dal_dw_plan_destroy
+ * frees it. */
+typedef struct dal_dw_plan dal_dw_plan_t;
+int dal_dw_plan_create(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
+                       const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
+                       const int64_t* density_fixed, double density_err, const uint8_t* base_flags,
+                       uint8_t* flags, double beta, int64_t idx_base, const double* norm64,
+                       const double* colsum, int64_t k, int64_t cap, int32_t level1_passes, void* ws,
+                       size_t ws_bytes, int32_t* votes, double* scores, uint64_t* keys_lo, uint64_t* keys_hi,
+                       int64_t* out_pair, uint64_t* out_keys, int32_t* dev_status, dal_stream_t stream,
+                       dal_dw_plan_t** plan);
+int dal_dw_plan_run(dal_dw_plan_t* plan, const int64_t* unl, int64_t n_unl, int64_t* out_copy,
+                    int32_t* status, dal_stream_t stream);
+void dal_dw_plan_destroy(dal_dw_plan_t* plan);
+
 /* ---- (a12, config 5) max-cosine to a labeled set -----------------------
  * Restates similarity.py:26-43 (columnSimilarities of the normalised pool) as
  * m_i = max_{l in L} cos(x_i, x_l) over a bf16 pool (row-major [n][d],

@@ -12,6 +12,7 @@
 #   pmc=TAG=CTRS[=ARGS]   rocprofv3 --pmc CTRS (',' = space) of bench.py ARGS -> gpurun_out/pmc_TAG/
 #   pmcpy=TAG=CTRS=SCRIPT[=ARGS]  rocprofv3 --pmc CTRS of python SCRIPT ARGS -> gpurun_out/pmc_TAG/
 #   py=SCRIPT[=ARGS]      python SCRIPT ARGS                  -> gpurun_out/py_<n>.log
+#   trace=TAG=SCRIPT[=ARGS]  rocprofv3 --kernel-trace of python SCRIPT ARGS -> gpurun_out/trace_TAG/
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -75,6 +76,17 @@ for step in "$@"; do
         python3 -u $scr ${args//,/ } > gpurun_out/pmc_$tag.log 2>&1
       rc=$?
       echo "[$n] pmcpy $tag rc=$rc"
+      ;;
+    trace)
+      tag=${rest%%=*}
+      r2=${rest#*=}
+      scr=${r2%%=*}
+      args=""
+      [[ "$r2" == *=* ]] && args=${r2#*=}
+      timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_$tag -o run -- \
+        python3 -u $scr ${args//,/ } > gpurun_out/trace_$tag.log 2>&1
+      rc=$?
+      echo "[$n] trace $tag rc=$rc"
       ;;
     py)
       scr=${rest%%=*}

@@ -128,3 +128,105 @@ def test_warm_graph_outputs_survive_later_steps(cuda):
         assert np.array_equal(a.votes.cpu().numpy(), b.votes.cpu().numpy())
         assert np.array_equal(a.scores.cpu().numpy().view(np.int64), b.scores.cpu().numpy().view(np.int64))
         assert np.array_equal(a.indices.cpu().numpy(), b.indices.cpu().numpy())
+
+
+@pytest.mark.parametrize("n,d,trees,passes", [(100_000, 64, 10, 2), (284_807 // 4, 30, 100, 2),
+                                              (100_000, 256, 10, 2), (20_000, 32, 10, 0),
+                                              (3_000, 16, 7, 1)])
+def test_dw_step_matches_separate_calls(cuda, n, d, trees, passes):
+    """dal_dw_step (fused launches: pass-0 histogram in the score kernel --
+    or a separate pass 0 when the grid is large, as at d = 256 here -- the
+    re-rank inside the threshold append, capacity check + header clear in the
+    sort) gives the same bits as dal_forest_score + dal_dw_select, call after
+    call on one workspace with DAL_STEP_WS_CLEAN, and DAL_STEP_RESET_STATUS
+    clears a stale status word."""
+    import torch
+
+    from dal import _lib, engine
+    from dal._lib import DAL_STEP_RESET_STATUS, DAL_STEP_WS_CLEAN, call
+    from dal.forest import Forest
+
+    X = O.synthetic_pool(n, d, seed=4)
+    E = np.arange(10)
+    unl = np.arange(10, n)
+    st = engine.PoolState(X, excluded=E, device=cuda)
+    st.density_fixed()
+    dens, colsum, norm64 = st.density_fixed(), st.colsum(), st.norms()
+    flags, _, _ = st.row_flags(unl)
+    k = 100
+    cap = engine.candidate_cap(n, k)
+    lib = _lib.load()
+    lut = engine.device_lut("entropy", trees, cuda)
+    derr = engine.density_error(st)
+    P = lambda t: t.data_ptr()  # noqa: E731
+    S = torch.cuda.current_stream(cuda).cuda_stream
+    for it in range(3):
+        F = Forest.synthetic(trees, 4, d, seed=40 + it)
+        inner, leaf = F.device(cuda)
+        # reference: the two calls
+        v0, s0, klo0, khi0 = engine.forest_score(st, F, lut, flags, _lib.DAL_DESCENDING, density=dens,
+                                                 density_err=derr, want_hi=True)
+        wsb = int(lib.dal_dw_select_workspace_bytes(n, k, cap))
+        ws0, wsp0 = engine.workspace(wsb, cuda)
+        i0 = torch.empty(k, dtype=torch.int64, device=cuda)
+        c0 = torch.empty(k, dtype=torch.float64, device=cuda)
+        st.status.zero_()
+        call("dal_dw_select", P(klo0), P(khi0), P(v0), P(flags), n, k, 0, P(lut), 1.0, P(st.x), d, d, P(norm64),
+             P(colsum), cap, passes, wsp0, wsb, P(i0), P(c0), 0, P(st.status), 0, S)
+        assert int(st.status.item()) == 0
+        # the fused call, on one workspace zeroed once
+        if it == 0:
+            ws, wsp = engine.workspace(int(lib.dal_dw_step_workspace_bytes(n, k, cap)), cuda)
+            ws.zero_()
+        v = torch.empty(n, dtype=torch.int32, device=cuda)
+        s = torch.empty(n, dtype=torch.float64, device=cuda)
+        klo = torch.empty(n, dtype=torch.int64, device=cuda)
+        khi = torch.empty(n, dtype=torch.int64, device=cuda)
+        i1 = torch.empty(k, dtype=torch.int64, device=cuda)
+        c1 = torch.empty(k, dtype=torch.float64, device=cuda)
+        ok1 = torch.empty(k, dtype=torch.int64, device=cuda)
+        st.status.fill_(_lib.DAL_FLAG_CAND_OVERFLOW)  # stale: the step must clear it on the device
+        call("dal_dw_step", P(st.x), n, d, d, P(inner), P(leaf), trees, 4, P(lut), P(dens), float(derr), P(flags),
+             1.0, 0, P(norm64), P(colsum), k, cap, passes, DAL_STEP_RESET_STATUS | DAL_STEP_WS_CLEAN, wsp,
+             int(lib.dal_dw_step_workspace_bytes(n, k, cap)), P(v), P(s), P(klo), P(khi), P(i1), P(c1), P(ok1),
+             P(st.status), 0, S)
+        assert int(st.status.item()) == 0
+        assert torch.equal(v, v0)
+        assert torch.equal(s.view(torch.int64), s0.view(torch.int64))
+        assert torch.equal(klo, klo0) and torch.equal(khi, khi0)
+        assert torch.equal(i1, i0)
+        assert torch.equal(c1.view(torch.int64), c0.view(torch.int64))
+        hdr = ws[(wsp - ws.data_ptr()):(wsp - ws.data_ptr()) + 49312]  # sizeof(TopkHdr)
+        assert int(hdr.count_nonzero()) == 0  # the header is left zero for the next call
+
+
+def test_dw_step_sample_miss_flag(cuda):
+    """A truncated level 1 over capacity raises DAL_FLAG_SAMPLE_MISS from the
+    fused sort (the engine then re-runs with the exact level 1)."""
+    import torch
+
+    from dal import _lib, engine
+    from dal._lib import call
+    from dal.forest import Forest
+
+    n, d, k = 50_000, 32, 100
+    X = O.synthetic_pool(n, d, seed=5)
+    st = engine.PoolState(X, excluded=np.arange(10), device=cuda)
+    dens, colsum, norm64 = st.density_fixed(), st.colsum(), st.norms()
+    flags, _, _ = st.row_flags(np.arange(10, n))
+    F = Forest.synthetic(10, 4, d, seed=1)
+    inner, leaf = F.device(cuda)
+    lut = engine.device_lut("entropy", 10, cuda)
+    lib = _lib.load()
+    cap = k  # the bucket bound holds more candidates than k
+    wsb = int(lib.dal_dw_step_workspace_bytes(n, k, cap))
+    ws, wsp = engine.workspace(wsb, cuda)
+    P = lambda t: t.data_ptr()  # noqa: E731
+    outs = [torch.empty(n, dtype=t, device=cuda) for t in (torch.int32, torch.float64, torch.int64, torch.int64)]
+    i1 = torch.empty(k, dtype=torch.int64, device=cuda)
+    c1 = torch.empty(k, dtype=torch.float64, device=cuda)
+    st.status.zero_()
+    call("dal_dw_step", P(st.x), n, d, d, P(inner), P(leaf), 10, 4, P(lut), P(dens), float(engine.density_error(st)),
+         P(flags), 1.0, 0, P(norm64), P(colsum), k, cap, 2, 0, wsp, wsb, *[P(t) for t in outs], P(i1), P(c1), 0,
+         P(st.status), 0, torch.cuda.current_stream(cuda).cuda_stream)
+    assert int(st.status.item()) & _lib.DAL_FLAG_SAMPLE_MISS
