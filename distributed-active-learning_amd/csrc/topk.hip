@@ -66,6 +66,10 @@ struct TopkHdr {
   unsigned long long krem[kPasses + 1];
   unsigned long long kstar, kfinal, total_lt, total_eq;
   unsigned int cand_count, overflow, pad0, pad1;
+  // append_rerank_kernel: (rows with pessimistic key <= tau) << 32 | candidates,
+  // one 64-bit atomic per block sweep
+  unsigned long long packed;
+  unsigned long long pad2;
 };
 
 struct TopkLayout {
@@ -473,6 +477,42 @@ __device__ __forceinline__ bool dw_canonical_score_wave(const DwRerank& R, int64
   return true;
 }
 
+// The same canonical score computed by one lane alone (sequential over f,
+// the row's features fetched 64 at a time); e = lut[vote] passed in when the
+// LUT is held in lanes (n_lut > 0).  For waves with many candidates, where
+// one wave-wide pass per candidate would serialise them.
+__device__ __forceinline__ bool dw_canonical_score_lane(const DwRerank& R, int64_t i, double& s, double e_in,
+                                                        int n_lut) {
+  const uint8_t fl = R.flags ? R.flags[i] : DAL_ROW_CANDIDATE;
+  if (!(fl & DAL_ROW_CANDIDATE)) {
+    s = __builtin_nan("");
+    return false;
+  }
+  const double nr = R.norm64[i];
+  const float* xr = R.x + i * R.ldx;
+  double acc = 0.0;
+  constexpr int kChunk = 64;
+  int f0 = 0;
+  for (; f0 + kChunk <= R.d; f0 += kChunk) {
+    float xv[kChunk];
+#pragma unroll
+    for (int q = 0; q < kChunk; ++q) xv[q] = xr[f0 + q];
+#pragma unroll
+    for (int q = 0; q < kChunk; ++q) {
+      const double u = static_cast<double>(xv[q]) / nr;
+      acc = acc + u * R.colsum[f0 + q];
+    }
+  }
+  for (int f = f0; f < R.d; ++f) {
+    const double u = static_cast<double>(xr[f]) / nr;
+    acc = acc + u * R.colsum[f];
+  }
+  if (fl & DAL_ROW_EXCLUDED) acc = __builtin_nan("");
+  const double e = n_lut ? e_in : R.lut[R.votes[i]];
+  s = e * (R.beta == 1.0 ? acc : pow(acc, R.beta));
+  return true;
+}
+
 // ---------------------------------------------------- truncated level 1 ----
 // dal_dw_step's fused re-rank target (append_rerank_kernel).
 struct AppendRerank {
@@ -540,19 +580,25 @@ __global__ __launch_bounds__(kRadixThreads) void threshold_append_kernel(
   }
 }
 
-// dal_dw_step's candidate search + re-rank: one key per thread (grid-stride),
-// the first keys and the LUT fetched before the level-1 state is resolved,
-// each wave's slot reservation issued before it scores its candidates (the
-// atomic's round trip overlaps the candidate loads), each candidate scored by
-// the whole wave and stored by its own lane.
+// dal_dw_step's candidate search + re-rank: one key per thread (block-uniform
+// grid-stride sweeps), the first keys and the LUT fetched before the level-1
+// state is resolved.  Per sweep the block reserves its candidate slots and
+// counts its rows under tau with ONE packed 64-bit atomic (TopkHdr::packed),
+// issued before the candidates are scored so its round trip overlaps them.
+// A wave with <= 2 candidates scores each with all 64 lanes
+// (dw_canonical_score_wave); with more, each lane scores its own
+// (dw_canonical_score_lane) -- the same operations in the same order either way.
 __global__ __launch_bounds__(kRadixThreads) void append_rerank_kernel(
     const uint64_t* __restrict__ keys_lo, const uint64_t* __restrict__ keys_hi, int64_t n, int64_t idx_base,
     int passes, TopkHdr* __restrict__ h, int64_t* __restrict__ cidx, int64_t cap, AppendRerank AR, int n_lut) {
-  __shared__ uint32_t scan[kRadixThreads / 64];
-  __shared__ unsigned long long red[kRadixThreads / 64];
-  const int tid = threadIdx.x, lane = tid & 63;
+  constexpr int kWaves = kRadixThreads / 64;
+  __shared__ uint32_t scan[kWaves];
+  __shared__ unsigned s_wc[kWaves], s_wb[kWaves];
+  __shared__ unsigned long long s_old;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kRadixThreads;
-  int64_t i = static_cast<int64_t>(blockIdx.x) * kRadixThreads + tid;
+  int64_t b = static_cast<int64_t>(blockIdx.x) * kRadixThreads;
+  int64_t i = b + tid;
   unsigned long long lo = i < n ? keys_lo[i] : DAL_KEY_NONE;
   unsigned long long hi = i < n ? keys_hi[i] : DAL_KEY_NONE;
   const double lut_lane = lane < n_lut ? AR.R.lut[lane] : 0.0;
@@ -561,47 +607,63 @@ __global__ __launch_bounds__(kRadixThreads) void append_rerank_kernel(
   const int sh = digit_shift(passes - 1);
   const unsigned long long tau = prefix | (sh ? ((1ull << sh) - 1ull) : 0ull);
   if (blockIdx.x == 0 && tid == 0) h->kstar = tau;
-  unsigned long long below = 0;
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
-  for (;;) {  // wave-uniform: a wave's lanes hold consecutive rows
+  for (;;) {  // block-uniform
     const bool valid = i < n;
-    below += valid && lo <= tau;
     const bool cand = valid && hi <= tau && hi != DAL_KEY_NONE;
     const unsigned long long cm = __ballot(cand);
+    const unsigned long long bm = __ballot(valid && lo <= tau);
+    if (lane == 0) {
+      s_wc[w] = static_cast<unsigned>(__popcll(cm));
+      s_wb[w] = static_cast<unsigned>(__popcll(bm));
+    }
+    __syncthreads();
+    unsigned before = 0, tot_c = 0, tot_b = 0;
+#pragma unroll
+    for (int q = 0; q < kWaves; ++q) {
+      if (q < w) before += s_wc[q];
+      tot_c += s_wc[q];
+      tot_b += s_wb[q];
+    }
+    unsigned long long old = 0;
+    if (tid == 0 && (tot_c | tot_b))
+      old = atomicAdd(&h->packed, (static_cast<unsigned long long>(tot_b) << 32) | tot_c);
+    double my_s = 0.0;
+    bool my_ok = false;
     if (cm) {
-      unsigned int base = 0;
-      if (lane == 0) base = atomicAdd(&h->cand_count, static_cast<unsigned>(__popcll(cm)));
-      double my_s = 0.0;
-      bool my_ok = false;
-      for (unsigned long long t = cm; t;) {
-        const int l = __ffsll(static_cast<long long>(t)) - 1;
-        t &= t - 1;
-        double sc;
-        const bool ok = dw_canonical_score_wave(AR.R, i - lane + l, sc, lut_lane, n_lut);
-        if (lane == l) {
-          my_s = sc;
-          my_ok = ok;
+      if (__popcll(cm) > 2) {
+        const int v = cand ? AR.R.votes[i] : 0;
+        const double e = n_lut ? __shfl(lut_lane, v) : 0.0;  // every lane active here
+        if (cand) my_ok = dw_canonical_score_lane(AR.R, i, my_s, e, n_lut);
+      } else {
+        for (unsigned long long t = cm; t;) {
+          const int l = __ffsll(static_cast<long long>(t)) - 1;
+          t &= t - 1;
+          double sc;
+          const bool ok = dw_canonical_score_wave(AR.R, i - lane + l, sc, lut_lane, n_lut);
+          if (lane == l) {
+            my_s = sc;
+            my_ok = ok;
+          }
         }
       }
-      const int64_t pos = static_cast<int64_t>(__shfl(base, 0)) + __popcll(cm & lt_mask);
-      if (cand && pos < cap) {
+    }
+    if (tid == 0) s_old = old;
+    __syncthreads();
+    if (cand) {
+      const int64_t pos = static_cast<int64_t>(static_cast<unsigned>(s_old & 0xFFFFFFFFull)) + before +
+                          __popcll(cm & lt_mask);
+      if (pos < cap) {
         cidx[pos] = idx_base + i;
         AR.cpay[pos] = my_s;
         AR.ckey[pos] = my_ok ? score_key(my_s, DAL_DESCENDING) : DAL_KEY_NONE;
       }
     }
-    i += stride;
-    if (i - lane >= n) break;
+    b += stride;
+    if (b >= n) break;
+    i = b + tid;
     lo = i < n ? keys_lo[i] : DAL_KEY_NONE;
     hi = i < n ? keys_hi[i] : DAL_KEY_NONE;
-  }
-  for (int o = 32; o > 0; o >>= 1) below += __shfl_xor(below, o);
-  if (lane == 0) red[tid >> 6] = below;
-  __syncthreads();
-  if (tid == 0) {
-    unsigned long long t = 0;
-    for (int w = 0; w < kRadixThreads / 64; ++w) t += red[w];
-    atomicAdd(&h->total_lt, t);
   }
 }
 
@@ -796,6 +858,7 @@ struct SortTail {
   int64_t clear_words = 0;
   int64_t* const* out_slot = nullptr;
   int32_t* status_mirror = nullptr;
+  bool packed = false;  // counts in TopkHdr::packed (append_rerank_kernel)
 };
 
 __device__ __forceinline__ int64_t* load_out_slot(int64_t* const* slot) {
@@ -825,6 +888,109 @@ __global__ __launch_bounds__(256) void publish_kernel(const int64_t* __restrict_
   }
 }
 
+// Block radix select for sort_kernel: m (<= 4 * kSortThreads) keys, k-th
+// smallest.  Digits of 8 bits MSB first over the keys that still match the
+// resolved prefix; stops as soon as the k-th key's bucket holds <= kSelSmall
+// keys.  Then the keys below the prefix (all in the top k) and the keys in
+// the bucket are compacted (any order) into sk/si/sp[0..m_out).  Returns
+// false (nothing written) when the bucket never shrinks that far (many equal
+// keys): the caller sorts everything.  Block-uniform.
+constexpr int64_t kSelMin = 1024;    // below this the full bitonic is cheap
+constexpr int64_t kSelMaxK = 1536;   // k + kSelSmall must fit the sort arrays
+constexpr int kSelSmall = 512;
+
+__device__ bool select_compact(const uint64_t* __restrict__ keys, const int64_t* __restrict__ idx,
+                               const double* __restrict__ pay, int64_t m, int64_t k, unsigned long long* sk,
+                               long long* si, double* sp, int64_t& m_out) {
+  __shared__ unsigned int hist[256];
+  __shared__ unsigned long long s_prefix;
+  __shared__ unsigned int s_krem, s_neq, s_count;
+  const int tid = threadIdx.x, lane = tid & 63;
+  constexpr int kPer = DAL_SORT_CAP_PAYLOAD / kSortThreads;  // 4
+  unsigned long long key[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int64_t e = tid + static_cast<int64_t>(j) * kSortThreads;
+    key[j] = e < m ? keys[e] : 0ull;
+  }
+  unsigned long long prefix = 0, mask = 0;
+  unsigned int krem = static_cast<unsigned int>(k), neq = static_cast<unsigned int>(m);
+  for (int pass = 0; pass < 8 && neq > static_cast<unsigned int>(kSelSmall); ++pass) {
+    const int shift = 56 - 8 * pass;
+    if (tid < 256) hist[tid] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const bool valid = tid + j * kSortThreads < m && (key[j] & mask) == prefix;
+      const unsigned bin = static_cast<unsigned>((key[j] >> shift) & 255ull);
+      // the wave's most common bin (the first valid lane's) with one atomic
+      const unsigned long long vm = __ballot(valid);
+      if (vm) {
+        const int first = __ffsll(static_cast<long long>(vm)) - 1;
+        const unsigned b0 = __shfl(bin, first);
+        const unsigned long long m0 = __ballot(valid && bin == b0);
+        if (lane == first) atomicAdd(&hist[b0], static_cast<unsigned>(__popcll(m0)));
+        if (valid && bin != b0) atomicAdd(&hist[bin], 1u);
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {  // one wave: 4 bins per lane, inclusive scan, locate krem
+      unsigned c[4], tot = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        c[q] = hist[lane * 4 + q];
+        tot += c[q];
+      }
+      unsigned x = tot;
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+      }
+      unsigned run = x - tot;
+      if (run < krem && run + tot >= krem) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (run < krem && run + c[q] >= krem) {
+            s_prefix = prefix | (static_cast<unsigned long long>(lane * 4 + q) << shift);
+            s_krem = krem - run;
+            s_neq = c[q];
+          }
+          run += c[q];
+        }
+      }
+    }
+    __syncthreads();
+    prefix = s_prefix;
+    krem = s_krem;
+    neq = s_neq;
+    mask |= 255ull << shift;
+    __syncthreads();
+  }
+  if (neq > static_cast<unsigned int>(kSelSmall)) return false;
+  // the k - krem keys below the prefix and the neq keys in its bucket
+  if (tid == 0) s_count = 0u;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int64_t e = tid + static_cast<int64_t>(j) * kSortThreads;
+    const bool take = e < m && (key[j] & mask) <= prefix;
+    const unsigned long long tm = __ballot(take);
+    if (!tm) continue;
+    unsigned base = 0;
+    if (lane == 0) base = atomicAdd(&s_count, static_cast<unsigned>(__popcll(tm)));
+    base = __shfl(base, 0);
+    if (take) {
+      const unsigned p = base + static_cast<unsigned>(__popcll(tm & ((1ull << lane) - 1ull)));
+      sk[p] = key[j];
+      si[p] = idx[e];
+      sp[p] = pay[e];
+    }
+  }
+  __syncthreads();
+  m_out = s_count;
+  return true;
+}
+
 template <bool PAY>
 __global__ __launch_bounds__(kSortThreads) void sort_kernel(const uint64_t* __restrict__ keys,
                                                             const int64_t* __restrict__ idx,
@@ -841,16 +1007,31 @@ __global__ __launch_bounds__(kSortThreads) void sort_kernel(const uint64_t* __re
   __shared__ int64_t* s_dest;
   const int tid = threadIdx.x;
   if (tid == 0) s_dest = load_out_slot(tail.out_slot);  // one host round trip, overlapping the sort
-  int64_t m = h ? static_cast<int64_t>(h->cand_count) : n_static;
-  if (tail.need_k && tid == 0 &&
-      (h->total_lt < static_cast<unsigned long long>(tail.need_k) || m > tail.cap))
+  const unsigned long long packed = tail.packed ? h->packed : 0ull;
+  int64_t m = !h ? n_static : tail.packed ? static_cast<int64_t>(packed & 0xFFFFFFFFull)
+                                          : static_cast<int64_t>(h->cand_count);
+  const unsigned long long total_lt = !h ? 0ull : tail.packed ? (packed >> 32) : h->total_lt;
+  if (tail.need_k && tid == 0 && (total_lt < static_cast<unsigned long long>(tail.need_k) || m > tail.cap))
     atomicOr(tail.status, DAL_FLAG_SAMPLE_MISS);
   if (tail.cap && m > tail.cap) m = tail.cap;
   if (m > CAP) m = CAP;
+  // Large candidate lists (config 3: ~4,000): a block radix select of the
+  // k-th key first (8-bit digits, keys in registers), then only the keys
+  // below its bucket plus the bucket itself (<= kSelSmall) are sorted -- the
+  // full bitonic over 4,096 keys is LDS-bound (~95 us).  Same result: every
+  // key of the top k lies in the sorted subset.
+  bool loaded = false;
+  if (PAY && h && m > kSelMin && k <= kSelMaxK && k < m) loaded = select_compact(keys, idx, pay, m, k, sk, si, sp, m);
   int mp = 2;
   while (mp < m) mp <<= 1;
   for (int i = tid; i < mp; i += kSortThreads) {
-    if (i < m) {
+    if (loaded) {
+      if (i >= m) {
+        sk[i] = ~0ull;
+        si[i] = 0x7FFFFFFFFFFFFFFFll;
+        if (PAY) sp[i] = 0.0;
+      }
+    } else if (i < m) {
       sk[i] = keys[i];
       si[i] = idx[i];
       if (PAY) sp[i] = pay[i];
@@ -1174,6 +1355,7 @@ int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_
   tail.clear_words = kHdrWords;
   tail.out_slot = out_slot;
   tail.status_mirror = status_mirror;
+  tail.packed = true;
   hipLaunchKernelGGL(sort_kernel<true>, dim3(1), dim3(kSortThreads), 0, st, ckey, cidx, cpay, h1, int64_t{0}, k,
                      out_keys, out_idx, out_scores, tail);
   DAL_RETURN_IF_LAUNCH_FAILED();

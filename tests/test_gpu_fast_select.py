@@ -196,7 +196,7 @@ def test_dw_step_matches_separate_calls(cuda, n, d, trees, passes):
         assert torch.equal(klo, klo0) and torch.equal(khi, khi0)
         assert torch.equal(i1, i0)
         assert torch.equal(c1.view(torch.int64), c0.view(torch.int64))
-        hdr = ws[(wsp - ws.data_ptr()):(wsp - ws.data_ptr()) + 49312]  # sizeof(TopkHdr)
+        hdr = ws[(wsp - ws.data_ptr()):(wsp - ws.data_ptr()) + 49328]  # sizeof(TopkHdr)
         assert int(hdr.count_nonzero()) == 0  # the header is left zero for the next call
 
 
