@@ -253,7 +253,8 @@ int forest_score_launch(const float* x, int64_t n, int64_t d, int64_t ldx, const
   const int x_floats = x_lds ? R * static_cast<int>(d + (pad4 ? 4 : 1)) : 0;
   const int64_t n_inner = (int64_t{1} << depth) - 1, n_leaf = int64_t{1} << depth;
   const int64_t f_bytes = n_trees * (n_inner * 8 + n_leaf);
-  const bool f_lds = f_bytes <= 65536;
+  bool f_lds = f_bytes <= 65536;
+  if (const char* e = getenv("DAL_FOREST_FLDS")) f_lds = f_lds && atoi(e) != 0;  // timing knob (A/B runs)
   const int xf = static_cast<int>(round_up(x_floats, 4));  // forest region 16-B aligned
   size_t smem = static_cast<size_t>(xf) * 4 + (f_lds ? static_cast<size_t>(f_bytes) : 0);
   const int64_t blocks = ceil_div(n, R);

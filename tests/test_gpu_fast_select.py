@@ -230,3 +230,29 @@ def test_dw_step_sample_miss_flag(cuda):
          P(flags), 1.0, 0, P(norm64), P(colsum), k, cap, 2, 0, wsp, wsb, *[P(t) for t in outs], P(i1), P(c1), 0,
          P(st.status), 0, torch.cuda.current_stream(cuda).cuda_stream)
     assert int(st.status.item()) & _lib.DAL_FLAG_SAMPLE_MISS
+
+
+@pytest.mark.parametrize("n_distinct", [8, 300])
+def test_many_candidates_and_ties(cuda, n_distinct):
+    """Candidate lists above 1,024 take the block radix select before the
+    one-block sort: with few distinct rows (massive exact ties: the k-th key's
+    bucket never shrinks, full-sort fallback) and with many (the select
+    path), cold and warm (plan) steps equal the oracle, ties to the lower index."""
+    from dal import density_weighting as dw
+    from dal.engine import PoolState
+    from dal.forest import Forest
+
+    n, d, k = 20_000, 32, 150
+    base = O.synthetic_pool(n_distinct, d, seed=21)
+    rng = np.random.default_rng(5)
+    X = base[rng.integers(0, n_distinct, size=n)]
+    of = O.synthetic_forest(10, 4, d, seed=1)
+    F = Forest.synthetic(10, 4, d, seed=1)
+    E = np.arange(10)
+    unl = np.arange(10, n)
+    _, ref_idx, ref_ss = O.density_select(X, unl, of, k, 1.0, E)
+    st = PoolState(X, excluded=E, device=cuda)
+    for _ in range(2):  # cold (dal_dw_step), then warm (dal_dw_plan)
+        sel = dw.select(st, unl, F, k)
+        assert np.array_equal(sel.indices.cpu().numpy(), ref_idx)
+        assert np.array_equal(sel.selected_scores.cpu().numpy().view(np.int64), ref_ss.view(np.int64))
