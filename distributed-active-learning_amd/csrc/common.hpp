@@ -51,11 +51,19 @@ __device__ __forceinline__ double from_fixed(long long a) {
   return static_cast<double>(a) * (1.0 / DAL_FIXED_SCALE);
 }
 
-// Internal hook of dal_dw_step into dal_forest_score's kernel (forest.hip):
-// status_reset (nullable) is zeroed by the first thread, before any later
-// kernel of the step can raise a flag (a replayed step starts clean).
+// Internal hooks of dal_dw_step into dal_forest_score's kernel (forest.hip):
+//   status_reset (nullable) is zeroed by the first thread, before any later
+//                kernel of the step can raise a flag (a replayed step starts clean);
+//   base_flags   (nullable; the warm-step plan) the row flags are built here:
+//                base_flags[r] | (stamp[r] == *step_id ? DAL_ROW_CANDIDATE : 0),
+//                written to row_flags for the step's later kernels -- the
+//                unlabeled rows were stamped by the plan's mark kernel, so no
+//                per-step copy of the base flags.
 struct ForestStepHooks {
   int32_t* status_reset = nullptr;
+  const uint8_t* base_flags = nullptr;
+  const uint32_t* stamp = nullptr;
+  const uint32_t* step_id = nullptr;
 };
 
 int forest_score_launch(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
@@ -73,6 +81,7 @@ int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_
                  int64_t k, int64_t cap, int32_t level1_passes, uint32_t step_flags, void* ws, size_t ws_bytes,
                  int32_t* votes, double* scores, uint64_t* keys_lo, uint64_t* keys_hi, int64_t* out_idx,
                  double* out_scores, uint64_t* out_keys, int32_t* dev_status, dal_event_t colsum_ready,
-                 dal_stream_t stream, int64_t* const* out_slot, int32_t* status_mirror);
+                 dal_stream_t stream, int64_t* const* out_slot, int32_t* status_mirror,
+                 const ForestStepHooks* plan_hooks);
 
 }  // namespace dal

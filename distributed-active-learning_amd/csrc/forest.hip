@@ -68,6 +68,14 @@ __device__ __forceinline__ double density_pow_err(double d, double derr, double 
   return fmax(fabs(hi - p), fabs(p - lo)) * (1.0 + 1e-12) + fabs(p) * 1e-14;
 }
 
+// A row's flags: row_flags[row], or (warm-step plan) the pool's base flags
+// with DAL_ROW_CANDIDATE from this step's mark stamp.
+__device__ __forceinline__ uint8_t row_flag(const ForestArgs& A, int64_t row) {
+  if (!A.hooks.base_flags) return A.flags[row];
+  const bool cand = A.hooks.stamp[row] == *A.hooks.step_id;
+  return static_cast<uint8_t>(A.hooks.base_flags[row] | (cand ? DAL_ROW_CANDIDATE : 0));
+}
+
 template <bool X_LDS, bool F_LDS>
 __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs A, int R, int tpr,
                                                                       int x_floats, bool vec4, bool pad4,
@@ -101,7 +109,7 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
   uint8_t fl_pre = DAL_ROW_CANDIDATE;
   long long dens_pre = 0;
   if (pre && live && sub == 0) {
-    if (A.flags) fl_pre = A.flags[row];
+    if (A.flags) fl_pre = row_flag(A, row);
     if (A.dkind) dens_pre = static_cast<const long long*>(A.density)[row];
   }
   if (X_LDS) {
@@ -181,7 +189,8 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
   for (int o = 1; o < tpr; o <<= 1) v += __shfl_xor(v, o);
   if (!live || sub != 0) return;
 
-  const uint8_t fl = pre ? fl_pre : A.flags ? A.flags[row] : DAL_ROW_CANDIDATE;
+  const uint8_t fl = pre ? fl_pre : A.flags ? row_flag(A, row) : DAL_ROW_CANDIDATE;
+  if (A.hooks.base_flags) const_cast<uint8_t*>(A.flags)[row] = fl;  // the step's flags for the later kernels
   const double e = A.lut[v];
   double s, err = 0.0;
   if (A.dkind) {

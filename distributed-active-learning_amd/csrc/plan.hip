@@ -1,14 +1,17 @@
 // Warm-step plan: one density-weighted AL iteration (dal_dw_step) captured
 // once as a hipGraph over caller-owned static buffers and replayed by
-// dal_dw_plan_run, which also does the per-step refresh (base flags -> step
-// flags, mark the unlabeled rows); the graph's last kernel writes the
+// dal_dw_plan_run.  The per-step refresh (stamp the unlabeled rows, whose list
+// address and length the host leaves in a host-mapped slot; the score kernel
+// builds the step's row flags from the base flags and the stamps) runs inside
+// the graph; the graph's last kernel writes the
 // selection into the caller's fresh buffer and the status word into
-// host-mapped memory -- the host side of a warm step is ONE call and nothing
-// but the stream sync follows the replay.
+// host-mapped memory -- the host side of a warm step is ONE call, and the
+// host spins on that word instead of a blocking stream sync.
 //
 // Reference: the body of density_weighting.py:133-176 (per iteration: T x
 // predict, entropy x density, sortBy, take(window_size)) with the proximity
 // matrix of :58-100 cached across iterations, as the reference does.
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -21,10 +24,48 @@
 // destination (a fresh tensor each step, set by the host before the replay)
 // and the final status word.  No copy launches follow the graph.
 struct PlanSlot {
-  int64_t* out;
+  int64_t* out[2];     // selected indices (int64 [k]), selected scores (fp64 [k])
+  const int64_t* unl;  // this iteration's unlabeled index list (device) ...
+  int64_t n_unl;       // ... and its length
+  uint32_t step;       // this iteration's stamp (1, 2, ...)
   int32_t status;
-  int32_t pad;
 };
+
+namespace {
+
+constexpr int kPlanThreads = 256;
+constexpr int kMarkBlocks = 512;  // fixed at capture: the list length varies per iteration
+
+// In-graph row marking.  The unlabeled list's (address, length) and the
+// step's stamp are copied from the host-mapped slot into device memory by ONE
+// thread (reads of host memory from many blocks serialise: 512 blocks took
+// 274 us), then stamp[r] = step for every listed row of this pool; the score
+// kernel ORs DAL_ROW_CANDIDATE into the base flags where stamp[r] == step (no
+// per-step copy of the flags).
+__global__ __launch_bounds__(64) void plan_fetch_kernel(const PlanSlot* slot, int64_t* __restrict__ args,
+                                                        uint32_t* __restrict__ step_dev) {
+  if (threadIdx.x != 0) return;
+  args[0] = reinterpret_cast<int64_t>(
+      __hip_atomic_load(const_cast<const int64_t**>(&slot->unl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  args[1] = __hip_atomic_load(const_cast<int64_t*>(&slot->n_unl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  *step_dev = __hip_atomic_load(const_cast<uint32_t*>(&slot->step), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(kPlanThreads) void plan_mark_kernel(const int64_t* __restrict__ args,
+                                                                 const uint32_t* __restrict__ step_dev,
+                                                                 int64_t row_base, int64_t n,
+                                                                 uint32_t* __restrict__ stamp) {
+  const int64_t* idx = reinterpret_cast<const int64_t*>(args[0]);
+  const int64_t count = args[1];
+  const uint32_t step = *step_dev;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kPlanThreads;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kPlanThreads + threadIdx.x; t < count; t += stride) {
+    const int64_t r = idx[t] - row_base;
+    if (r >= 0 && r < n) stamp[r] = step;  // duplicates write the same value
+  }
+}
+
+}  // namespace
 
 struct dal_dw_plan {
   hipGraph_t graph = nullptr;
@@ -36,6 +77,9 @@ struct dal_dw_plan {
   int32_t* dev_status = nullptr;
   PlanSlot* slot = nullptr;       // host view
   PlanSlot* slot_dev = nullptr;   // the same words as the device addresses them
+  uint32_t* stamp = nullptr;      // device [n + 1]: per-row mark stamps, then the current step id
+  int64_t* args = nullptr;        // device copy of (slot->unl, slot->n_unl)
+  uint32_t step = 0;
   bool timing = false;            // DAL_PLAN_TIMING=1: host time per phase, printed by destroy
   double t_refresh = 0, t_launch = 0, t_sync = 0;
   int64_t runs = 0;
@@ -70,17 +114,33 @@ extern "C" int dal_dw_plan_create(const float* x, int64_t n, int64_t d, int64_t 
       hipHostGetDevicePointer(reinterpret_cast<void**>(&p->slot_dev), p->slot, 0) != hipSuccess)
     rc = DAL_ERR_HIP;
   if (!rc) {
-    p->slot->out = nullptr;
+    p->slot->out[0] = p->slot->out[1] = nullptr;
+    p->slot->unl = nullptr;
+    p->slot->n_unl = 0;
+    p->slot->step = 0;
     p->slot->status = 0;
   }
+  // stamps start at 0 and steps at 1: no row is marked before its first step
+  if (!rc && (hipMalloc(reinterpret_cast<void**>(&p->stamp), (n + 1) * sizeof(uint32_t)) != hipSuccess ||
+              hipMemsetAsync(p->stamp, 0, (n + 1) * sizeof(uint32_t), st) != hipSuccess ||
+              hipStreamSynchronize(st) != hipSuccess))
+    rc = DAL_ERR_HIP;
+  if (!rc && hipMalloc(reinterpret_cast<void**>(&p->args), 2 * sizeof(int64_t)) != hipSuccess) rc = DAL_ERR_HIP;
   if (!rc && hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) rc = DAL_ERR_HIP;
   if (!rc && hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) != hipSuccess) rc = DAL_ERR_HIP;
   if (!rc) {
+    hipLaunchKernelGGL(plan_fetch_kernel, dim3(1), dim3(64), 0, cs, p->slot_dev, p->args, p->stamp + n);
+    hipLaunchKernelGGL(plan_mark_kernel, dim3(kMarkBlocks), dim3(kPlanThreads), 0, cs, p->args, p->stamp + n,
+                       idx_base, n, p->stamp);
+    ForestStepHooks hooks;
+    hooks.base_flags = base_flags;
+    hooks.stamp = p->stamp;
+    hooks.step_id = p->stamp + n;
     const int step_rc = dw_step_impl(x, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, density_err,
                                      flags, beta, idx_base, norm64, colsum, k, cap, level1_passes,
                                      DAL_STEP_RESET_STATUS | DAL_STEP_WS_CLEAN, ws, ws_bytes, votes, scores, keys_lo,
                                      keys_hi, out_pair, reinterpret_cast<double*>(out_pair + k), out_keys,
-                                     dev_status, nullptr, cs, &p->slot_dev->out, &p->slot_dev->status);
+                                     dev_status, nullptr, cs, p->slot_dev->out, &p->slot_dev->status, &hooks);
     const hipError_t end = hipStreamEndCapture(cs, &p->graph);
     rc = step_rc ? step_rc : (end != hipSuccess ? DAL_ERR_HIP : DAL_OK);
   }
@@ -103,23 +163,30 @@ extern "C" int dal_dw_plan_create(const float* x, int64_t n, int64_t d, int64_t 
   return DAL_OK;
 }
 
-extern "C" int dal_dw_plan_run(dal_dw_plan_t* p, const int64_t* unl, int64_t n_unl, int64_t* out_copy,
-                               int32_t* status_out, dal_stream_t stream) {
+extern "C" int dal_dw_plan_run(dal_dw_plan_t* p, const int64_t* unl, int64_t n_unl, int64_t* out_idx,
+                               double* out_scores, int32_t* status_out, dal_stream_t stream) {
   if (!p || !status_out || (!unl && n_unl)) return DAL_ERR_ARG;
   hipStream_t st = as_stream(stream);
   const double t0 = p->timing ? now_us() : 0.0;
-  if (hipMemcpyAsync(p->flags, p->base_flags, static_cast<size_t>(p->n), hipMemcpyDeviceToDevice, st) != hipSuccess)
-    return DAL_ERR_HIP;
-  int rc = dal_mark_rows(unl, n_unl, p->row_base, p->n, DAL_ROW_CANDIDATE, p->flags, stream);
-  if (rc) return rc;
   volatile PlanSlot* slot = p->slot;
-  slot->out = out_copy;
+  slot->unl = unl;  // read by the graph's first kernel
+  slot->n_unl = n_unl;
+  slot->step = ++p->step;
+  slot->out[0] = out_idx;
+  slot->out[1] = reinterpret_cast<int64_t*>(out_scores);
   slot->status = -1;  // overwritten by the graph's last kernel
   std::atomic_thread_fence(std::memory_order_seq_cst);
   const double t1 = p->timing ? now_us() : 0.0;
   if (hipGraphLaunch(p->exec, st) != hipSuccess) return DAL_ERR_HIP;
   const double t2 = p->timing ? now_us() : 0.0;
-  if (hipStreamSynchronize(st) != hipSuccess) return DAL_ERR_HIP;
+  // the graph's last kernel publishes the status word last: spin on it (a
+  // blocking stream sync wakes up tens of microseconds late), bounded, then
+  // fall back to the sync.  Later work on the stream is ordered after the
+  // graph anyway.
+  const auto spin_end = std::chrono::steady_clock::now() + std::chrono::milliseconds(20);
+  while (slot->status < 0 && std::chrono::steady_clock::now() < spin_end) __builtin_ia32_pause();
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  if (slot->status < 0 && hipStreamSynchronize(st) != hipSuccess) return DAL_ERR_HIP;
   std::atomic_thread_fence(std::memory_order_seq_cst);
   if (p->timing) {
     const double t3 = now_us();
@@ -142,5 +209,7 @@ extern "C" void dal_dw_plan_destroy(dal_dw_plan_t* p) {
   if (p->exec) (void)hipGraphExecDestroy(p->exec);
   if (p->graph) (void)hipGraphDestroy(p->graph);
   if (p->slot) (void)hipHostFree(p->slot);
+  if (p->stamp) (void)hipFree(p->stamp);
+  if (p->args) (void)hipFree(p->args);
   delete p;
 }

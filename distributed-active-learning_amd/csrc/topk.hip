@@ -845,11 +845,11 @@ __global__ __launch_bounds__(256) void gather_selected_kernel(const int64_t* __r
 // candidates -> DAL_FLAG_SAMPLE_MISS), the candidate count clamped to cap, and
 // the level-1 header cleared once every thread has read it, so the next call
 // (a replayed hipGraph) starts from a zero header without a memset launch.
-// Plan publishing (dal_dw_plan_run): out_slot is a host-mapped word holding
-// the device address the selection is also written to (a fresh tensor per
-// step; NULL: none), status_mirror a host-mapped copy of the status word
-// written last -- the host reads both after its stream sync, with no copy
-// launches after the graph.
+// Plan publishing (dal_dw_plan_run): out_slot points at two host-mapped
+// words holding the device addresses the selected indices and scores are
+// also written to (fresh tensors per step; NULL: none), status_mirror at a
+// host-mapped copy of the status word written last -- the host reads both
+// after its stream sync, with no copy launches after the graph.
 struct SortTail {
   int64_t cap = 0;
   int64_t need_k = 0;
@@ -861,8 +861,9 @@ struct SortTail {
   bool packed = false;  // counts in TopkHdr::packed (append_rerank_kernel)
 };
 
-__device__ __forceinline__ int64_t* load_out_slot(int64_t* const* slot) {
-  return slot ? __hip_atomic_load(const_cast<int64_t**>(slot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : nullptr;
+__device__ __forceinline__ int64_t* load_out_slot(int64_t* const* slot, int which) {
+  return slot ? __hip_atomic_load(const_cast<int64_t**>(slot) + which, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+              : nullptr;
 }
 
 __device__ __forceinline__ void publish_status(int32_t* status, int32_t* mirror) {
@@ -875,12 +876,11 @@ __global__ __launch_bounds__(256) void publish_kernel(const int64_t* __restrict_
                                                       const double* __restrict__ out_scores, int64_t k,
                                                       int64_t* const* out_slot, int32_t* status,
                                                       int32_t* status_mirror) {
-  int64_t* dest = load_out_slot(out_slot);
-  if (dest) {
-    for (int64_t i = threadIdx.x; i < k; i += 256) {
-      dest[i] = out_idx[i];
-      dest[k + i] = __double_as_longlong(out_scores[i]);
-    }
+  int64_t* const di = load_out_slot(out_slot, 0);
+  double* const ds = reinterpret_cast<double*>(load_out_slot(out_slot, 1));
+  for (int64_t i = threadIdx.x; i < k; i += 256) {
+    if (di) di[i] = out_idx[i];
+    if (ds) ds[i] = out_scores[i];
   }
   if (status_mirror) {
     __syncthreads();
@@ -1004,9 +1004,9 @@ __global__ __launch_bounds__(kSortThreads) void sort_kernel(const uint64_t* __re
   __shared__ unsigned long long sk[CAP];
   __shared__ long long si[CAP];
   __shared__ double sp[PAY ? CAP : 1];
-  __shared__ int64_t* s_dest;
+  __shared__ int64_t* s_dest[2];
   const int tid = threadIdx.x;
-  if (tid == 0) s_dest = load_out_slot(tail.out_slot);  // one host round trip, overlapping the sort
+  if (tid < 2) s_dest[tid] = load_out_slot(tail.out_slot, tid);  // host round trips, overlapping the sort
   const unsigned long long packed = tail.packed ? h->packed : 0ull;
   int64_t m = !h ? n_static : tail.packed ? static_cast<int64_t>(packed & 0xFFFFFFFFull)
                                           : static_cast<int64_t>(h->cand_count);
@@ -1069,16 +1069,15 @@ __global__ __launch_bounds__(kSortThreads) void sort_kernel(const uint64_t* __re
   if (tail.clear) {  // every thread read the header before the first barrier above
     for (int64_t w = tid; w < tail.clear_words; w += kSortThreads) tail.clear[w] = 0u;
   }
-  int64_t* const dest = s_dest;  // written before the first barrier
+  int64_t* const di = s_dest[0];  // written before the first barrier
+  double* const ds = reinterpret_cast<double*>(s_dest[1]);
   const int64_t kk = k < m ? k : m;
   for (int i = tid; i < kk; i += kSortThreads) {
     if (out_keys) out_keys[i] = sk[i];
     out_idx[i] = si[i];
     if (PAY && out_pay) out_pay[i] = sp[i];
-    if (PAY && dest) {
-      dest[i] = si[i];
-      dest[k + i] = __double_as_longlong(sp[i]);
-    }
+    if (di) di[i] = si[i];
+    if (PAY && ds) ds[i] = sp[i];
   }
   // candidate lists (h != null) shorter than k -- a shard with fewer than k
   // unlabeled rows under the sampled level 1 -- are padded with the NONE key
@@ -1087,10 +1086,8 @@ __global__ __launch_bounds__(kSortThreads) void sort_kernel(const uint64_t* __re
       if (out_keys) out_keys[i] = DAL_KEY_NONE;
       out_idx[i] = -1;
       if (out_pay) out_pay[i] = __builtin_nan("");
-      if (dest) {
-        dest[i] = -1;
-        dest[k + i] = __double_as_longlong(__builtin_nan(""));
-      }
+      if (di) di[i] = -1;
+      if (ds) ds[i] = __builtin_nan("");
     }
   }
   if (tail.status_mirror) {  // last: every status writer of the step has finished
@@ -1295,7 +1292,8 @@ int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_
                  int64_t k, int64_t cap, int32_t level1_passes, uint32_t step_flags, void* ws, size_t ws_bytes,
                  int32_t* votes, double* scores, uint64_t* keys_lo, uint64_t* keys_hi, int64_t* out_idx,
                  double* out_scores, uint64_t* out_keys, int32_t* dev_status, dal_event_t colsum_ready,
-                 dal_stream_t stream, int64_t* const* out_slot, int32_t* status_mirror) {
+                 dal_stream_t stream, int64_t* const* out_slot, int32_t* status_mirror,
+                 const ForestStepHooks* plan_hooks) {
   if (!x || !inner || !leaf || !lut || !density_fixed || !norm64 || !colsum || !ws || !votes || !scores ||
       !keys_lo || !keys_hi || !out_idx || !out_scores || !dev_status)
     return DAL_ERR_ARG;
@@ -1308,6 +1306,7 @@ int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_
   hipStream_t st = as_stream(stream);
   const bool clean = step_flags & DAL_STEP_WS_CLEAN;
   ForestStepHooks hooks;
+  if (plan_hooks) hooks = *plan_hooks;
   if (step_flags & DAL_STEP_RESET_STATUS) hooks.status_reset = dev_status;
   const TopkLayout L1 = topk_layout(n, cap);
   char* base = static_cast<char*>(ws);
@@ -1375,7 +1374,7 @@ extern "C" int dal_dw_step(const float* x, int64_t n, int64_t d, int64_t ldx, co
   return dw_step_impl(x, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, density_err, row_flags, beta,
                       idx_base, norm64, colsum, k, cap, level1_passes, step_flags, ws, ws_bytes, votes, scores,
                       keys_lo, keys_hi, out_idx, out_scores, out_keys, dev_status, colsum_ready, stream, nullptr,
-                      nullptr);
+                      nullptr, nullptr);
 }
 
 extern "C" size_t dal_maxcos_select_workspace_bytes(int64_t n, int64_t k, int64_t cap) {

@@ -37,6 +37,12 @@ def _stream(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+def _raw_stream(device) -> int:
+    """The current HIP stream of ``device`` (an indexed torch.device) as an
+    integer, without building a Stream object (warm-step host path)."""
+    return _torch()._C._cuda_getCurrentRawStream(device.index)
+
+
 def _ptr(t) -> int:
     return t.data_ptr()
 
@@ -45,7 +51,10 @@ def _require_cuda(device):
     torch = _torch()
     if not torch.cuda.is_available():
         raise _lib.DalError("dal requires a ROCm GPU (torch.cuda.is_available() is False)")
-    return torch.device(device if device is not None else "cuda")
+    dev = torch.device(device if device is not None else "cuda")
+    if dev.type == "cuda" and dev.index is None:  # pin the index (raw stream / index checks)
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return dev
 
 
 class Selection:
@@ -417,7 +426,9 @@ def _gram_kind(gram) -> str:
 def _as_index(idx, device):
     torch = _torch()
     if isinstance(idx, torch.Tensor):
-        return idx.to(device=device, dtype=torch.int64)
+        if idx.dtype is torch.int64 and idx.is_cuda and idx.get_device() == device.index and idx.is_contiguous():
+            return idx  # already a device index list (the AL loop's steady state)
+        return idx.to(device=device, dtype=torch.int64).contiguous()
     return torch.from_numpy(np.asarray(idx, dtype=np.int64).reshape(-1)).to(device)
 
 
@@ -766,27 +777,32 @@ class WarmStepGraph:
         self.plan = plan
         self._status = ctypes.c_int32()
         self._status_ref = ctypes.byref(self._status)
+        self._run = lib.dal_dw_plan_run
         self._finalizer = weakref.finalize(self, lib.dal_dw_plan_destroy, plan)
 
     def run(self, forest: Forest, unl):
         """Refresh the inputs, replay, read the status: returns (votes,
-        scores, selection pair, status).  votes / scores are the plan's
-        buffers, valid until the next replay (copy-on-write: the previous
-        step's Selection is materialised before they are reused); the pair
-        (indices | score bits) is a fresh tensor."""
+        scores, selected indices, selected scores, status).  votes / scores
+        are the plan's buffers, valid until the next replay (copy-on-write:
+        the previous step's Selection is materialised before they are
+        reused); the selection lands in fresh tensors."""
         torch = _torch()
         prev = self._last() if self._last is not None else None
         if prev is not None:
             prev._detach()
+        dev = self.state.device
         if forest is not self.forest_ref:
-            inner, leaf = forest.device(self.state.device)
+            inner, leaf = forest.device(dev)
             self.inner.copy_(inner)
             self.leaf.copy_(leaf)
             self.forest_ref = forest
-        pair = torch.empty(2 * self.k, dtype=torch.int64, device=self.state.device)
-        call("dal_dw_plan_run", self.plan, _ptr(unl), int(unl.shape[0]), _ptr(pair), self._status_ref,
-             _stream(self.state.device))
-        return self.votes, self.scores, pair, int(self._status.value)
+        idx = torch.empty(self.k, dtype=torch.int64, device=dev)
+        sc = torch.empty(self.k, dtype=torch.float64, device=dev)
+        rc = self._run(self.plan, unl.data_ptr(), unl.shape[0], idx.data_ptr(), sc.data_ptr(), self._status_ref,
+                       _raw_stream(dev))
+        if rc:
+            _lib.check(rc, "dal_dw_plan_run")
+        return self.votes, self.scores, idx, sc, self._status.value
 
 
 def _density_step_graph(state: PoolState, unl, forest: Forest, kk: int, beta: float) -> Selection:
@@ -803,7 +819,7 @@ def _density_step_graph(state: PoolState, unl, forest: Forest, kk: int, beta: fl
         g = state._graphs.get(key)
         if g is None:
             g = state._graphs[key] = WarmStepGraph(state, forest, kk, beta, cap, passes)
-        votes, scores, pair, st = g.run(forest, unl)
+        votes, scores, idx, sel_scores, st = g.run(forest, unl)
         state.last_status = st
         if st & DAL_FLAG_SAMPLE_MISS:
             state.status.bitwise_and_(~(DAL_FLAG_SAMPLE_MISS | DAL_FLAG_CAND_OVERFLOW))
@@ -814,8 +830,7 @@ def _density_step_graph(state: PoolState, unl, forest: Forest, kk: int, beta: fl
             state.cap_scale *= 4
             continue
         state.check_status(st)
-        sel = Selection(scores=(scores, loc), indices=pair[:kk], selected_scores=pair[kk:].view(torch_float64()),
-                        votes=(votes, loc))
+        sel = Selection(scores=(scores, loc), indices=idx, selected_scores=sel_scores, votes=(votes, loc))
         g._last = weakref.ref(sel)
         return sel
 

@@ -294,13 +294,14 @@ int dal_dw_step(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t
  * ``flags`` is the step's row-flag buffer, rebuilt by every run from
  * ``base_flags`` (the pool's EXCLUDED bits) and the unlabeled list; the
  * selection lands in out_pair[0..k) (indices) and out_pair[k..2k) (fp64
- * score bits).  dal_dw_plan_run(plan, unl, n_unl, out_copy, status, stream):
- * flags <- base_flags, mark unl as DAL_ROW_CANDIDATE, replay (the graph's
- * last kernel also writes the selection to out_copy -- nullable, 2k int64 --
- * and the final status word to host-mapped memory), synchronise ``stream``
- * and return the status in *status -- the density_weighting.py:133-176
- * iteration in one call.  Buffers must outlive the plan; dal_dw_plan_destroy
- * frees it. */
+ * score bits).  dal_dw_plan_run(plan, unl, n_unl, out_idx, out_scores,
+ * status, stream): flags <- base_flags, mark unl as DAL_ROW_CANDIDATE, replay
+ * (the graph's last kernel also writes the selection to out_idx / out_scores
+ * -- nullable, k each -- and the final status word to host-mapped memory),
+ * wait for that word (a bounded spin, then a stream sync) and return the
+ * status in *status -- the
+ * density_weighting.py:133-176 iteration in one call.  Buffers must outlive
+ * the plan; dal_dw_plan_destroy frees it. */
 typedef struct dal_dw_plan dal_dw_plan_t;
 int dal_dw_plan_create(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
                        const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
@@ -310,8 +311,8 @@ int dal_dw_plan_create(const float* x, int64_t n, int64_t d, int64_t ldx, const 
                        size_t ws_bytes, int32_t* votes, double* scores, uint64_t* keys_lo, uint64_t* keys_hi,
                        int64_t* out_pair, uint64_t* out_keys, int32_t* dev_status, dal_stream_t stream,
                        dal_dw_plan_t** plan);
-int dal_dw_plan_run(dal_dw_plan_t* plan, const int64_t* unl, int64_t n_unl, int64_t* out_copy,
-                    int32_t* status, dal_stream_t stream);
+int dal_dw_plan_run(dal_dw_plan_t* plan, const int64_t* unl, int64_t n_unl, int64_t* out_idx,
+                    double* out_scores, int32_t* status, dal_stream_t stream);
 void dal_dw_plan_destroy(dal_dw_plan_t* plan);
 
 /* ---- (a12, config 5) max-cosine to a labeled set -----------------------
