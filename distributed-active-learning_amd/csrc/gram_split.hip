@@ -989,7 +989,7 @@ __global__ __launch_bounds__(kSpThreads, 2) void gram_sym2_kernel(
         const int ch = ct % NCH;
         const bool fresh = fresh_stage && ct < NCH;
         // column tile ct's sums: this wave's turn (wave-uniform branch)
-        const bool sig = SIG && (ct & 3) == wave;
+        const bool sig = SIG && (ct & 3) == wave && DAL_SYM2_ABL != 8;
         acc_t sg = {};
 #pragma unroll
         for (int c = 0; c < C::NKS; ++c) {

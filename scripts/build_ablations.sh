@@ -9,7 +9,7 @@ while [ $# -ge 2 ]; do
   name=$1; defs=$2; shift 2
   d=../../build/$name
   mkdir -p $d/obj
-  for f in abi normalize gram forest topk maxcos ingest rf_train; do cp ../../build/csrc/$f.o $d/obj/$f.o; done
+  for f in abi normalize gram forest topk maxcos ingest rf_train plan; do cp ../../build/csrc/$f.o $d/obj/$f.o; done
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I../../include \
     $defs -c gram_split.hip -o $d/obj/gram_split.o &
 done
