@@ -1198,11 +1198,13 @@ constexpr int kNsRows = 64;
 __global__ __launch_bounds__(256) void normalize_split_kernel(
     const float* __restrict__ x, int64_t n, int d, int64_t ldx, const uint8_t* __restrict__ flags,
     int64_t n_pad, int d_pad, int ks, uint16_t* __restrict__ out, double* __restrict__ norm64,
-    int32_t* __restrict__ status) {
+    int32_t* __restrict__ status, long long* __restrict__ acc_zero) {
   __shared__ float tile[kNsRows][65];
   __shared__ double rnorm[kNsRows];
   const int tid = threadIdx.x;
   const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kNsRows;
+  // the density accumulator of these rows starts at zero (no separate fill)
+  if (acc_zero && tid < kNsRows && row0 + tid < n_pad) acc_zero[row0 + tid] = 0;
   double n2 = 0.0;
   for (int c0 = 0; c0 < d; c0 += 64) {
     // 16 independent loads per thread, all in flight before the LDS writes
@@ -1605,7 +1607,7 @@ extern "C" int dal_canon_colsum_partials(const float* x, int64_t n, int64_t d, i
 
 extern "C" int dal_prep_split(const float* x, int64_t n, int64_t d, int64_t ldx, const uint8_t* row_flags,
                               int64_t n_pad, int64_t d_pad, uint16_t* out, double* norm64, double* partials,
-                              int32_t* dev_status, dal_stream_t stream) {
+                              int64_t* acc_zero, int32_t* dev_status, dal_stream_t stream) {
   if (!x || !out || (!norm64 && n) || !dev_status) return DAL_ERR_ARG;
   if (n < 0 || d < 1 || ldx < d || n_pad < n || n_pad % DAL_ROW_GRANULE || d > (1 << 20)) return DAL_ERR_SHAPE;
   if (d_pad != dal_pad_features(d_pad) || d_pad < d) return DAL_ERR_SHAPE;
@@ -1614,7 +1616,7 @@ extern "C" int dal_prep_split(const float* x, int64_t n, int64_t d, int64_t ldx,
   // vs 21 + 29 us at 100k x 64: too few blocks for the sequential chains)
   hipLaunchKernelGGL(normalize_split_kernel, dim3(static_cast<unsigned>(ceil_div(n_pad, kNsRows))), dim3(256), 0,
                      as_stream(stream), x, n, static_cast<int>(d), ldx, row_flags, n_pad, static_cast<int>(d_pad),
-                     split_ks(d_pad), out, norm64, dev_status);
+                     split_ks(d_pad), out, norm64, dev_status, reinterpret_cast<long long*>(acc_zero));
   DAL_RETURN_IF_LAUNCH_FAILED();
   if (partials && n > 0) return dal_canon_colsum_partials(x, n, d, ldx, norm64, row_flags, partials, stream);
   return DAL_OK;

@@ -58,7 +58,7 @@ SIGNATURES = {
     "dal_split_f16_halves": (c_int64, [c_int64, c_int64]),
     "dal_split_f16": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p]),
     "dal_prep_split": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64, c_int64,
-                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "dal_gram_rowsum_split": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_void_p, c_int,
                                       c_void_p]),
     "dal_density_error_bound_split": (c_double, [c_int64]),

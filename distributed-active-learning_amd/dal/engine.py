@@ -156,6 +156,8 @@ class PoolState:
         self._colsum_partials = None
         self._colsum = None
         self._density_exact = None
+        self._acc_pre = None  # density accumulator already zeroed by the prep kernel
+        self._ws_clean = {}   # (n, k, cap) -> workspace whose top-k header is zero (dal_dw_step)
         self.gram_events = None  # list -> (start, end) HIP events around each Gram call
         self.forest_events = None  # list -> (start, end) HIP events around each forest-score call
         self.select_events = None  # list -> (start, end) HIP events around each dal_dw_select call
@@ -219,15 +221,20 @@ class PoolState:
                  _stream(self.device))
         return self._u, self._norm64
 
-    def gram_operand(self, with_partials: bool = True):
+    def gram_operand(self, with_partials: bool = True, acc_zero=None):
         """The density GEMM's operand for this shard's rows: the fp32 unit rows
         (gram "f32") or their two-term fp16 split [n_pad, 2*d_pad] (gram
         "split", dal_split_f16).  All-gathered as is in the multi-GPU path.
         with_partials: the fused prep also writes the canonical column-sum
-        partials (else they are left to colsum_partials())."""
+        partials (else they are left to colsum_partials()).  acc_zero: an
+        int64 [n_pad] density accumulator to zero (by the prep kernel when it
+        runs here, else by a fill)."""
         if self.gram == "f32":
             u, _ = self.normalized()
+            if acc_zero is not None:
+                acc_zero.zero_()
             return u
+        zeroed = False
         if self._split is None:  # "split" and "sym" share the operand
             torch = _torch()
             self._split = torch.empty((self.n_pad, 2 * self.d_pad), dtype=torch.int16, device=self.device)
@@ -246,11 +253,15 @@ class PoolState:
                     parts = torch.empty((chunks, self.d), dtype=torch.float64, device=self.device)
                 call("dal_prep_split", _ptr(self.x), self.n, self.d, self.d, _ptr(self.flags),
                      self.n_pad, self.d_pad, _ptr(self._split), _ptr(norm64),
-                     0 if parts is None else _ptr(parts), _ptr(self.status), _stream(self.device))
+                     0 if parts is None else _ptr(parts), 0 if acc_zero is None else _ptr(acc_zero),
+                     _ptr(self.status), _stream(self.device))
+                zeroed = True
                 if self._norm64 is None:
                     self._norm64 = norm64
                 if parts is not None:
                     self._colsum_partials = parts
+        if acc_zero is not None and not zeroed:
+            acc_zero.zero_()
         return self._split
 
     def colsum_partials(self):
@@ -286,7 +297,10 @@ class PoolState:
                 raise ValueError("gram 'sym' over a gathered operand: use ShardedSelector")
             if self.gram == "sym" and (self.row_base or self.n_total != self.n):
                 raise ValueError("gram 'sym' on a shard: use ShardedSelector")
-            acc = torch.zeros(self.n_pad, dtype=torch.int64, device=self.device)
+            if u_cols is None and self._acc_pre is not None:
+                acc, self._acc_pre = self._acc_pre, None  # zeroed by the prep kernel
+            else:
+                acc = torch.zeros(self.n_pad, dtype=torch.int64, device=self.device)
             cols = op if u_cols is None else u_cols
             ncp = self.n_pad if n_cols_pad is None else int(n_cols_pad)
             self.gram_accumulate(acc, cols, ncp)
@@ -620,13 +634,20 @@ def dw_step_local(state: PoolState, forest: Forest, flags, dens, lut_dev, k: int
     while True:
         passes = level1_passes(state, n, k, cap)
         wsb = int(lib.dal_dw_step_workspace_bytes(n, k, cap))
-        ws, wsp = workspace(wsb, dev)
+        # one workspace per (n, k, cap), zeroed once: DAL_STEP_WS_CLEAN leaves
+        # its header zero after every call (no zeroing launch per step)
+        key = (n, k, cap)
+        if key not in state._ws_clean:
+            ws, wsp = workspace(wsb, dev)
+            ws.zero_()
+            state._ws_clean[key] = (ws, wsp)
+        ws, wsp = state._ws_clean[key]
         out_idx = torch.empty(k, dtype=torch.int64, device=dev)
         out_scores = torch.empty(k, dtype=torch.float64, device=dev)
         call("dal_dw_step", _ptr(state.x), n, state.d, state.d, _ptr(inner), _ptr(leaf), forest.n_trees,
              forest.depth, _ptr(lut_dev), _ptr(dens), derr, _ptr(flags), float(beta), state.row_base,
-             _ptr(norm64), _ptr(colsum), k, cap, passes, 0, wsp, wsb, _ptr(votes), _ptr(scores), _ptr(keys_lo),
-             _ptr(keys_hi), _ptr(out_idx), _ptr(out_scores), 0, _ptr(state.status),
+             _ptr(norm64), _ptr(colsum), k, cap, passes, DAL_STEP_WS_CLEAN, wsp, wsb, _ptr(votes), _ptr(scores),
+             _ptr(keys_lo), _ptr(keys_hi), _ptr(out_idx), _ptr(out_scores), 0, _ptr(state.status),
              0 if colsum_ready is None else colsum_ready.cuda_event, _stream(dev))
         st = int(state.status.item())  # the step's one host sync
         state.last_status = st
@@ -698,7 +719,12 @@ def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: 
         # runs on a side stream AFTER the Gram, beside the vote / score chain
         # (beside the Gram itself it would slow the persistent Gram blocks)
         torch = _torch()
-        state.gram_operand(with_partials=False)
+        # the fused prep also writes the canonical column-sum partials (the side
+        # stream below then only reduces them: 56 us less per config-2 step than
+        # computing them after the Gram) and zeroes the density accumulator
+        acc = torch.empty(state.n_pad, dtype=torch.int64, device=state.device)
+        state.gram_operand(with_partials=True, acc_zero=acc)
+        state._acc_pre = acc
         dens = state.density_fixed()
         main = torch.cuda.current_stream(state.device)
         side = _side_stream(state.device)

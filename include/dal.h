@@ -155,10 +155,12 @@ int dal_split_f16(const float* u, int64_t n_pad, int64_t d_pad, int64_t ld, uint
  * dal_canon_colsum_partials, same bits (the fp32 unit rows never reach HBM): norm64[i] =
  * canonical ||x_i||, the split operand of the unit rows (E rows, zero-norm
  * rows and padding rows -> zeros) and, if partials != NULL, the canonical
- * column-sum partials [ceil(n / DAL_CANON_CHUNK)][d].  n_pad % 512 == 0. */
+ * column-sum partials [ceil(n / DAL_CANON_CHUNK)][d]; acc_zero (nullable,
+ * int64 [n_pad]: the density accumulator the Gram adds into) is zeroed by the
+ * same kernel (ABI v3).  n_pad % 512 == 0. */
 int dal_prep_split(const float* x, int64_t n, int64_t d, int64_t ldx, const uint8_t* row_flags,
                    int64_t n_pad, int64_t d_pad, uint16_t* out, double* norm64, double* partials,
-                   int32_t* dev_status, dal_stream_t stream);
+                   int64_t* acc_zero, int32_t* dev_status, dal_stream_t stream);
 int dal_gram_rowsum_split(const uint16_t* rows, int64_t n_rows_pad, const uint16_t* cols,
                           int64_t n_cols_pad, int64_t d_pad, int64_t* acc, int grid_blocks,
                           dal_stream_t stream);
