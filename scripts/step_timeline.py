@@ -44,8 +44,12 @@ if __name__ == "__main__":
 
     dev = torch.device("cuda:0")
     n, d = (int(v) for v in os.environ.get("TL_SHAPE", "100000x64").split("x"))
-    x = bench.upload(bench.host_pool(0, n, d, "uniform"), dev)
-    forest = Forest.synthetic(10, 4, d, seed=1, dist="uniform")
+    trees, dist = 10, "uniform"
+    if os.environ.get("TL_CONFIG"):  # a BASELINE config of bench.py (pool, forest)
+        cfg = bench.CONFIGS[os.environ["TL_CONFIG"]]
+        n, d, trees, dist = cfg["n"], cfg["d"], cfg["trees"], cfg["dist"]
+    x = bench.upload(bench.host_pool(0, n, d, dist), dev)
+    forest = Forest.synthetic(trees, 4, d, seed=1, dist=dist)
     unl = torch.arange(10, n, device=dev, dtype=torch.int64)
     state = engine.PoolState(x, excluded=np.arange(10), device=dev)
     warm = len(sys.argv) > 1 and sys.argv[1] == "warm"
