@@ -551,7 +551,20 @@ def main():
                     help="comma list of extra configs reported under 'extra' (default: '2' with config 4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--warm-steps", type=int, default=None)
+    ap.add_argument("--trees", type=int, default=None, help="override the config's forest size (config 4: T=100)")
+    ap.add_argument("--k", type=int, default=None, help="override the config's selection size (config 4: k=1000)")
     args = ap.parse_args()
+    if args.trees is not None or args.k is not None:  # config 4 also at T=100 and k=1000
+        cfg = dict(CONFIGS[args.config])
+        note = []
+        if args.trees is not None and "trees" in cfg:
+            cfg["trees"] = args.trees
+            note.append(f"T={args.trees}")
+        if args.k is not None:
+            cfg["k"] = args.k
+            note.append(f"k={args.k}")
+        cfg["workload"] += f" [override: {', '.join(note)}]"
+        CONFIGS[args.config] = cfg
     big = args.config in ("4",)
     steps = args.steps if args.steps is not None else (5 if big else 50)
     warmup = args.warmup if args.warmup is not None else (1 if big else 10)
