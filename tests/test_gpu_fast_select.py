@@ -256,3 +256,27 @@ def test_many_candidates_and_ties(cuda, n_distinct):
         sel = dw.select(st, unl, F, k)
         assert np.array_equal(sel.indices.cpu().numpy(), ref_idx)
         assert np.array_equal(sel.selected_scores.cpu().numpy().view(np.int64), ref_ss.view(np.int64))
+
+
+def test_warm_plan_exact_level1_and_capacity_growth(cuda):
+    """Warm steps through dal_dw_plan when the truncated level 1 overflows
+    (the plan is rebuilt with the exact level 1: dal_dw_select inside the
+    graph + the publishing kernel) and when the re-rank capacity must grow:
+    every step equals the oracle, and the pool keeps the modes it fell back to."""
+    from dal import engine
+    from dal.forest import Forest
+
+    X, _, E, unl = _case(40_000, 32, seed=13)
+    st = engine.PoolState(X, excluded=E, device=cuda)
+    st.cap_base = 100  # capacity k: the bucket bound overflows the truncated level 1
+    k = 100
+    for it in range(3):
+        F = Forest.synthetic(10, 4, 32, seed=200 + it)
+        of = O.synthetic_forest(10, 4, 32, seed=200 + it)
+        sel = engine.density_step(st, unl, F, k)
+        _, ref_idx, ref_ss = O.density_select(X, unl, of, k, 1.0, E)
+        assert np.array_equal(sel.indices.cpu().numpy(), ref_idx)
+        assert np.array_equal(sel.selected_scores.cpu().numpy().view(np.int64), ref_ss.view(np.int64))
+        unl = np.setdiff1d(unl, ref_idx)
+    assert not st.level1_fast
+    assert len(st._graphs) >= 1  # the warm steps went through a plan
