@@ -1,0 +1,30 @@
+"""dal_forest_score at one BASELINE shape, a few launches, for rocprofv3 --pmc
+(FETCH_SIZE / WRITE_SIZE in separate passes).  usage: python scripts/forest_pmc.py NxDxT [reps]"""
+import os
+import sys
+
+REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(REPO, "distributed-active-learning_amd"))
+sys.path.insert(0, REPO)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from dal import engine  # noqa: E402
+from dal._lib import DAL_DESCENDING  # noqa: E402
+from dal.forest import Forest  # noqa: E402
+
+dev = torch.device("cuda:0")
+n, d, t = (int(v) for v in sys.argv[1].split("x"))
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+dist = "normal" if d == 30 else "uniform"
+x = bench.upload(bench.host_pool(0, n, d, dist), dev)
+forest = Forest.synthetic(t, 4, d, seed=1, dist=dist)
+st = engine.PoolState(x, excluded=np.arange(10), device=dev)
+flags, _, _ = st.row_flags(torch.arange(10, n, device=dev))
+lut = engine.device_lut("entropy", t, dev)
+dens = torch.zeros(st.n_pad, dtype=torch.int64, device=dev)
+for _ in range(reps):
+    engine.forest_score(st, forest, lut, flags, DAL_DESCENDING, density=dens, density_err=1e-3, want_hi=True)
+torch.cuda.synchronize()
+print("ok", n, d, t, reps)
