@@ -79,7 +79,7 @@ __device__ __forceinline__ uint8_t row_flag(const ForestArgs& A, int64_t row) {
 template <bool X_LDS, bool F_LDS>
 __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs A, int R, int tpr,
                                                                       int x_floats, bool vec4, bool pad4,
-                                                                      bool pre) {
+                                                                      bool pre, bool dma) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* xs = reinterpret_cast<float*>(smem);
   if (A.hooks.status_reset && blockIdx.x == 0 && threadIdx.x == 0) *A.hooks.status_reset = 0;
@@ -114,7 +114,33 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
   }
   if (X_LDS) {
     const int rows_here = static_cast<int>(min(static_cast<int64_t>(R), A.n - row0));
-    if (vec4) {
+    if (dma) {
+      // LDS-DMA staging (d % 4 == 0, 16-B-aligned padded rows): one
+      // global_load_lds_dwordx4 per 1 KiB of a row (the last piece with only
+      // the lanes it needs), lane l's 16 B landing at M0 + 16 l; no VGPRs and
+      // no LDS write instructions (2M x 256: 535 -> 433 us)
+      const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+      const int row_bytes = A.d * 4;
+      for (int rr = wave; rr < rows_here; rr += kForestThreads / 64) {
+        const float* src = A.x + (row0 + rr) * A.ldx;
+        for (int p = 0; p * 1024 < row_bytes; ++p) {
+          typedef __attribute__((address_space(3))) float lds_float;
+          const unsigned dst = __builtin_amdgcn_readfirstlane(
+              static_cast<unsigned>(reinterpret_cast<uintptr_t>((lds_float*)(xs + rr * xstride + p * 256))));
+          const unsigned voff = static_cast<unsigned>(p * 1024 + lane * 16);
+          if (static_cast<int>(voff) < row_bytes) {
+            unsigned keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                "global_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(voff), "s"(dst), "s"(src)
+                : "memory");
+          }
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (vec4) {
       // 16-B loads, kStageBatch per thread issued before any LDS write (the
       // block's whole tile in flight: this kernel is an HBM stream)
       constexpr int kStageBatch = 8;
@@ -259,6 +285,10 @@ int forest_score_launch(const float* x, int64_t n, int64_t d, int64_t ldx, const
   if (const char* e = getenv("DAL_FOREST_PAD4")) pad4 = vec4 && atoi(e) != 0;  // timing knob (A/B runs)
   bool pre = true;
   if (const char* e = getenv("DAL_FOREST_PREFETCH")) pre = atoi(e) != 0;  // timing knob (A/B runs)
+  // LDS-DMA staging for wide rows (pad4: d % 4 == 0, ldx % 4 == 0, 16-B-aligned pool); narrow rows
+  // leave most lanes of each DMA instruction idle (2M x 32 x 100: 264 -> 290 us, 100k x 64: 18.4 -> 19.8)
+  bool dma = pad4 && d >= 128;
+  if (const char* e = getenv("DAL_FOREST_DMA")) dma = dma && atoi(e) != 0;  // timing knob (A/B runs)
   const int x_floats = x_lds ? R * static_cast<int>(d + (pad4 ? 4 : 1)) : 0;
   const int64_t n_inner = (int64_t{1} << depth) - 1, n_leaf = int64_t{1} << depth;
   const int64_t f_bytes = n_trees * (n_inner * 8 + n_leaf);
@@ -276,7 +306,7 @@ int forest_score_launch(const float* x, int64_t n, int64_t d, int64_t ldx, const
         hipSuccess)                                                                                 \
       return DAL_ERR_HIP;                                                                           \
     hipLaunchKernelGGL((forest_score_kernel<XL, FL>), grid, dim3(kForestThreads), smem, st, A, R,  \
-                       tpr, xf, vec4, pad4, pre);                                                            \
+                       tpr, xf, vec4, pad4, pre, dma);                                                            \
   } while (0)
   if (x_lds && f_lds) DAL_FOREST_LAUNCH(true, true);
   else if (x_lds) DAL_FOREST_LAUNCH(true, false);
