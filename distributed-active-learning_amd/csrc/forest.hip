@@ -264,7 +264,10 @@ int forest_score_launch(const float* x, int64_t n, int64_t d, int64_t ldx, const
   // 100k x 64 and 284,807 x 30 (scripts/gpu_job63.sh, gpu_job64.sh)
   int R = 256;
   bool x_lds = true;
-  int64_t tile_cap = 16640;
+  // LDS-DMA staging (wide rows, below) holds no registers: 32 KiB tiles there
+  // (2M x 256: 441 -> 411 us; 64 KiB 1248)
+  const bool dma_rows = d >= 128 && d % 4 == 0 && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0;
+  int64_t tile_cap = dma_rows ? 33280 : 16640;
   if (const char* e = getenv("DAL_FOREST_TILE_BYTES")) tile_cap = atoll(e);  // timing knob (A/B runs)
   while (R > 16 && static_cast<int64_t>(R) * (d + 1) * 4 > tile_cap) R >>= 1;
   // wide rows: 16 rows may exceed the preferred tile; LDS staging up to 64 KiB

@@ -31,7 +31,7 @@ def timed(state, forest, lut, flags, dens, err):
 
 
 SHAPES = ((284807, 30, 100, "normal"), (100000, 64, 10, "uniform"),
-                      (100000, 64, 100, "uniform"), (2000000, 256, 10, "uniform"),
+                      (100000, 64, 100, "uniform"), (2000000, 256, 10, "uniform"), (2000000, 256, 100, "uniform"),
                       (2000000, 32, 100, "uniform"))
 if only and only.startswith("sweepT"):  # fixed cost vs trees at the config-3 shape
     SHAPES = tuple((284807, 30, t, "normal") for t in (1, 4, 16, 50, 100))
