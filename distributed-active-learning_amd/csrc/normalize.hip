@@ -8,6 +8,8 @@
 // definition the selected set is bit-exact to, so the library is built with
 // -ffp-contract=off: every multiply and add rounds separately, in the order
 // the oracle uses (sequential over features / rows).
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace dal {
@@ -78,7 +80,7 @@ __global__ __launch_bounds__(kNormThreads) void normalize_rows_kernel(
 // (lanes = features, coalesced loads) into an fp64 LDS tile; wave 0 then adds
 // the 256 rows in order -- the canonical sequence, but with the divisions and
 // loads in parallel.
-constexpr int kColFeat = 16;
+template <int kColFeat>
 __global__ __launch_bounds__(256) void canon_colsum_partials_kernel(
     const float* __restrict__ x, int64_t n, int d, int64_t ldx, const double* __restrict__ norm64,
     const uint8_t* __restrict__ flags, double* __restrict__ partials) {
@@ -251,10 +253,18 @@ extern "C" int dal_canon_colsum_partials(const float* x, int64_t n, int64_t d, i
   if (!x || !norm64 || !partials) return DAL_ERR_ARG;
   if (n < 1 || d < 1 || ldx < d) return DAL_ERR_SHAPE;
   const int64_t chunks = ceil_div(n, DAL_CANON_CHUNK);
-  hipLaunchKernelGGL(canon_colsum_partials_kernel,
-                     dim3(static_cast<unsigned>(chunks), static_cast<unsigned>(ceil_div(d, kColFeat))),
-                     dim3(256), 0, as_stream(stream), x, n, static_cast<int>(d), ldx, norm64,
-                     row_flags, partials);
+  // features per block: 8 (scripts/colsum_ab.py: 100k x 64 33.3 -> 27.8 us, 284,807 x 30
+  // 48.4 -> 36.6, 2M x 256 2.31 -> 1.58 ms against 16; 4 and 32 slower): more, smaller
+  // blocks keep more of the sequential 256-add chains in flight
+  int cf = 8;
+  if (const char* e = getenv("DAL_COLSUM_FEAT")) cf = atoi(e);  // timing knob (A/B runs): 8, 16
+#define DAL_COLSUM_LAUNCH(CF)                                                                             \
+  hipLaunchKernelGGL(canon_colsum_partials_kernel<CF>,                                                   \
+                     dim3(static_cast<unsigned>(chunks), static_cast<unsigned>(ceil_div(d, CF))), dim3(256), \
+                     0, as_stream(stream), x, n, static_cast<int>(d), ldx, norm64, row_flags, partials)
+  if (cf == 16) DAL_COLSUM_LAUNCH(16);
+  else DAL_COLSUM_LAUNCH(8);
+#undef DAL_COLSUM_LAUNCH
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
 }
