@@ -65,6 +65,22 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mark_kernel(const int64_t* 
   }
 }
 
+// The same marking with the list's (address, length) and the step id as kernel
+// arguments, rewritten before each replay by hipGraphExecKernelNodeSetParams:
+// no fetch kernel, no host-memory reads in the graph.  Block 0 publishes the
+// step id for the score kernel.
+__global__ __launch_bounds__(kPlanThreads) void plan_mark_direct_kernel(const int64_t* __restrict__ idx, int64_t count,
+                                                                        uint32_t step, int64_t row_base, int64_t n,
+                                                                        uint32_t* __restrict__ stamp,
+                                                                        uint32_t* __restrict__ step_dev) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *step_dev = step;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kPlanThreads;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kPlanThreads + threadIdx.x; t < count; t += stride) {
+    const int64_t r = idx[t] - row_base;
+    if (r >= 0 && r < n) stamp[r] = step;
+  }
+}
+
 }  // namespace
 
 struct dal_dw_plan {
@@ -79,6 +95,8 @@ struct dal_dw_plan {
   PlanSlot* slot_dev = nullptr;   // the same words as the device addresses them
   uint32_t* stamp = nullptr;      // device [n + 1]: per-row mark stamps, then the current step id
   int64_t* args = nullptr;        // device copy of (slot->unl, slot->n_unl)
+  hipGraphNode_t mark_node = nullptr;  // the direct mark kernel's node (null: fetch-kernel mode)
+  hipKernelNodeParams mark_params{};   // its launch shape, reused by every SetParams
   uint32_t step = 0;
   bool timing = false;            // DAL_PLAN_TIMING=1: host time per phase, printed by destroy
   double t_refresh = 0, t_launch = 0, t_sync = 0;
@@ -127,11 +145,23 @@ extern "C" int dal_dw_plan_create(const float* x, int64_t n, int64_t d, int64_t 
     rc = DAL_ERR_HIP;
   if (!rc && hipMalloc(reinterpret_cast<void**>(&p->args), 2 * sizeof(int64_t)) != hipSuccess) rc = DAL_ERR_HIP;
   if (!rc && hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) rc = DAL_ERR_HIP;
-  if (!rc && hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) != hipSuccess) rc = DAL_ERR_HIP;
-  if (!rc) {
-    hipLaunchKernelGGL(plan_fetch_kernel, dim3(1), dim3(64), 0, cs, p->slot_dev, p->args, p->stamp + n);
-    hipLaunchKernelGGL(plan_mark_kernel, dim3(kMarkBlocks), dim3(kPlanThreads), 0, cs, p->args, p->stamp + n,
-                       idx_base, n, p->stamp);
+  // DAL_PLAN_SETPARAMS=0 keeps the fetch-kernel marking; so does a failed
+  // lookup of the direct mark kernel's node.
+  const char* sp = getenv("DAL_PLAN_SETPARAMS");
+  bool direct = !(sp && atoi(sp) == 0);
+  for (int attempt = 0; attempt < 2 && !rc; ++attempt) {
+    if (hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) != hipSuccess) {
+      rc = DAL_ERR_HIP;
+      break;
+    }
+    if (direct) {
+      hipLaunchKernelGGL(plan_mark_direct_kernel, dim3(kMarkBlocks), dim3(kPlanThreads), 0, cs,
+                         static_cast<const int64_t*>(nullptr), int64_t{0}, 0u, idx_base, n, p->stamp, p->stamp + n);
+    } else {
+      hipLaunchKernelGGL(plan_fetch_kernel, dim3(1), dim3(64), 0, cs, p->slot_dev, p->args, p->stamp + n);
+      hipLaunchKernelGGL(plan_mark_kernel, dim3(kMarkBlocks), dim3(kPlanThreads), 0, cs, p->args, p->stamp + n,
+                         idx_base, n, p->stamp);
+    }
     ForestStepHooks hooks;
     hooks.base_flags = base_flags;
     hooks.stamp = p->stamp;
@@ -143,8 +173,32 @@ extern "C" int dal_dw_plan_create(const float* x, int64_t n, int64_t d, int64_t 
                                      dev_status, nullptr, cs, p->slot_dev->out, &p->slot_dev->status, &hooks);
     const hipError_t end = hipStreamEndCapture(cs, &p->graph);
     rc = step_rc ? step_rc : (end != hipSuccess ? DAL_ERR_HIP : DAL_OK);
+    if (!rc && hipGraphInstantiate(&p->exec, p->graph, nullptr, nullptr, 0) != hipSuccess) rc = DAL_ERR_HIP;
+    if (rc || !direct) break;
+    // find the direct mark kernel's node: its arguments change every replay
+    size_t n_nodes = 0;
+    hipGraphNode_t nodes[64];
+    if (hipGraphGetNodes(p->graph, nullptr, &n_nodes) == hipSuccess && n_nodes <= 64 &&
+        hipGraphGetNodes(p->graph, nodes, &n_nodes) == hipSuccess) {
+      for (size_t i = 0; i < n_nodes && !p->mark_node; ++i) {
+        hipGraphNodeType ty;
+        hipKernelNodeParams kp{};
+        if (hipGraphNodeGetType(nodes[i], &ty) != hipSuccess || ty != hipGraphNodeTypeKernel) continue;
+        if (hipGraphKernelNodeGetParams(nodes[i], &kp) != hipSuccess) continue;
+        if (kp.func == reinterpret_cast<void*>(&plan_mark_direct_kernel)) {
+          p->mark_node = nodes[i];
+          p->mark_params = kp;
+        }
+      }
+    }
+    if (p->mark_node) break;
+    // not found: recapture with the fetch kernel
+    (void)hipGraphExecDestroy(p->exec);
+    (void)hipGraphDestroy(p->graph);
+    p->exec = nullptr;
+    p->graph = nullptr;
+    direct = false;
   }
-  if (!rc && hipGraphInstantiate(&p->exec, p->graph, nullptr, nullptr, 0) != hipSuccess) rc = DAL_ERR_HIP;
   if (cs) (void)hipStreamDestroy(cs);
   if (rc) {
     dal_dw_plan_destroy(p);
@@ -169,9 +223,21 @@ extern "C" int dal_dw_plan_run(dal_dw_plan_t* p, const int64_t* unl, int64_t n_u
   hipStream_t st = as_stream(stream);
   const double t0 = p->timing ? now_us() : 0.0;
   volatile PlanSlot* slot = p->slot;
-  slot->unl = unl;  // read by the graph's first kernel
-  slot->n_unl = n_unl;
-  slot->step = ++p->step;
+  const uint32_t step = ++p->step;
+  if (p->mark_node) {
+    hipKernelNodeParams np = p->mark_params;
+    int64_t row_base = p->row_base, n = p->n;
+    uint32_t* stamp = p->stamp;
+    uint32_t* step_dev = p->stamp + p->n;
+    void* kargs[7] = {&unl, &n_unl, const_cast<uint32_t*>(&step), &row_base, &n, &stamp, &step_dev};
+    np.kernelParams = kargs;
+    np.extra = nullptr;
+    if (hipGraphExecKernelNodeSetParams(p->exec, p->mark_node, &np) != hipSuccess) return DAL_ERR_HIP;
+  } else {
+    slot->unl = unl;  // read by the graph's fetch kernel
+    slot->n_unl = n_unl;
+    slot->step = step;
+  }
   slot->out[0] = out_idx;
   slot->out[1] = reinterpret_cast<int64_t*>(out_scores);
   slot->status = -1;  // overwritten by the graph's last kernel
@@ -204,7 +270,8 @@ extern "C" int dal_dw_plan_run(dal_dw_plan_t* p, const int64_t* unl, int64_t n_u
 extern "C" void dal_dw_plan_destroy(dal_dw_plan_t* p) {
   if (!p) return;
   if (p->timing && p->runs)
-    fprintf(stderr, "dal_dw_plan: %lld runs, host us per run: refresh %.1f, graph launch %.1f, sync %.1f\n",
+    fprintf(stderr, "dal_dw_plan (%s): %lld runs, host us per run: refresh %.1f, graph launch %.1f, sync %.1f\n",
+            p->mark_node ? "setparams" : "fetch",
             static_cast<long long>(p->runs), p->t_refresh / p->runs, p->t_launch / p->runs, p->t_sync / p->runs);
   if (p->exec) (void)hipGraphExecDestroy(p->exec);
   if (p->graph) (void)hipGraphDestroy(p->graph);
