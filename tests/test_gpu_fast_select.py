@@ -280,3 +280,29 @@ def test_warm_plan_exact_level1_and_capacity_growth(cuda):
         unl = np.setdiff1d(unl, ref_idx)
     assert not st.level1_fast
     assert len(st._graphs) >= 1  # the warm steps went through a plan
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("setparams", ["1", "0"])
+def test_warm_plan_marking_modes(cuda, monkeypatch, setparams):
+    """The plan's per-step marking, both ways: kernel arguments rewritten per
+    replay (hipGraphExecKernelNodeSetParams, the default) and the host-mapped
+    slot read by a fetch kernel (DAL_PLAN_SETPARAMS=0).  The unlabeled list
+    shrinks every step (stale stamps of earlier steps must not count) and the
+    selections equal the oracle's."""
+    from dal import engine
+    from dal.forest import Forest
+
+    monkeypatch.setenv("DAL_PLAN_SETPARAMS", setparams)
+    X, _, E, unl = _case(30_000, 64, seed=17)
+    st = engine.PoolState(X, excluded=E, device=cuda)
+    F = Forest.synthetic(10, 4, 64, seed=31)
+    of = O.synthetic_forest(10, 4, 64, seed=31)
+    k = 64
+    for it in range(5):
+        sel = engine.density_step(st, unl, F, k)
+        _, ref_idx, ref_ss = O.density_select(X, unl, of, k, 1.0, E)
+        assert np.array_equal(sel.indices.cpu().numpy(), ref_idx), it
+        assert np.array_equal(sel.selected_scores.cpu().numpy().view(np.int64), ref_ss.view(np.int64)), it
+        unl = np.setdiff1d(unl, ref_idx)[: max(k, len(unl) - 3000)]
+    assert len(st._graphs) >= 1
