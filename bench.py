@@ -290,6 +290,63 @@ def _max_over_ranks(vals, world, dist, tdev):
     return [float(v) for v in t]
 
 
+def host_colsum64(x_host: np.ndarray, lo: int, n_excluded: int, chunk: int = 65536) -> np.ndarray:
+    """fp64 sum of the unit rows u_j = x_j / ||x_j|| of this rank's rows that
+    are not in E = {0..n_excluded-1} (global indices; rows [lo, lo + len)).
+    numpy, independent of the library: the reference for the accuracy block."""
+    n_loc, d = x_host.shape
+    s = np.zeros(d, dtype=np.float64)
+    for c0 in range(0, n_loc, chunk):
+        xc = x_host[c0:c0 + chunk].astype(np.float64)
+        xc /= np.sqrt(np.einsum("ij,ij->i", xc, xc))[:, None]
+        xc[np.arange(lo + c0, lo + c0 + xc.shape[0]) < n_excluded] = 0.0
+        s += xc.sum(axis=0)
+    return s
+
+
+def sample_rows(n_loc: int, lo: int, n_excluded: int, m: int) -> np.ndarray:
+    """Up to m evenly spaced local rows outside E (always the shard's first and last scored rows)."""
+    first = max(0, n_excluded - lo)
+    if first >= n_loc:
+        return np.zeros(0, dtype=np.int64)
+    return np.unique(np.linspace(first, n_loc - 1, min(m, n_loc - first)).round().astype(np.int64))
+
+
+def density_accuracy(x_host, lo, gram_density, colsum, n_excluded, m=4096):
+    """SURVEY §8(d) accuracy instrumentation: the Gram-path density of m
+    sampled rows against d_i = <u_i, s> in fp64 on the host (``colsum`` = s
+    over every row outside E).  Returns (max, mean) relative error and the
+    smallest |d_ref| of the sample, the max absolute error, and the sample size."""
+    pick = sample_rows(x_host.shape[0], lo, n_excluded, m)
+    if pick.size == 0:
+        return 0.0, 0.0, float("inf"), 0.0, 0
+    xs = x_host[pick].astype(np.float64)
+    xs /= np.sqrt(np.einsum("ij,ij->i", xs, xs))[:, None]
+    d_ref = xs @ colsum
+    err = np.abs(np.asarray(gram_density(pick), dtype=np.float64) - d_ref)
+    rel = err / np.abs(d_ref)
+    return float(rel.max()), float(rel.mean()), float(np.abs(d_ref).min()), float(err.max()), int(pick.size)
+
+
+def abs_rowsum_tolerance(x_host, pick, gram_density, n_excluded, m=256, chunk=32768):
+    """SURVEY §8(d) config-3 tolerance form: max_i |d_gram_i - d_ref_i| / sum_j |S_ij|
+    (j outside E) over m of the sampled rows, fp64 on the host over every
+    column (one GPU: the host holds the whole pool)."""
+    pick = pick[np.linspace(0, pick.size - 1, min(m, pick.size)).round().astype(np.int64)]
+    us = x_host[pick].astype(np.float64)
+    us /= np.sqrt(np.einsum("ij,ij->i", us, us))[:, None]
+    d_ref = np.zeros(pick.size)
+    a_ref = np.zeros(pick.size)
+    for c0 in range(max(n_excluded, 0), x_host.shape[0], chunk):
+        xc = x_host[c0:c0 + chunk].astype(np.float64)
+        xc /= np.sqrt(np.einsum("ij,ij->i", xc, xc))[:, None]
+        S = us @ xc.T
+        d_ref += S.sum(axis=1)
+        a_ref += np.abs(S).sum(axis=1)
+    err = np.abs(np.asarray(gram_density(pick), dtype=np.float64) - d_ref)
+    return float((err / a_ref).max())
+
+
 def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, backend, cpu=True):
     """Density-weighted selection on one config; returns the JSON dict."""
     import torch
@@ -339,6 +396,27 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
     gram_ms = sum(a.elapsed_time(b) for a, b in events) / max(steps, 1)
     elapsed, gram_ms_max = _max_over_ranks([elapsed, gram_ms], world, dist, tdev)
 
+    # accuracy (outside the timed region): the timed step's
+    # Gram density on sampled rows vs an fp64 host restatement
+    s_host = host_colsum64(x_host, lo, N_EXCLUDED)
+    if world > 1:
+        t = torch.from_numpy(s_host).to(tdev)
+        dist.all_reduce(t)
+        s_host = t.cpu().numpy()
+    dens_gram = state.density("gram")
+    acc_max, acc_mean, dref_min, abs_max, n_acc = density_accuracy(
+        x_host, lo, lambda pick: dens_gram[torch.from_numpy(pick).to(dev)].cpu().numpy(), s_host, N_EXCLUDED)
+    tol_abs = None
+    if world == 1 and cfg["dist"] == "normal" and n * d <= 20_000_000:  # signed data (config 3)
+        tol_abs = abs_rowsum_tolerance(x_host, sample_rows(n, 0, N_EXCLUDED, 4096),
+                                       lambda pick: dens_gram[torch.from_numpy(pick).to(dev)].cpu().numpy(),
+                                       N_EXCLUDED)
+    del dens_gram
+    err_bound = float(engine.density_error(state))
+    n_cols = n - N_EXCLUDED
+    acc_max, acc_mean_max, bound_rel, abs_ncols = _max_over_ranks(
+        [acc_max, acc_mean, err_bound / dref_min, abs_max / n_cols], world, dist, tdev)
+
     # self-check (outside the timed region): the timed step's selection equals
     # the exact separable-density selection, indices and fp64 score bits
     idx_s, sc_s = step("separable")
@@ -381,6 +459,15 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
         (ts,) = _max_over_ranks([ts], world, dist, tdev)
         sep_ms = ts * 1000 / warm_steps
 
+    # k-th boundary gap: the (k+1)-best score from the exact path, beside the
+    # observed Gram error (the exact re-rank makes the selection independent of it)
+    if world > 1:
+        _, sc_k1 = parallel.select(sel, comm, unl, forest, k + 1, mode="dw", density_mode="separable")
+    else:
+        sc_k1 = engine.density_step(state, unl, forest, k + 1, mode="separable").selected_scores
+    sk = sc_k1.cpu().numpy()
+    gap_rel = float((sk[k - 1] - sk[k]) / abs(sk[k - 1])) if len(sk) > k and sk[k - 1] != 0 else None
+
     # roofline of the dominant kernel (density Gram row-sum), this rank's launch
     rows_local = (hi - lo) - int(np.sum((excluded >= lo) & (excluded < hi)))
     flops = 2.0 * rows_local * (n - N_EXCLUDED) * d
@@ -415,6 +502,22 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
                        "warm_selection_equals_cold_selection": warm_same, "k": k,
                        "note": "last timed step vs the exact O(N*D) density path, and the last warm step "
                                "vs the cold one: indices + fp64 score bits"},
+        "accuracy": {"density_max_rel_err": acc_max, "density_mean_rel_err": acc_mean_max,
+                     "density_max_abs_err_over_ncols": abs_ncols,
+                     "density_err_bound_over_ncols": err_bound / n_cols,
+                     "density_max_err_over_abs_rowsum": tol_abs,
+                     "sampled_rows_per_rank": n_acc,
+                     "density_err_bound_rel": bound_rel,
+                     "kth_gap_rel": gap_rel,
+                     "note": "Gram-path density (MFMA, fixed point) of evenly spaced sampled rows vs "
+                             "<u_i, sum_j u_j> in fp64 numpy on the host (max over ranks); *_over_ncols: "
+                             "absolute errors / (N - |E|) >= sum_j |S_ij| / (N - |E|) scale, the form "
+                             "for signed data; *_over_abs_rowsum: |dd_i| / sum_j |S_ij| on 256 of the "
+                             "sampled rows (SURVEY config-3 tolerance 1e-5; signed one-GPU pools); "
+                             "the bound is the rigorous interval "
+                             "half-width; "
+                             "kth_gap_rel = (s_k - s_k+1) / |s_k| of the exact scores (the selection "
+                             "itself is exact: interval keys + fp64 re-rank)"},
         "separable": ({"cold_selection_latency_ms": sep_ms, "rows_per_s": n_scored / (sep_ms * 1e-3),
                        "note": "density via the exact O(N*D) identity sum_j<u_i,u_j> = <u_i, sum_j u_j> "
                                "(canonical fp64, same selection); HBM-bound, not the MFMA path"}

@@ -35,3 +35,44 @@ def test_shard_ranges_cover_the_pool():
             assert got[0][0] == 0 and got[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(got, got[1:]))
             assert all(lo % 512 == 0 for lo, _ in got)
+
+
+def test_density_accuracy_host_reference():
+    """bench.py's accuracy block: the host fp64 column sum and sampled-row
+    densities equal a brute-force full Gram row-sum (E excluded), sharded or not."""
+    rng = np.random.default_rng(5)
+    x = rng.random((300, 7), dtype=np.float32)
+    u = x.astype(np.float64) / np.linalg.norm(x.astype(np.float64), axis=1, keepdims=True)
+    S = u @ u.T
+    n_ex = 10
+    d_full = S[:, n_ex:].sum(axis=1)
+    s = bench.host_colsum64(x, 0, n_ex, chunk=64)
+    s2 = bench.host_colsum64(x[:130], 0, n_ex, chunk=50) + bench.host_colsum64(x[130:], 130, n_ex)
+    assert np.allclose(s, s2, rtol=1e-14, atol=0)
+    for lo, hi in ((0, 300), (0, 130), (130, 300), (5, 12)):
+        got = {}
+
+        def dens(pick, lo=lo):
+            got["pick"] = pick
+            return d_full[lo + pick] * (1 + 1e-9)
+
+        mx, mean, dmin, amax, m = bench.density_accuracy(x[lo:hi], lo, dens, s, n_ex, m=50)
+        pick = got["pick"]
+        assert m == len(pick) and len(pick) <= 50
+        assert np.all(lo + pick >= n_ex) and pick.max() == hi - lo - 1
+        assert abs(mx - 1e-9) < 1e-12 and abs(mean - 1e-9) < 1e-12
+        assert np.isclose(dmin, np.abs(d_full[lo + pick]).min())
+    assert bench.sample_rows(5, 0, 10, 50).size == 0
+
+
+def test_abs_rowsum_tolerance():
+    rng = np.random.default_rng(6)
+    x = rng.standard_normal((500, 5), dtype=np.float32)
+    u = x.astype(np.float64) / np.linalg.norm(x.astype(np.float64), axis=1, keepdims=True)
+    S = u @ u.T
+    d_full, a_full = S[:, 10:].sum(axis=1), np.abs(S[:, 10:]).sum(axis=1)
+    pick = bench.sample_rows(500, 0, 10, 100)
+    sub = pick[np.linspace(0, pick.size - 1, 20).round().astype(np.int64)]
+    got = bench.abs_rowsum_tolerance(x, pick, lambda p: d_full[p] + 1e-7 * a_full[p], 10, m=20, chunk=64)
+    assert abs(got - 1e-7) < 1e-12
+    assert sub.size == 20
