@@ -76,3 +76,13 @@ def test_abs_rowsum_tolerance():
     got = bench.abs_rowsum_tolerance(x, pick, lambda p: d_full[p] + 1e-7 * a_full[p], 10, m=20, chunk=64)
     assert abs(got - 1e-7) < 1e-12
     assert sub.size == 20
+
+
+def test_cpu_baseline_small_pool():
+    """Both CPU-baseline variants (full fp64 Gram row-sum; separable density) run on a small pool."""
+    cfg = dict(bench.CONFIGS["2"])
+    x = bench.host_pool(0, 3000, 16, "uniform")
+    of = O.synthetic_forest(cfg["trees"], cfg["depth"], 16, seed=1, dist="uniform")
+    r = bench.cpu_baseline(x, cfg, of, budget_s=0.3)
+    assert r["value"] > 0 and r["kind"] == "port" and r["cores"] >= 1
+    assert r["separable"]["value"] > 0 and "separable" not in r["sample"]
