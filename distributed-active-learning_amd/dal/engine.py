@@ -613,11 +613,13 @@ def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k
 
 
 def dw_step_local(state: PoolState, forest: Forest, flags, dens, lut_dev, k: int, beta: float, colsum,
-                  colsum_ready=None):
-    """dal_dw_step on this (single-GPU) pool: votes, scores and interval keys
+                  colsum_ready=None, cap_scale: int = None, sync: bool = True):
+    """dal_dw_step on this pool or shard: votes, scores and interval keys
     of every row, then the exact canonical top-k -- one C call with fused
     launches (the truncated level 1).  Same retries as dw_select_local.
-    Returns (votes, scores, indices, selected scores)."""
+    Returns (votes, scores, indices, selected scores); sync=False (the
+    multi-GPU path: the caller reads the status word after the merge and
+    re-runs with a larger ``cap_scale``) also returns the selected keys."""
     torch = _torch()
     lib = _lib.load()
     n = state.n
@@ -630,7 +632,7 @@ def dw_step_local(state: PoolState, forest: Forest, flags, dens, lut_dev, k: int
     keys_lo = torch.empty(n, dtype=torch.int64, device=dev)
     keys_hi = torch.empty(n, dtype=torch.int64, device=dev)
     base = candidate_cap(n, k) if state.cap_base is None else max(int(k), int(state.cap_base))
-    cap = int(min(n, base * state.cap_scale))
+    cap = int(min(n, base * (state.cap_scale if cap_scale is None else cap_scale)))
     while True:
         passes = level1_passes(state, n, k, cap)
         wsb = int(lib.dal_dw_step_workspace_bytes(n, k, cap))
@@ -644,11 +646,15 @@ def dw_step_local(state: PoolState, forest: Forest, flags, dens, lut_dev, k: int
         ws, wsp = state._ws_clean[key]
         out_idx = torch.empty(k, dtype=torch.int64, device=dev)
         out_scores = torch.empty(k, dtype=torch.float64, device=dev)
+        out_keys = None if sync else torch.empty(k, dtype=torch.int64, device=dev)
         call("dal_dw_step", _ptr(state.x), n, state.d, state.d, _ptr(inner), _ptr(leaf), forest.n_trees,
              forest.depth, _ptr(lut_dev), _ptr(dens), derr, _ptr(flags), float(beta), state.row_base,
              _ptr(norm64), _ptr(colsum), k, cap, passes, DAL_STEP_WS_CLEAN, wsp, wsb, _ptr(votes), _ptr(scores),
-             _ptr(keys_lo), _ptr(keys_hi), _ptr(out_idx), _ptr(out_scores), 0, _ptr(state.status),
+             _ptr(keys_lo), _ptr(keys_hi), _ptr(out_idx), _ptr(out_scores),
+             0 if out_keys is None else _ptr(out_keys), _ptr(state.status),
              0 if colsum_ready is None else colsum_ready.cuda_event, _stream(dev))
+        if not sync:
+            return votes, scores, out_idx, out_scores, out_keys
         st = int(state.status.item())  # the step's one host sync
         state.last_status = st
         if st & DAL_FLAG_SAMPLE_MISS:  # truncated level 1 over capacity: exact level 1 from now on

@@ -224,7 +224,8 @@ class ShardedSelector:
     def local_select(self, u_full, partials_full, unlabeled_idx, forest, k: int, mode: str = "dw",
                      strategy: str = "least_confidence", beta: float = 1.0,
                      density_mode: str = "gram") -> LocalTopk:
-        from .engine import (density_error, device_lut, dw_select_local, forest_score, topk_keys)
+        from .engine import (density_error, device_lut, dw_select_local, dw_step_local, forest_score,
+                             topk_keys)
         from .luts import ASCENDING
 
         torch = __import__("torch")
@@ -253,10 +254,14 @@ class ShardedSelector:
             dens = self.local_density(u_full)
             colsum = st.colsum(partials_full)
             lut_dev = device_lut("entropy", forest.n_trees, st.device)
-            votes, sc, klo, khi = forest_score(st, forest, lut_dev, flags, DAL_DESCENDING, density=dens,
-                                               density_err=density_error(st), beta=beta, want_hi=True)
-            i, s, kk_keys = dw_select_local(st, flags, votes, klo, khi, lut_dev, kk, beta, colsum,
-                                            cap_scale=self.cap_scale, sync=False)
+            if st.events_off():  # one fused call (dal_dw_step), as the single-GPU step
+                _, _, i, s, kk_keys = dw_step_local(st, forest, flags, dens, lut_dev, kk, beta, colsum,
+                                                    cap_scale=self.cap_scale, sync=False)
+            else:  # bench per-kernel timing: K2 and K3 as separate calls
+                votes, sc, klo, khi = forest_score(st, forest, lut_dev, flags, DAL_DESCENDING, density=dens,
+                                                   density_err=density_error(st), beta=beta, want_hi=True)
+                i, s, kk_keys = dw_select_local(st, flags, votes, klo, khi, lut_dev, kk, beta, colsum,
+                                                cap_scale=self.cap_scale, sync=False)
         else:
             order = DAL_ASCENDING if ASCENDING[strategy] else DAL_DESCENDING
             lut_dev = device_lut(strategy, forest.n_trees, st.device)

@@ -44,7 +44,25 @@ def single():
     return r.indices, r.selected_scores
 
 
-for name, fn in (("single", single), ("sharded-P1", sharded), ("single", single), ("sharded-P1", sharded)):
+def single_warm():
+    r = engine.density_step(st, unl, forest, k)
+    return r.indices, r.selected_scores
+
+
+def sharded_warm():  # density cached: one fused dal_dw_step per rank
+    return parallel.select(sel, comm, unl, forest, k, mode="dw")
+
+
+def sharded_warm_sep():  # the same with K2 and K3 as separate calls (event-timed path)
+    sel.state.forest_events, sel.state.select_events = [], []
+    r = parallel.select(sel, comm, unl, forest, k, mode="dw")
+    sel.state.forest_events = sel.state.select_events = None
+    return r
+
+
+for name, fn in (("single", single), ("sharded-P1", sharded), ("single", single), ("sharded-P1", sharded),
+                 ("single-warm", single_warm), ("sh-warm-fused", sharded_warm), ("sh-warm-sep", sharded_warm_sep),
+                 ("sh-warm-fused", sharded_warm), ("sh-warm-sep", sharded_warm_sep)):
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
@@ -52,8 +70,10 @@ for name, fn in (("single", single), ("sharded-P1", sharded), ("single", single)
     for _ in range(steps):
         idx, sc = fn()
     torch.cuda.synchronize()
-    print(f"{name:11s} {1000 * (time.perf_counter() - t0) / steps:.3f} ms/step", flush=True)
+    print(f"{name:14s} {1000 * (time.perf_counter() - t0) / steps:.3f} ms/step", flush=True)
 a = single()
 b = sharded()
-print("same selection:", bool(torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])), flush=True)
+c = sharded_warm()
+print("same selection:", bool(torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[0], c[0])
+                              and torch.equal(a[1], c[1])), flush=True)
 dist.destroy_process_group()
