@@ -1443,26 +1443,32 @@ inline int64_t sym2_pairs(int64_t P, int64_t a, int64_t b, int64_t skip_lo, int6
 }
 
 // Column-chunk count for the super-block kernel's units (P, chunk of J),
-// dealt round-robin: the fewest chunks whose most loaded block has at most 8 %
-// more pairs than the best balance found (exact pair counts; cached per shape).
-// Fewer chunks = fewer A-fragment loads and row flushes per block; at 100k x 64
-// and 284,807 x 30 five chunks beat the best-balanced 10-28 by 2-3 %.
+// dealt round-robin: the fewest chunks, at least kSym2MinChunks, whose most
+// loaded block has at most 8 % more pairs than the best balance found (exact
+// pair counts; cached per shape).  Fewer chunks = fewer A-fragment loads and
+// row flushes per block; more chunks = a smaller column working set swept by
+// every block together (MALL hits): at 2M x 256 16-32 chunks beat the 1 the
+// balance rule alone picks by 3.9 % (500k x 256: 1.7 %, 4M x 64: 0.9 %;
+// scripts/gram_knob_ab.py).  Chunk mode only runs for operands > 40 MB.
+constexpr int64_t kSym2MinChunks = 16;
 inline int64_t sym2_chunks(int64_t srow0, int64_t n_srb, int64_t lo, int64_t hi, int64_t skip_lo, int64_t skip_hi,
                            int64_t ns_active, int64_t G0) {
   if (const char* e = getenv("DAL_GRAM_NC")) {  // timing knob: force the chunk count
     const int64_t f = atoll(e);
     if (f > 0) return f < hi - lo ? f : hi - lo;
   }
+  int64_t min_nc = kSym2MinChunks;
+  if (const char* e = getenv("DAL_GRAM_NC_MIN")) min_nc = atoll(e);  // A/B knob (1 = balance rule only)
   struct Entry {
-    int64_t k[8];
+    int64_t k[9];
     int64_t nc;
   };
   static thread_local Entry cache[8] = {};
   static thread_local int cache_next = 0;
-  const int64_t key[8] = {srow0, n_srb, lo, hi, skip_lo, skip_hi, ns_active, G0};
+  const int64_t key[9] = {srow0, n_srb, lo, hi, skip_lo, skip_hi, ns_active, G0, min_nc};
   for (const Entry& e : cache) {
     bool hit = e.nc > 0;
-    for (int i = 0; i < 8 && hit; ++i) hit = e.k[i] == key[i];
+    for (int i = 0; i < 9 && hit; ++i) hit = e.k[i] == key[i];
     if (hit) return e.nc;
   }
   const int64_t nj = hi - lo;
@@ -1487,15 +1493,17 @@ inline int64_t sym2_chunks(int64_t srow0, int64_t n_srb, int64_t lo, int64_t hi,
     cand.emplace_back(ncc, mx);
     if (best_max < 0 || mx < best_max) best_max = mx;
   }
-  int64_t best_nc = cand.back().first;
-  for (const auto& c : cand)
-    if (c.second * 100 <= best_max * 108) {
-      best_nc = c.first;
-      break;
-    }
+  int64_t best_nc = -1;
+  for (int pass = 0; pass < 2 && best_nc < 0; ++pass)  // at least min_nc chunks if balanced, else any
+    for (const auto& c : cand)
+      if ((pass || c.first >= min_nc) && c.second * 100 <= best_max * 108) {
+        best_nc = c.first;
+        break;
+      }
+  if (best_nc < 0) best_nc = cand.back().first;
   Entry& e = cache[cache_next];
   cache_next = (cache_next + 1) % 8;
-  for (int i = 0; i < 8; ++i) e.k[i] = key[i];
+  for (int i = 0; i < 9; ++i) e.k[i] = key[i];
   e.nc = best_nc;
   return best_nc;
 }
