@@ -1515,14 +1515,14 @@ int launch_sym2(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint16
   const int G0 = grid_blocks > 0 ? grid_blocks : 2 * device_cus_split();
   const int64_t nj = j_hi - j_lo;
   // scheduling: contiguous equal shares of the pair grid per block when the
-  // column operand is L2/MALL-resident (<= 40 MB: 100k x 64 = 25.6 MB is 2 %,
-  // 284,807 x 30 = 36.5 MB is 3 % faster), else round-robin column-chunk
-  // units, whose blocks sweep the same column stages together (200k x 64 =
-  // 51 MB: 3 %, 500k x 256: 6 % faster than contiguous).  Exact integer
-  // accumulation: the schedule never changes the bits.
+  // column operand is small (<= 32 MB: 100k x 64 = 25.6 MB is 2-5 % faster),
+  // else round-robin column-chunk units, whose blocks sweep the same column
+  // stages together (with the 16-chunk floor: 284,807 x 30 = 36.5 MB 2.7 %,
+  // 200k x 64 = 51 MB 3 %, 500k x 256 6 % faster than contiguous).  Exact
+  // integer accumulation: the schedule never changes the bits.
   // DAL_GRAM_CONTIG=0/1 forces one (A/B knob).
   const char* cenv = getenv("DAL_GRAM_CONTIG");
-  const int contig = cenv ? atoi(cenv) != 0 : nj * 256 * ldh * 2 <= (int64_t{40} << 20);
+  const int contig = cenv ? atoi(cenv) != 0 : nj * 256 * ldh * 2 <= (int64_t{32} << 20);
   int64_t cbk = nj, n_chunks = 1, G;
   if (contig) {
     const int64_t sl = skip_lo > j_lo ? skip_lo : j_lo, sh = skip_hi < j_hi ? skip_hi : j_hi;

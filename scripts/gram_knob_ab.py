@@ -27,11 +27,12 @@ for shape in os.environ.get("AB_SHAPES", "1000000x256").split(","):
     ref = None
     for r in range(rounds + 1):
         for v in variants:
-            for key in ("DAL_GRAM_NC", "DAL_GRAM_NC_MIN", "DAL_GRAM_CONTIG"):
+            for key in ("DAL_GRAM_NC", "DAL_GRAM_NC_MIN", "DAL_GRAM_CONTIG", "DAL_GRAM_ANT"):
                 os.environ.pop(key, None)
             if v != "default":
-                kk, val = v.rsplit("=", 1)
-                os.environ["DAL_GRAM_" + kk] = val
+                for part in v.split("+"):  # e.g. CONTIG=0+NC=32
+                    kk, val = part.rsplit("=", 1)
+                    os.environ["DAL_GRAM_" + kk] = val
             st.clear_caches()
             st.gram_operand()
             torch.cuda.synchronize()
@@ -52,5 +53,5 @@ for shape in os.environ.get("AB_SHAPES", "1000000x256").split(","):
               f"{flops / ms / 1e9 / 1666.67:.3f} of 1667", flush=True)
     del st, x
     torch.cuda.empty_cache()
-for key in ("DAL_GRAM_NC", "DAL_GRAM_NC_MIN", "DAL_GRAM_CONTIG"):
+for key in ("DAL_GRAM_NC", "DAL_GRAM_NC_MIN", "DAL_GRAM_CONTIG", "DAL_GRAM_ANT"):
     os.environ.pop(key, None)
