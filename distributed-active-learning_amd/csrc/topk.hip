@@ -1425,6 +1425,69 @@ extern "C" int dal_interval_keys_f32(const float* values, int64_t n, double err,
   return DAL_OK;
 }
 
+// ---- multi-GPU merge over the packed all-gather --------------------------
+// packed [n_ranks][width] int64: keys [k] | global indices [k] | fp64 score
+// bits [k] (| status word): one all-gather's output, read in place.
+namespace dal {
+namespace {
+__global__ __launch_bounds__(256) void merge_unpack_kernel(const int64_t* __restrict__ packed, int64_t n_ranks,
+                                                           int64_t width, int64_t k, uint64_t* __restrict__ keys,
+                                                           int64_t* __restrict__ pos,
+                                                           int32_t* __restrict__ status_or) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (status_or && t == 0) {
+    int32_t s = 0;
+    for (int64_t r = 0; r < n_ranks; ++r) s |= static_cast<int32_t>(packed[r * width + 3 * k]);
+    *status_or = s;
+  }
+  if (t >= n_ranks * k) return;
+  const int64_t r = t / k, i = t - r * k;
+  keys[t] = static_cast<uint64_t>(packed[r * width + i]);
+  pos[t] = t;  // rank-major: lists are sorted per rank and ranks hold ascending rows
+}
+
+__global__ __launch_bounds__(256) void merge_gather_kernel(const int64_t* __restrict__ packed, int64_t width,
+                                                           int64_t k, const int64_t* __restrict__ best,
+                                                           int64_t* __restrict__ out_idx,
+                                                           double* __restrict__ out_scores) {
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (j >= k) return;
+  const int64_t p = best[j], r = p / k, i = p - r * k;
+  out_idx[j] = packed[r * width + k + i];
+  out_scores[j] = __builtin_bit_cast(double, packed[r * width + 2 * k + i]);
+}
+}  // namespace
+}  // namespace dal
+
+extern "C" size_t dal_topk_merge_workspace_bytes(int64_t n_ranks, int64_t k) {
+  if (n_ranks < 1 || k < 1) return 0;
+  return static_cast<size_t>(n_ranks * k) * 16 + static_cast<size_t>(k) * 16;
+}
+
+extern "C" int dal_topk_merge(const int64_t* packed, int64_t n_ranks, int64_t width, int64_t k, void* ws,
+                              size_t ws_bytes, int64_t* out_idx, double* out_scores, uint64_t* out_keys,
+                              int32_t* status_or, dal_stream_t stream) {
+  if (!packed || !ws || !out_idx || !out_scores) return DAL_ERR_ARG;
+  if (n_ranks < 1 || k < 1 || width < 3 * k + (status_or ? 1 : 0)) return DAL_ERR_SHAPE;
+  const int64_t n = n_ranks * k;
+  if (n > DAL_SORT_CAP) return DAL_ERR_CAPACITY;
+  if (ws_bytes < dal_topk_merge_workspace_bytes(n_ranks, k)) return DAL_ERR_CAPACITY;
+  hipStream_t st = as_stream(stream);
+  uint64_t* keys = static_cast<uint64_t*>(ws);
+  int64_t* pos = reinterpret_cast<int64_t*>(keys + n);
+  uint64_t* ws_keys = reinterpret_cast<uint64_t*>(pos + n);
+  int64_t* best = reinterpret_cast<int64_t*>(ws_keys + k);
+  if (!out_keys) out_keys = ws_keys;
+  hipLaunchKernelGGL(merge_unpack_kernel, dim3(static_cast<unsigned>(ceil_div(n, 256))), dim3(256), 0, st, packed,
+                     n_ranks, width, k, keys, pos, status_or);
+  hipLaunchKernelGGL(sort_kernel<false>, dim3(1), dim3(kSortThreads), 0, st, keys, pos, nullptr, nullptr, n, k,
+                     out_keys, best, nullptr, SortTail{});
+  hipLaunchKernelGGL(merge_gather_kernel, dim3(static_cast<unsigned>(ceil_div(k, 256))), dim3(256), 0, st, packed,
+                     width, k, best, out_idx, out_scores);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}
+
 extern "C" int dal_sort_pairs(const uint64_t* keys, const int64_t* idx, const double* payload, int64_t n,
                               int64_t k, uint64_t* out_keys, int64_t* out_idx, double* out_payload,
                               dal_stream_t stream) {

@@ -108,6 +108,9 @@ SIGNATURES = {
     "dal_maxcos_select": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64,
                                   c_int64, c_void_p, c_int64, c_int64, c_int32, c_void_p, c_size_t, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p]),
+    "dal_topk_merge_workspace_bytes": (c_size_t, [c_int64, c_int64]),
+    "dal_topk_merge": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_size_t, c_void_p, c_void_p,
+                               c_void_p, c_void_p, c_void_p]),
     "dal_sort_pairs": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
                                c_void_p, c_void_p]),
     "dal_gram_entries": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p]),

@@ -395,12 +395,15 @@ def select(sel: ShardedSelector, comm, unlabeled_idx, forest, k: int, mode: str 
     # every rank's status word (zero-norm rows, re-rank capacity overflow)
     # rides in the top-k all-gather and is read once, after the merge is
     # queued: the step's one host sync, and every rank sees the same bits
-    keys_all, idx_all, sc_all, st_all = gather_topk(comm, top, sel.status_word())
     n_unl_global = int(unl.shape[0])  # single source of truth for the candidate count
-    out = merge_topk(keys_all, idx_all, sc_all, k, sort_fn, all_valid=n_unl_global >= k)
-    st = 0
-    for v in st_all.tolist():
-        st |= int(v)
+    if sort_fn is hip_sort_positions and sel.world * k <= _lib.DAL_SORT_CAP and top.keys.is_cuda:
+        out, st = merge_packed(comm, top, sel.status_word(), k, all_valid=n_unl_global >= k)
+    else:
+        keys_all, idx_all, sc_all, st_all = gather_topk(comm, top, sel.status_word())
+        out = merge_topk(keys_all, idx_all, sc_all, k, sort_fn, all_valid=n_unl_global >= k)
+        st = 0
+        for v in st_all.tolist():
+            st |= int(v)
     if mode != "dw":
         st &= ~_lib.DAL_FLAG_ZERO_NORM  # a zero row only matters to the cosine density
     if st & _lib.DAL_FLAG_ZERO_NORM:
@@ -430,6 +433,37 @@ def gather_topk(comm, top: LocalTopk, status=None):
     if status is not None:
         out = out + (g[:, 3 * k],)
     return out
+
+
+def merge_packed(comm, top: LocalTopk, status, k: int, all_valid: bool = False):
+    """gather_topk + merge_topk in one all-gather and one C call
+    (dal_topk_merge reads the gathered [P, 3k+1] rows in place: unpack, sort
+    by (key, rank-major position), gather; the status words OR-ed on the
+    device).  Returns ((indices, scores), status) -- the status read is the
+    step's one host sync."""
+    torch = __import__("torch")
+    from .engine import _ptr, _stream
+    from ._lib import call
+
+    dev = top.keys.device
+    packed = torch.cat([top.keys, top.idx, top.scores.view(torch.int64), status.reshape(1).to(torch.int64)])
+    w = int(packed.shape[0])
+    g = comm.all_gather(packed.reshape(1, w))  # [P, 3k + 1]
+    n_ranks = int(g.shape[0])
+    lib = _lib.load()
+    wsb = int(lib.dal_topk_merge_workspace_bytes(n_ranks, k))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    out_idx = torch.empty(k, dtype=torch.int64, device=dev)
+    out_sc = torch.empty(k, dtype=torch.float64, device=dev)
+    out_keys = None if all_valid else torch.empty(k, dtype=torch.int64, device=dev)
+    st_or = torch.empty(1, dtype=torch.int32, device=dev)
+    call("dal_topk_merge", _ptr(g), n_ranks, w, k, _ptr(ws), wsb, _ptr(out_idx), _ptr(out_sc),
+         0 if out_keys is None else _ptr(out_keys), _ptr(st_or), _stream(dev))
+    st = int(st_or.item())
+    if out_keys is not None:
+        valid = out_keys != _as_i64(DAL_KEY_NONE)
+        out_idx, out_sc = out_idx[valid], out_sc[valid]
+    return (out_idx, out_sc), st
 
 
 def emulate(selectors, unlabeled_idx, forest, k: int, mode: str = "dw",

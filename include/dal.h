@@ -376,6 +376,21 @@ int dal_sort_pairs(const uint64_t* keys, const int64_t* idx, const double* paylo
                    int64_t k, uint64_t* out_keys, int64_t* out_idx, double* out_payload,
                    dal_stream_t stream);
 
+/* dal_topk_merge: the same merge read straight from one all-gather's output.
+ * packed [n_ranks][width] int64 rows = a rank's k keys | k global indices |
+ * k fp64 score bit patterns (| its status word at 3k when status_or is
+ * given).  Writes the k best by (key, rank-major position) -- ties resolve
+ * by global row index -- to out_idx / out_scores, and the OR of the status
+ * words to *status_or (nullable), the winners' keys to out_keys (nullable;
+ * DAL_KEY_NONE marks padding that won only because fewer than k candidates
+ * exist).  Three launches; n_ranks * k <= DAL_SORT_CAP.
+ * Replaces the sortBy(...).take(k) of density_weighting.py:168,172 across
+ * shards (the Spark range-partition sort over all executors). */
+size_t dal_topk_merge_workspace_bytes(int64_t n_ranks, int64_t k);
+int dal_topk_merge(const int64_t* packed, int64_t n_ranks, int64_t width, int64_t k, void* ws, size_t ws_bytes,
+                   int64_t* out_idx, double* out_scores, uint64_t* out_keys, int32_t* status_or,
+                   dal_stream_t stream);
+
 /* ---- pool ingest (host-side parser) -------------------------------------
  * Replaces uncertainty_sampling.py:37-42 / density_weighting.py:45-53,59-65
  * (sc.textFile -> split -> LabeledPoint(0 if int(_[-1]) == -1 else 1,

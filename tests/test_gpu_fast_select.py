@@ -306,3 +306,53 @@ def test_warm_plan_marking_modes(cuda, monkeypatch, setparams):
         assert np.array_equal(sel.selected_scores.cpu().numpy().view(np.int64), ref_ss.view(np.int64)), it
         unl = np.setdiff1d(unl, ref_idx)[: max(k, len(unl) - 3000)]
     assert len(st._graphs) >= 1
+
+
+class _OneShotComm:
+    """all_gather of an already gathered [P, w] tensor (the merge alone)."""
+
+    def __init__(self, g):
+        self.g = g
+
+    def all_gather(self, t):
+        return self.g
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_ranks,k,pad", [(1, 5, 0), (3, 100, 0), (8, 1000, 0), (4, 64, 40), (5, 7, 7)])
+def test_topk_merge_packed(cuda, n_ranks, k, pad):
+    """dal_topk_merge over a packed all-gather equals the (key, rank-major
+    position) merge: per-rank lists sorted by (key, index), ranks in row
+    order, many tied keys, padding keys at the tail, statuses OR-ed."""
+    import torch
+
+    from dal import _lib, parallel
+
+    rng = np.random.default_rng(n_ranks * 1000 + k)
+    none = np.uint64(_lib.DAL_KEY_NONE)
+    rows = []
+    keys_all, idx_all, sc_all = [], [], []
+    for r in range(n_ranks):
+        keys = np.sort(rng.integers(0, 50, size=k).astype(np.uint64) * np.uint64(1 << 40))
+        idx = r * 100_000 + np.sort(rng.choice(100_000, size=k, replace=False)).astype(np.int64)
+        if pad:
+            keys[k - pad:] = none
+            idx[k - pad:] = -1
+        sc = rng.random(k)
+        st = np.int64(1 << r if r < 3 else 0)
+        rows.append(np.concatenate([keys.view(np.int64), idx, sc.view(np.int64), [st]]))
+        keys_all.append(keys)
+        idx_all.append(idx)
+        sc_all.append(sc)
+    g = torch.from_numpy(np.stack(rows)).to(cuda)
+    K, I, S = np.concatenate(keys_all), np.concatenate(idx_all), np.concatenate(sc_all)
+    order = np.lexsort((np.arange(K.size), K))[:k]
+    valid = K[order] != none
+    top = parallel.LocalTopk(g[0, :k], g[0, k:2 * k], g[0, 2 * k:3 * k].contiguous().view(torch.float64))
+    status = g[0, 3 * k:3 * k + 1].to(torch.int32)
+    for all_valid in ((True, False) if not pad else (False,)):
+        (oi, os_), st = parallel.merge_packed(_OneShotComm(g), top, status, k, all_valid=all_valid)
+        want = order if all_valid else order[valid]
+        assert np.array_equal(oi.cpu().numpy(), I[want])
+        assert np.array_equal(os_.cpu().numpy().view(np.int64), S[want].view(np.int64))
+        assert st == sum(1 << r for r in range(min(n_ranks, 3)))
