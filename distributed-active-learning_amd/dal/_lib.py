@@ -49,6 +49,7 @@ SIGNATURES = {
     "dal_density_error_bound": (c_double, [c_int64]),
     "dal_normalize_rows": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64, c_int64,
                                    c_void_p, c_void_p, c_void_p, c_void_p]),
+    "dal_mark_rows_count": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
     "dal_mark_rows": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p]),
     "dal_canon_colsum_partials": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p,
                                           c_void_p, c_void_p]),

@@ -136,13 +136,14 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
     else:
         flags = torch.zeros(n, dtype=torch.uint8, device=dev)
         gidx = _as_index(candidates, dev)
-        _lib.call("dal_mark_rows", _ptr(gidx), int(gidx.shape[0]), int(row_base), n, DAL_ROW_CANDIDATE,
-                  _ptr(flags), _stream(dev))
+        # the marking kernel also counts the candidates inside this shard
+        in_range = torch.empty(1, dtype=torch.int32, device=dev)
+        _lib.call("dal_mark_rows_count", _ptr(gidx), int(gidx.shape[0]), int(row_base), n, DAL_ROW_CANDIDATE,
+                  _ptr(flags), _ptr(in_range), _stream(dev))
         cand = gidx - row_base if row_base else gidx
         # an upper bound until the status read: global candidates of other
         # shards are not ours (filtered below, off the common path)
         n_cand = int(cand.shape[0])
-        in_range = ((cand >= 0) & (cand < n)).sum(dtype=torch.int32).reshape(1)
         if n_cand == 0:
             return Selection(scores=mx[cand], indices=torch.empty(0, dtype=torch.int64, device=dev),
                              selected_scores=torch.empty(0, dtype=torch.float64, device=dev))

@@ -104,6 +104,12 @@ int dal_normalize_rows(const float* x, int64_t n, int64_t d, int64_t ldx,
  * list without a host round trip. */
 int dal_mark_rows(const int64_t* idx, int64_t count, int64_t row_base, int64_t n, int bits,
                   uint8_t* flags, dal_stream_t stream);
+/* dal_mark_rows that also writes to *in_range (device int32, zeroed by the
+ * call) how many of the count indices fall inside this shard -- the
+ * candidate count of a shard given global candidates, with no extra pass
+ * (ABI v4). */
+int dal_mark_rows_count(const int64_t* idx, int64_t count, int64_t row_base, int64_t n, int bits,
+                        uint8_t* flags, int32_t* in_range, dal_stream_t stream);
 
 /* ---- canonical fp64 column sum (re-rank side of the density) -----------
  * partials[c][f] = sum over rows c*256 .. c*256+255 (< n, not EXCLUDED) of
