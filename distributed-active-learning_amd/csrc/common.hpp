@@ -51,6 +51,41 @@ __device__ __forceinline__ double from_fixed(long long a) {
   return static_cast<double>(a) * (1.0 / DAL_FIXED_SCALE);
 }
 
+__device__ __forceinline__ float bf16_bits_to_f32(uint16_t b) { return __uint_as_float(static_cast<unsigned>(b) << 16); }
+
+// sum_f x_f^2 of one bf16 row in fp64, sequential in f (the canonical order);
+// 16-B aligned rows with d % 8 == 0 are read 64 features at a time (8
+// independent loads in flight instead of d dependent-latency scalar loads).
+__device__ __forceinline__ double row_sq_norm_bf16(const uint16_t* __restrict__ xr, int d) {
+  double s = 0.0;
+  if ((reinterpret_cast<uintptr_t>(xr) & 15) == 0 && (d & 7) == 0) {
+    for (int f0 = 0; f0 < d; f0 += 64) {
+      uint4 q[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        q[j] = f0 + 8 * j < d ? *reinterpret_cast<const uint4*>(xr + f0 + 8 * j) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (f0 + 8 * j >= d) break;
+        const uint32_t w[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {  // little endian: feature 2e in the low half
+          const double lo = bf16_bits_to_f32(static_cast<uint16_t>(w[e] & 0xFFFFu));
+          const double hi = bf16_bits_to_f32(static_cast<uint16_t>(w[e] >> 16));
+          s = s + lo * lo;
+          s = s + hi * hi;
+        }
+      }
+    }
+    return s;
+  }
+  for (int f = 0; f < d; ++f) {
+    const double v = bf16_bits_to_f32(xr[f]);
+    s = s + v * v;
+  }
+  return s;
+}
+
 // Internal hooks of dal_dw_step into dal_forest_score's kernel (forest.hip):
 //   status_reset (nullable) is zeroed by the first thread, before any later
 //                kernel of the step can raise a flag (a replayed step starts clean);

@@ -319,39 +319,6 @@ __global__ __launch_bounds__(256, OCC) void maxcos_kernel(
   }
 }
 
-// sum_f x_f^2 of one bf16 row in fp64, sequential in f (the canonical order);
-// 16-B aligned rows with d % 8 == 0 are read 64 features at a time (8
-// independent loads in flight instead of d dependent-latency scalar loads).
-__device__ __forceinline__ double row_sq_norm_bf16(const uint16_t* __restrict__ xr, int d) {
-  double s = 0.0;
-  if ((reinterpret_cast<uintptr_t>(xr) & 15) == 0 && (d & 7) == 0) {
-    for (int f0 = 0; f0 < d; f0 += 64) {
-      uint4 q[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        q[j] = f0 + 8 * j < d ? *reinterpret_cast<const uint4*>(xr + f0 + 8 * j) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (f0 + 8 * j >= d) break;
-        const uint32_t w[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {  // little endian: feature 2e in the low half
-          const double lo = bf16_to_f32(static_cast<uint16_t>(w[e] & 0xFFFFu));
-          const double hi = bf16_to_f32(static_cast<uint16_t>(w[e] >> 16));
-          s = s + lo * lo;
-          s = s + hi * hi;
-        }
-      }
-    }
-    return s;
-  }
-  for (int f = 0; f < d; ++f) {
-    const double v = bf16_to_f32(xr[f]);
-    s = s + v * v;
-  }
-  return s;
-}
-
 // 1/||x|| (fp32) of bf16 rows, ||x||^2 summed in fp64; zero rows flag status.
 // Rows in [n, n_pad) get NaN (padding of the labeled table).
 __global__ __launch_bounds__(256) void inv_norms_bf16_kernel(const uint16_t* __restrict__ x, int64_t n,
@@ -408,14 +375,7 @@ __global__ __launch_bounds__(256) void maxcos_argmax_resolve_kernel(const uint16
   for (int q = 0; q < cnt; ++q) {
     const int64_t row = static_cast<int64_t>(blockIdx.x) * 256 + list[q];
     const uint16_t* xr = pool + row * ld;
-    if (tid == 0) {
-      double n2 = 0.0;
-      for (int f = 0; f < d; ++f) {
-        const double v = bf16_to_f32(xr[f]);
-        n2 = n2 + v * v;
-      }
-      s_nr = __builtin_sqrt(n2);
-    }
+    if (tid == 0) s_nr = __builtin_sqrt(row_sq_norm_bf16(xr, d));
     __syncthreads();
     if (tid < d) su[tid] = static_cast<double>(bf16_to_f32(xr[tid])) / s_nr;
     __syncthreads();

@@ -733,12 +733,7 @@ __global__ __launch_bounds__(256) void rerank_maxcos_kernel(const TopkHdr* __res
     const int64_t c = c0 + wave;
     if (c < count) {
       const uint16_t* xr = pool + (cidx[c] - idx_base) * ld;
-      double n2 = 0.0;
-      for (int f = 0; f < d; ++f) {
-        const double v = bf16f(xr[f]);
-        n2 = n2 + v * v;
-      }
-      const double nr = __builtin_sqrt(n2);
+      const double nr = __builtin_sqrt(row_sq_norm_bf16(xr, d));  // sequential in f, vector loads
       for (int f = lane; f < d; f += 64) su[f][wave] = static_cast<double>(bf16f(xr[f])) / nr;
     } else {
       for (int f = lane; f < d; f += 64) su[f][wave] = 0.0;
