@@ -15,6 +15,8 @@
 // Host code only (no kernels): a byte range is split at line starts into one
 // segment per thread; each thread counts its rows, the counts are prefix-summed
 // and each thread parses its rows into their final positions.
+#include <locale.h>
+
 #include <cerrno>
 #include <cstdlib>
 #include <thread>
@@ -62,16 +64,32 @@ int64_t count_rows(const char* t, size_t a, size_t b) {
   return r;
 }
 
+// The "C" numeric locale, created once: the reference parses with Python's
+// float(), which ignores LC_NUMERIC ('.' is the only decimal point).
+locale_t c_numeric_locale() {
+  static locale_t loc = newlocale(LC_NUMERIC_MASK, "C", static_cast<locale_t>(0));
+  return loc;
+}
+
 // Parse one field [a, b) as fp64 (the token must be consumed entirely).
+// Python's float() accepts decimal literals, inf/infinity/nan (any case, with
+// a sign); strtod also takes hex floats ("0x1p3") and "nan(chars)", which
+// float() rejects -- such tokens are rejected here too.
 bool parse_double(const char* t, size_t a, size_t b, double& v) {
   char buf[128];
   const size_t n = b - a;
   if (n == 0 || n >= sizeof(buf)) return false;
-  for (size_t i = 0; i < n; ++i) buf[i] = t[a + i];
+  for (size_t i = 0; i < n; ++i) {
+    const char c = t[a + i];
+    if (c == 'x' || c == 'X' || c == '(') return false;
+    buf[i] = c;
+  }
   buf[n] = 0;
+  const locale_t loc = c_numeric_locale();
+  if (!loc) return false;
   char* end = nullptr;
   errno = 0;
-  v = std::strtod(buf, &end);
+  v = strtod_l(buf, &end, loc);
   return end == buf + n;
 }
 

@@ -1,9 +1,9 @@
 // Warm-step plan: one density-weighted AL iteration (dal_dw_step) captured
 // once as a hipGraph over caller-owned static buffers and replayed by
 // dal_dw_plan_run.  The per-step refresh (stamp the unlabeled rows, whose list
-// address and length the host leaves in a host-mapped slot; the score kernel
-// builds the step's row flags from the base flags and the stamps) runs inside
-// the graph; the graph's last kernel writes the
+// address and length are the mark kernel's arguments, rewritten per replay;
+// the score kernel builds the step's row flags from the base flags and the
+// stamps) runs inside the graph; the graph's last kernel writes the
 // selection into the caller's fresh buffer and the status word into
 // host-mapped memory -- the host side of a warm step is ONE call, and the
 // host spins on that word instead of a blocking stream sync.
@@ -25,9 +25,6 @@
 // and the final status word.  No copy launches follow the graph.
 struct PlanSlot {
   int64_t* out[2];     // selected indices (int64 [k]), selected scores (fp64 [k])
-  const int64_t* unl;  // this iteration's unlabeled index list (device) ...
-  int64_t n_unl;       // ... and its length
-  uint32_t step;       // this iteration's stamp (1, 2, ...)
   int32_t status;
 };
 
@@ -36,39 +33,12 @@ namespace {
 constexpr int kPlanThreads = 256;
 constexpr int kMarkBlocks = 512;  // fixed at capture: the list length varies per iteration
 
-// In-graph row marking.  The unlabeled list's (address, length) and the
-// step's stamp are copied from the host-mapped slot into device memory by ONE
-// thread (reads of host memory from many blocks serialise: 512 blocks took
-// 274 us), then stamp[r] = step for every listed row of this pool; the score
-// kernel ORs DAL_ROW_CANDIDATE into the base flags where stamp[r] == step (no
-// per-step copy of the flags).
-__global__ __launch_bounds__(64) void plan_fetch_kernel(const PlanSlot* slot, int64_t* __restrict__ args,
-                                                        uint32_t* __restrict__ step_dev) {
-  if (threadIdx.x != 0) return;
-  args[0] = reinterpret_cast<int64_t>(
-      __hip_atomic_load(const_cast<const int64_t**>(&slot->unl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-  args[1] = __hip_atomic_load(const_cast<int64_t*>(&slot->n_unl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  *step_dev = __hip_atomic_load(const_cast<uint32_t*>(&slot->step), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-__global__ __launch_bounds__(kPlanThreads) void plan_mark_kernel(const int64_t* __restrict__ args,
-                                                                 const uint32_t* __restrict__ step_dev,
-                                                                 int64_t row_base, int64_t n,
-                                                                 uint32_t* __restrict__ stamp) {
-  const int64_t* idx = reinterpret_cast<const int64_t*>(args[0]);
-  const int64_t count = args[1];
-  const uint32_t step = *step_dev;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kPlanThreads;
-  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kPlanThreads + threadIdx.x; t < count; t += stride) {
-    const int64_t r = idx[t] - row_base;
-    if (r >= 0 && r < n) stamp[r] = step;  // duplicates write the same value
-  }
-}
-
-// The same marking with the list's (address, length) and the step id as kernel
-// arguments, rewritten before each replay by hipGraphExecKernelNodeSetParams:
-// no fetch kernel, no host-memory reads in the graph.  Block 0 publishes the
-// step id for the score kernel.
+// In-graph row marking: stamp[r] = step for every listed row of this pool;
+// the score kernel ORs DAL_ROW_CANDIDATE into the base flags where stamp[r] ==
+// step (no per-step copy of the flags).  The list's (address, length) and the
+// step id are kernel arguments, rewritten before each replay by
+// hipGraphExecKernelNodeSetParams: no host-memory reads in the graph.  Block 0
+// publishes the step id for the score kernel.
 __global__ __launch_bounds__(kPlanThreads) void plan_mark_direct_kernel(const int64_t* __restrict__ idx, int64_t count,
                                                                         uint32_t step, int64_t row_base, int64_t n,
                                                                         uint32_t* __restrict__ stamp,
@@ -94,8 +64,8 @@ struct dal_dw_plan {
   PlanSlot* slot = nullptr;       // host view
   PlanSlot* slot_dev = nullptr;   // the same words as the device addresses them
   uint32_t* stamp = nullptr;      // device [n + 1]: per-row mark stamps, then the current step id
-  int64_t* args = nullptr;        // device copy of (slot->unl, slot->n_unl)
-  hipGraphNode_t mark_node = nullptr;  // the direct mark kernel's node (null: fetch-kernel mode)
+  int device = 0;                 // the HIP device of the capture stream (every call runs there)
+  hipGraphNode_t mark_node = nullptr;  // the mark kernel's node (its arguments change every replay)
   hipKernelNodeParams mark_params{};   // its launch shape, reused by every SetParams
   uint32_t step = 0;
   bool timing = false;            // DAL_PLAN_TIMING=1: host time per phase, printed by destroy
@@ -109,6 +79,30 @@ static double now_us() {
 
 using namespace dal;
 
+// Makes the device of ``stream`` current for the guard's lifetime (and
+// restores the caller's): the plan's allocations, capture stream and graph
+// must live on the device whose buffers the captured kernels read, whichever
+// device the calling thread has current.
+class DeviceGuard {
+ public:
+  explicit DeviceGuard(hipStream_t st) {
+    if (hipGetDevice(&prev_) != hipSuccess) return;
+    hipDevice_t dev = prev_;
+    if (st && hipStreamGetDevice(st, &dev) != hipSuccess) return;
+    dev_ = dev;
+    ok_ = dev == prev_ || hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (ok_ && dev_ != prev_) (void)hipSetDevice(prev_);
+  }
+  bool ok() const { return ok_; }
+  int device() const { return dev_; }
+
+ private:
+  int prev_ = 0, dev_ = 0;
+  bool ok_ = false;
+};
+
 extern "C" int dal_dw_plan_create(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
                                   const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
                                   const int64_t* density_fixed, double density_err, const uint8_t* base_flags,
@@ -121,11 +115,14 @@ extern "C" int dal_dw_plan_create(const float* x, int64_t n, int64_t d, int64_t 
   *plan_out = nullptr;
   if (n < 1 || k < 1) return DAL_ERR_SHAPE;
   hipStream_t st = as_stream(stream);
+  const DeviceGuard guard(st);
+  if (!guard.ok()) return DAL_ERR_HIP;
   // the fused step leaves its level-1 header zero after every replay: zero it once
   if (hipMemsetAsync(ws, 0, ws_bytes, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
     return DAL_ERR_HIP;
   dal_dw_plan* p = new (std::nothrow) dal_dw_plan;
   if (!p) return DAL_ERR_HIP;
+  p->device = guard.device();
   hipStream_t cs = nullptr;
   int rc = DAL_OK;
   if (hipHostMalloc(reinterpret_cast<void**>(&p->slot), sizeof(PlanSlot), hipHostMallocMapped) != hipSuccess ||
@@ -133,9 +130,6 @@ extern "C" int dal_dw_plan_create(const float* x, int64_t n, int64_t d, int64_t 
     rc = DAL_ERR_HIP;
   if (!rc) {
     p->slot->out[0] = p->slot->out[1] = nullptr;
-    p->slot->unl = nullptr;
-    p->slot->n_unl = 0;
-    p->slot->step = 0;
     p->slot->status = 0;
   }
   // stamps start at 0 and steps at 1: no row is marked before its first step
@@ -143,25 +137,11 @@ extern "C" int dal_dw_plan_create(const float* x, int64_t n, int64_t d, int64_t 
               hipMemsetAsync(p->stamp, 0, (n + 1) * sizeof(uint32_t), st) != hipSuccess ||
               hipStreamSynchronize(st) != hipSuccess))
     rc = DAL_ERR_HIP;
-  if (!rc && hipMalloc(reinterpret_cast<void**>(&p->args), 2 * sizeof(int64_t)) != hipSuccess) rc = DAL_ERR_HIP;
   if (!rc && hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) rc = DAL_ERR_HIP;
-  // DAL_PLAN_SETPARAMS=0 keeps the fetch-kernel marking; so does a failed
-  // lookup of the direct mark kernel's node.
-  const char* sp = getenv("DAL_PLAN_SETPARAMS");
-  bool direct = !(sp && atoi(sp) == 0);
-  for (int attempt = 0; attempt < 2 && !rc; ++attempt) {
-    if (hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) != hipSuccess) {
-      rc = DAL_ERR_HIP;
-      break;
-    }
-    if (direct) {
-      hipLaunchKernelGGL(plan_mark_direct_kernel, dim3(kMarkBlocks), dim3(kPlanThreads), 0, cs,
-                         static_cast<const int64_t*>(nullptr), int64_t{0}, 0u, idx_base, n, p->stamp, p->stamp + n);
-    } else {
-      hipLaunchKernelGGL(plan_fetch_kernel, dim3(1), dim3(64), 0, cs, p->slot_dev, p->args, p->stamp + n);
-      hipLaunchKernelGGL(plan_mark_kernel, dim3(kMarkBlocks), dim3(kPlanThreads), 0, cs, p->args, p->stamp + n,
-                         idx_base, n, p->stamp);
-    }
+  if (!rc && hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) != hipSuccess) rc = DAL_ERR_HIP;
+  if (!rc) {
+    hipLaunchKernelGGL(plan_mark_direct_kernel, dim3(kMarkBlocks), dim3(kPlanThreads), 0, cs,
+                       static_cast<const int64_t*>(nullptr), int64_t{0}, 0u, idx_base, n, p->stamp, p->stamp + n);
     ForestStepHooks hooks;
     hooks.base_flags = base_flags;
     hooks.stamp = p->stamp;
@@ -173,9 +153,10 @@ extern "C" int dal_dw_plan_create(const float* x, int64_t n, int64_t d, int64_t 
                                      dev_status, nullptr, cs, p->slot_dev->out, &p->slot_dev->status, &hooks);
     const hipError_t end = hipStreamEndCapture(cs, &p->graph);
     rc = step_rc ? step_rc : (end != hipSuccess ? DAL_ERR_HIP : DAL_OK);
-    if (!rc && hipGraphInstantiate(&p->exec, p->graph, nullptr, nullptr, 0) != hipSuccess) rc = DAL_ERR_HIP;
-    if (rc || !direct) break;
-    // find the direct mark kernel's node: its arguments change every replay
+  }
+  if (!rc && hipGraphInstantiate(&p->exec, p->graph, nullptr, nullptr, 0) != hipSuccess) rc = DAL_ERR_HIP;
+  if (!rc) {
+    // find the mark kernel's node: its arguments change every replay
     size_t n_nodes = 0;
     hipGraphNode_t nodes[64];
     if (hipGraphGetNodes(p->graph, nullptr, &n_nodes) == hipSuccess && n_nodes <= 64 &&
@@ -191,13 +172,7 @@ extern "C" int dal_dw_plan_create(const float* x, int64_t n, int64_t d, int64_t 
         }
       }
     }
-    if (p->mark_node) break;
-    // not found: recapture with the fetch kernel
-    (void)hipGraphExecDestroy(p->exec);
-    (void)hipGraphDestroy(p->graph);
-    p->exec = nullptr;
-    p->graph = nullptr;
-    direct = false;
+    if (!p->mark_node) rc = DAL_ERR_HIP;
   }
   if (cs) (void)hipStreamDestroy(cs);
   if (rc) {
@@ -221,10 +196,12 @@ extern "C" int dal_dw_plan_run(dal_dw_plan_t* p, const int64_t* unl, int64_t n_u
                                double* out_scores, int32_t* status_out, dal_stream_t stream) {
   if (!p || !status_out || (!unl && n_unl)) return DAL_ERR_ARG;
   hipStream_t st = as_stream(stream);
+  const DeviceGuard guard(st);
+  if (!guard.ok() || guard.device() != p->device) return DAL_ERR_ARG;  // a stream of another device
   const double t0 = p->timing ? now_us() : 0.0;
   volatile PlanSlot* slot = p->slot;
   const uint32_t step = ++p->step;
-  if (p->mark_node) {
+  {
     hipKernelNodeParams np = p->mark_params;
     int64_t row_base = p->row_base, n = p->n;
     uint32_t* stamp = p->stamp;
@@ -233,10 +210,6 @@ extern "C" int dal_dw_plan_run(dal_dw_plan_t* p, const int64_t* unl, int64_t n_u
     np.kernelParams = kargs;
     np.extra = nullptr;
     if (hipGraphExecKernelNodeSetParams(p->exec, p->mark_node, &np) != hipSuccess) return DAL_ERR_HIP;
-  } else {
-    slot->unl = unl;  // read by the graph's fetch kernel
-    slot->n_unl = n_unl;
-    slot->step = step;
   }
   slot->out[0] = out_idx;
   slot->out[1] = reinterpret_cast<int64_t*>(out_scores);
@@ -270,13 +243,11 @@ extern "C" int dal_dw_plan_run(dal_dw_plan_t* p, const int64_t* unl, int64_t n_u
 extern "C" void dal_dw_plan_destroy(dal_dw_plan_t* p) {
   if (!p) return;
   if (p->timing && p->runs)
-    fprintf(stderr, "dal_dw_plan (%s): %lld runs, host us per run: refresh %.1f, graph launch %.1f, sync %.1f\n",
-            p->mark_node ? "setparams" : "fetch",
+    fprintf(stderr, "dal_dw_plan: %lld runs, host us per run: refresh %.1f, graph launch %.1f, sync %.1f\n",
             static_cast<long long>(p->runs), p->t_refresh / p->runs, p->t_launch / p->runs, p->t_sync / p->runs);
   if (p->exec) (void)hipGraphExecDestroy(p->exec);
   if (p->graph) (void)hipGraphDestroy(p->graph);
   if (p->slot) (void)hipHostFree(p->slot);
   if (p->stamp) (void)hipFree(p->stamp);
-  if (p->args) (void)hipFree(p->args);
   delete p;
 }

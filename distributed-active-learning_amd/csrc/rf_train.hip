@@ -460,6 +460,8 @@ extern "C" int dal_rf_train(const float* x, int64_t n, int64_t d, int64_t ldx, c
   if (max_depth < 1 || max_depth > DAL_RF_MAX_DEPTH) return DAL_ERR_UNSUPPORTED;
   if (num_splits < 0 || num_splits >= DAL_RF_MAX_SPLITS) return DAL_ERR_SHAPE;
   const int hb = num_splits + 2;  // find_splits emits at most num_splits + 1 thresholds
+  // the split kernel keeps one node's whole (slot, bin, class) histogram in LDS
+  if (static_cast<int64_t>(m) * hb * 2 * 4 > DAL_RF_SPLIT_LDS_BYTES) return DAL_ERR_UNSUPPORTED;
   const RfLayout L = rf_layout(n, d, n_trees, max_depth, m, hb);
   if (ws_bytes < L.total || reinterpret_cast<uintptr_t>(ws) % 256) return DAL_ERR_SHAPE;
   hipStream_t st = as_stream(stream);

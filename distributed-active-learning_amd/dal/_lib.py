@@ -39,6 +39,7 @@ DAL_STEP_WS_CLEAN = 2
 DAL_RF_MAX_SPLITS = 255
 DAL_RF_MAX_SPLIT_SAMPLE = 16384
 DAL_RF_MAX_DEPTH = 10
+DAL_RF_SPLIT_LDS_BYTES = 163840
 
 # name -> (restype, argtypes); every symbol of include/dal.h
 SIGNATURES = {

@@ -43,10 +43,14 @@ def select(pool, unlabeled_idx, forest: Forest, k: int, beta: float = 1.0, exclu
 
     excluded_idx  rows dropped from the density as i and as j.  Default "L0":
                   the reference's initial labeled window range(window_size)
-                  (density_weighting.py:89,95-100; window_size defaults to k,
-                  as the script's take(window_size) at :172); for a PoolState
-                  the default keeps the state's own excluded set.  None or []
-                  excludes nothing.
+                  (density_weighting.py:89,95-100); for a PoolState the default
+                  keeps the state's own excluded set.  None or [] excludes
+                  nothing.
+    window_size   the reference's window (L0 = range(window_size)).  Omitted,
+                  it is k -- the script takes window_size rows per iteration
+                  (:172) -- unless k may be a batch clamped to a short
+                  unlabeled set (k >= |unlabeled|), where L0 is ambiguous and
+                  window_size must be given.
     density       optional int64 fixed-point density from a previous call
                   (PoolState.density_fixed()); by default the pool's cached one
     mode          "gram" (default, the reference's algorithm on MFMA) or
@@ -55,7 +59,16 @@ def select(pool, unlabeled_idx, forest: Forest, k: int, beta: float = 1.0, exclu
     if isinstance(excluded_idx, str):
         if excluded_idx != L0:
             raise ValueError(f"excluded_idx must be index-like, None or {L0!r}")
-        excluded_idx = None if isinstance(pool, PoolState) else range(int(window_size or k))
+        if isinstance(pool, PoolState):
+            excluded_idx = None
+        else:
+            if window_size is None:
+                n_unl = len(unlabeled_idx) if hasattr(unlabeled_idx, "__len__") else None
+                if n_unl is not None and int(k) >= n_unl:
+                    raise ValueError("k >= the unlabeled count: k may be a clamped batch, so L0 = "
+                                     "range(window_size) is ambiguous -- pass window_size (or excluded_idx)")
+                window_size = k
+            excluded_idx = range(int(window_size))
     elif excluded_idx is None and isinstance(pool, PoolState):
         excluded_idx = []
     state = as_pool_state(pool, excluded=excluded_idx, device=device)

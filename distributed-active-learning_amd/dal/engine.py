@@ -647,12 +647,18 @@ def dw_step_local(state: PoolState, forest: Forest, flags, dens, lut_dev, k: int
         out_idx = torch.empty(k, dtype=torch.int64, device=dev)
         out_scores = torch.empty(k, dtype=torch.float64, device=dev)
         out_keys = None if sync else torch.empty(k, dtype=torch.int64, device=dev)
-        call("dal_dw_step", _ptr(state.x), n, state.d, state.d, _ptr(inner), _ptr(leaf), forest.n_trees,
-             forest.depth, _ptr(lut_dev), _ptr(dens), derr, _ptr(flags), float(beta), state.row_base,
-             _ptr(norm64), _ptr(colsum), k, cap, passes, DAL_STEP_WS_CLEAN, wsp, wsb, _ptr(votes), _ptr(scores),
-             _ptr(keys_lo), _ptr(keys_hi), _ptr(out_idx), _ptr(out_scores),
-             0 if out_keys is None else _ptr(out_keys), _ptr(state.status),
-             0 if colsum_ready is None else colsum_ready.cuda_event, _stream(dev))
+        try:
+            call("dal_dw_step", _ptr(state.x), n, state.d, state.d, _ptr(inner), _ptr(leaf), forest.n_trees,
+                 forest.depth, _ptr(lut_dev), _ptr(dens), derr, _ptr(flags), float(beta), state.row_base,
+                 _ptr(norm64), _ptr(colsum), k, cap, passes, DAL_STEP_WS_CLEAN, wsp, wsb, _ptr(votes),
+                 _ptr(scores), _ptr(keys_lo), _ptr(keys_hi), _ptr(out_idx), _ptr(out_scores),
+                 0 if out_keys is None else _ptr(out_keys), _ptr(state.status),
+                 0 if colsum_ready is None else colsum_ready.cuda_event, _stream(dev))
+        except _lib.DalError:
+            # a call that failed after queueing part of the step may leave the
+            # level-1 header dirty: never reuse this workspace as "clean"
+            state._ws_clean.pop(key, None)
+            raise
         if not sync:
             return votes, scores, out_idx, out_scores, out_keys
         st = int(state.status.item())  # the step's one host sync
@@ -851,7 +857,12 @@ def _density_step_graph(state: PoolState, unl, forest: Forest, kk: int, beta: fl
         g = state._graphs.get(key)
         if g is None:
             g = state._graphs[key] = WarmStepGraph(state, forest, kk, beta, cap, passes)
-        votes, scores, idx, sel_scores, st = g.run(forest, unl)
+        try:
+            votes, scores, idx, sel_scores, st = g.run(forest, unl)
+        except _lib.DalError:
+            # a failed replay may leave the plan's workspace header dirty: rebuild next time
+            state._graphs.pop(key, None)
+            raise
         state.last_status = st
         if st & DAL_FLAG_SAMPLE_MISS:
             state.status.bitwise_and_(~(DAL_FLAG_SAMPLE_MISS | DAL_FLAG_CAND_OVERFLOW))

@@ -24,7 +24,8 @@ import math
 import numpy as np
 
 from . import _lib
-from ._lib import DAL_FLAG_RF_SPLITS, DAL_RF_MAX_DEPTH, DAL_RF_MAX_SPLIT_SAMPLE, DAL_RF_MAX_SPLITS, call
+from ._lib import (DAL_FLAG_RF_SPLITS, DAL_RF_MAX_DEPTH, DAL_RF_MAX_SPLIT_SAMPLE, DAL_RF_MAX_SPLITS,
+                   DAL_RF_SPLIT_LDS_BYTES, call)
 from .forest import Forest
 
 
@@ -89,6 +90,18 @@ def _stream(device):
     return torch.cuda.current_stream(device).cuda_stream
 
 
+def check_split_histogram(m: int, n_splits: int) -> None:
+    """dal_rf_train's split kernel holds one node's (feature slot, bin, class)
+    histogram in LDS: m * (n_splits + 2) * 2 int32 counts must fit
+    DAL_RF_SPLIT_LDS_BYTES.  MLlib itself has no such limit; raise a clear
+    error instead of the kernel's DAL_ERR_UNSUPPORTED."""
+    need = int(m) * (int(n_splits) + 2) * 8
+    if need > DAL_RF_SPLIT_LDS_BYTES:
+        raise ValueError(f"{m} candidate features per node x {n_splits + 1} thresholds need {need} bytes of "
+                         f"split histogram, more than the GPU trainer's {DAL_RF_SPLIT_LDS_BYTES} "
+                         "(lower max_bins or use a smaller feature subset)")
+
+
 def train_classifier(X, y, num_trees: int = 10, max_depth: int = 4, max_bins: int = 32, seed: int = 0,
                      feature_subset_strategy: str = "auto", weights=None, feature_subsets=None,
                      min_instances_per_node: int = 1, min_info_gain: float = 0.0, device=None) -> Forest:
@@ -131,6 +144,7 @@ def train_classifier(X, y, num_trees: int = 10, max_depth: int = 4, max_bins: in
     if not 1 <= m <= d:
         raise ValueError("feature subsets must hold 1..d features")
     ns = num_splits(n, max_bins)
+    check_split_histogram(m, ns)
     rows = split_sample_rows(n, max_bins, seed)
     n_sample = n if rows is None else int(rows.shape[0])
     rows_t = None if rows is None else torch.from_numpy(rows).to(dev)

@@ -79,6 +79,7 @@ enum dal_status {
 #define DAL_RF_MAX_SPLITS 255          /* thresholds per feature (bins fit a uint8) */
 #define DAL_RF_MAX_SPLIT_SAMPLE 16384  /* rows one threshold search sorts in LDS */
 #define DAL_RF_MAX_DEPTH 10            /* deepest tree dal_rf_train grows */
+#define DAL_RF_SPLIT_LDS_BYTES 163840  /* m * (num_splits + 2) * 8 must fit (one node's histogram, LDS) */
 
 const char* dal_status_string(int status);
 int dal_abi_version(void);

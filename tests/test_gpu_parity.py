@@ -440,6 +440,25 @@ def test_dw_nan_scores_rank_last(cuda):
     assert np.array_equal(_np(sel.selected_scores), ref_ss, equal_nan=True)
 
 
+def test_dw_l0_default_uses_window_size(cuda):
+    """the L0 default is range(window_size), also when the batch k
+    is smaller (the loop's last iterations): density_weighting.py:89,95-100."""
+    from dal import density_weighting as dw
+    from dal.forest import Forest
+
+    X = O.synthetic_pool(3000, 16, seed=5)
+    F = Forest.synthetic(10, 4, 16, seed=1)
+    of = O.synthetic_forest(10, 4, 16, seed=1)
+    unl = np.arange(10, 3000)
+    sel = dw.select(X, unl, F, 5, window_size=10)
+    _, ref_idx, ref_ss = O.density_select(X, unl, of, 5, 1.0, np.arange(10))
+    assert np.array_equal(_np(sel.indices), ref_idx)
+    assert np.array_equal(_np(sel.selected_scores), ref_ss)
+    sel5 = dw.select(X, unl, F, 5)  # no window_size, k < |U|: L0 = range(k)
+    _, ref5, _ = O.density_select(X, unl, of, 5, 1.0, np.arange(5))
+    assert np.array_equal(_np(sel5.indices), ref5)
+
+
 def _oracle_from(F):
     """Heap-layout Forest -> oracle node arrays (test helper)."""
     feat, thr, left, right, val, roots = [], [], [], [], [], []

@@ -79,6 +79,54 @@ def test_parse_double_rounding_matches_fp64_then_fp32(tmp_path):
     assert got_y.tolist() == [1] * len(vals)
 
 
+def test_parse_rejects_tokens_python_float_rejects(tmp_path):
+    """Hex floats and nan(chars) parse with strtod but raise in the
+    reference's float(); inf/nan spellings float() takes are accepted."""
+    from dal import _lib
+    from dal.ingest import parse_labeled_text
+
+    p = tmp_path / "hex.txt"
+    for tok in ("0x1p3", "-0X10", "nan(123)"):
+        with pytest.raises(ValueError):
+            float(tok)
+        p.write_text(f"1 {tok} 1\n")
+        with pytest.raises(_lib.DalError):
+            parse_labeled_text(str(p))
+    p.write_text("inf -Infinity 1\nNaN +1.5 -1\n")
+    got_x, got_y = parse_labeled_text(str(p))
+    ref_x, ref_y = _ref_parse(str(p))
+    assert np.array_equal(got_x.view(np.int32), ref_x.view(np.int32))
+    assert np.array_equal(got_y, ref_y)
+
+
+def test_parse_ignores_process_numeric_locale(tmp_path):
+    """Python float() ignores LC_NUMERIC; so does the native parser (a
+    comma-decimal locale must not break '0.5')."""
+    import locale
+
+    from dal.ingest import parse_labeled_text
+
+    p = tmp_path / "loc.txt"
+    p.write_text("0.5 1.25 1\n")
+    old = locale.setlocale(locale.LC_NUMERIC)
+    switched = False
+    for name in ("de_DE.UTF-8", "de_DE.utf8", "fr_FR.UTF-8", "fr_FR.utf8"):
+        try:
+            locale.setlocale(locale.LC_NUMERIC, name)
+            switched = True
+            break
+        except locale.Error:
+            continue
+    if not switched:
+        pytest.skip("no comma-decimal locale installed in this image (locale -a: C, C.utf8, POSIX)")
+    try:
+        assert locale.localeconv()["decimal_point"] == ","
+        got_x, _ = parse_labeled_text(str(p))
+    finally:
+        locale.setlocale(locale.LC_NUMERIC, old)
+    assert got_x.tolist() == [[0.5, 1.25]]
+
+
 def test_parse_rejects_ragged_and_bad_fields(tmp_path):
     from dal import _lib
     from dal.ingest import parse_labeled_text

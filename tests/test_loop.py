@@ -40,3 +40,13 @@ def test_loop_runs_to_exhaustion_with_reference_log(strategy):
     chosen = np.concatenate(res.labeled_history)
     assert sorted(chosen.tolist()) == list(range(10, 120))  # every row labeled once
     assert len(res.accuracy) == 11
+
+
+def test_dw_l0_default_ambiguous_batch_raises_before_gpu():
+    """k >= |unlabeled| may be a clamped batch: L0 = range(window_size) cannot
+    be inferred from k, so select() asks for window_size (no GPU touched)."""
+    from dal import density_weighting as dw
+
+    X = np.random.default_rng(0).random((40, 4))
+    with pytest.raises(ValueError, match="window_size"):
+        dw.select(X, np.arange(35, 40), None, 5)

@@ -75,6 +75,27 @@ def test_bagging_inputs_shapes_and_determinism():
     assert feature_subset_size(784, 10) == 28 and feature_subset_size(30, 1) == 30
 
 
+def test_split_histogram_limit_rejected_before_launch():
+    """MLlib-valid inputs whose node histogram does not fit the
+    split kernel's LDS are rejected with a clear error (Python) and with
+    DAL_ERR_UNSUPPORTED before any HIP call (C ABI)."""
+    import ctypes
+
+    from dal import _lib
+    from dal.random_forest import check_split_histogram
+
+    check_split_histogram(600, 31)          # 600 x 33 x 8 = 158,400 B: fits
+    check_split_histogram(80, 200)          # 80 x 202 x 8 = 129,280 B
+    for m, ns in ((700, 31), (784, 31), (100, 254)):
+        with pytest.raises(ValueError, match="split histogram"):
+            check_split_histogram(m, ns)
+    lib = _lib.load()
+    p = ctypes.c_void_p(256)
+    # numTrees=1 'auto' -> all 784 features at maxBins 32
+    rc = lib.dal_rf_train(p, 1000, 784, 784, p, p, p, 31, p, p, 784, 1, 4, 1, 0.0, p, p, p, 1 << 30, None)
+    assert rc == -3  # DAL_ERR_UNSUPPORTED
+
+
 # ------------------------------------------------------------------- GPU --
 def _oracle_heap(sf, st, lc):
     inner = np.zeros(sf.shape + (2,), dtype=np.int32)
