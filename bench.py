@@ -58,6 +58,30 @@ CONFIGS = {
               n=8_000_000, d=128, k=1000, m=1024, dist="uniform", mode="div"),
 }
 N_EXCLUDED = 10
+# default extras beside the config-4 headline: configs 2, 3, 5
+# and config 4 at T = 100 and at k = 1000
+DEFAULT_EXTRA = "2,3,5,4:T100,4:k1000"
+
+
+def resolve(spec: str):
+    """'4', '4:T100', '4:k1000', '4:T100:k1000' -> (config key, cfg dict, label)."""
+    parts = spec.split(":")
+    c = parts[0]
+    cfg = dict(CONFIGS[c])
+    note = []
+    for p in parts[1:]:
+        if p[:1] == "T" and "trees" in cfg:
+            cfg["trees"] = int(p[1:])
+            note.append(f"T={cfg['trees']}")
+        elif p[:1] == "k":
+            cfg["k"] = int(p[1:])
+            note.append(f"k={cfg['k']}")
+        else:
+            raise SystemExit(f"bad config spec {spec!r}")
+    if note:
+        cfg["workload"] += f" [override: {', '.join(note)}]"
+    label = f"config{c}" + "".join(f"_{p}" for p in parts[1:])
+    return c, cfg, label
 POOL_SEED = 0
 DATA_NOTE = ("synthetic: numpy default_rng(0) pool of the BASELINE.md shape (rows of a shard generated "
              "by PCG64 advance, identical for every GPU count); forest synthetic (default_rng(1))")
@@ -190,33 +214,32 @@ def cpu_baseline_div(x_host_bf16_as_f32: np.ndarray, m: int, k: int, n_total: in
 
 
 # ------------------------------------------------------------ rooflines --
-def gram_roofline(gram, achieved, traffic, gram_ms, gram_ms_max, flops):
+def gram_roofline(gram, achieved, traffic, gram_ms, gram_ms_max, flops, products=3):
     """Roofline entry of the density GEMM.  achieved = ALGORITHMIC flops
-    (2 per feature per (row, column) pair) / launch time.  The split kernel
-    issues three fp16 MFMA products per algorithmic product, so its ceiling is
-    the dense fp16 peak / 3; the native fp32-MFMA peak is reported beside."""
+    (2 per feature per (row, column) pair, every pair of the N x N Gram) /
+    launch time; frac = achieved / the dense fp16 MFMA peak (2.5 PF) the
+    kernel issues on.  The symmetric kernel multiplies each block pair once
+    (S_ij and S_ji from one product) with ``products`` fp16 MFMA products per
+    feature pair, so it executes products / 2 fp16 flops per algorithmic
+    flop: ``mfma_util_executed`` is that executed rate over the same peak."""
     if gram == "f32":
         return {"bound": "mfma", "kernel": "dal_gram_rowsum (v_mfma_f32_32x32x2_f32)",
                 "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic, "launch_ms": gram_ms,
                 "launch_ms_max_over_ranks": gram_ms_max, "algorithmic_flops_per_launch": flops}
-    if gram == "sym":
-        peak = 2.0 * F16_MFMA_PEAK_TFLOPS / 3.0
-        return {"bound": "mfma",
-                "kernel": "dal_gram_rowsum_sym (symmetric block pairs once; 3 x v_mfma_f32_16x16x32_f16 "
-                          "per 32 features: h.h, h.l, l.h)",
-                "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
-                "peak_note": "dense fp16 MFMA peak 2500 TF/s / 3 products per algorithmic product, x2: "
-                             "each block-pair product serves S_ij and S_ji (row and column sums)",
-                "executed_fp16_tflops": 1.5 * achieved, "vs_fp32_mfma_peak": achieved / FP32_MFMA_PEAK_TFLOPS,
-                "traffic": traffic, "launch_ms": gram_ms, "launch_ms_max_over_ranks": gram_ms_max,
-                "algorithmic_flops_per_launch": flops}
-    peak = F16_MFMA_PEAK_TFLOPS / 3.0
+    sym = gram == "sym"
+    executed = achieved * products / (2.0 if sym else 1.0)
+    names = {3: "h.h, h.l, l.h", 2: "h.h, h.l + exact residual <l_i, block sums>"}
     return {"bound": "mfma",
-            "kernel": "dal_gram_rowsum_split (3 x v_mfma_f32_16x16x32_f16 per 32 features: h.h, h.l, l.h)",
-            "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
-            "peak_note": "dense fp16 MFMA peak 2500 TF/s / 3 products per algorithmic product",
-            "executed_fp16_tflops": 3.0 * achieved, "vs_fp32_mfma_peak": achieved / FP32_MFMA_PEAK_TFLOPS,
+            "kernel": (f"dal_gram_rowsum_{'sym' if sym else 'split'} ({'symmetric block pairs once; ' if sym else ''}"
+                       f"{products} x v_mfma_f32_16x16x32_f16 per 32 features: {names.get(products, '')})"),
+            "achieved": achieved, "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved / F16_MFMA_PEAK_TFLOPS,
+            "peak_note": "dense fp16 MFMA peak (MI355X_MICROARCH.md); achieved counts the algorithmic "
+                         "2*N_rows*(N-|E|)*D flops of the full Gram",
+            "executed_fp16_tflops": executed, "mfma_util_executed": executed / F16_MFMA_PEAK_TFLOPS,
+            "fp16_products_per_feature_pair": products, "symmetric_pairs": sym,
+            "vs_fp32_mfma_peak": achieved / FP32_MFMA_PEAK_TFLOPS,
             "traffic": traffic, "launch_ms": gram_ms, "launch_ms_max_over_ranks": gram_ms_max,
             "algorithmic_flops_per_launch": flops}
 
@@ -365,18 +388,31 @@ def abs_rowsum_tolerance(x_host, pick, gram_density, n_excluded, m=256, chunk=32
     return float((err / a_ref).max())
 
 
-def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, backend, cpu=True):
+_POOLS = {}
+
+
+def cached_pool(n, d, dist, lo, hi, dev):
+    """(host rows [lo, hi), device copy) of a BASELINE pool, generated once per
+    process (the config-4 variants share the 2M x 256 pool)."""
+    key = (n, d, dist, lo, hi)
+    if key not in _POOLS:
+        _POOLS.clear()  # keep one pool resident
+        x_host = host_pool(lo, hi, d, dist)
+        _POOLS[key] = (x_host, upload(x_host, dev))
+    return _POOLS[key]
+
+
+def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, backend, cpu=True, cfg=None):
     """Density-weighted selection on one config; returns the JSON dict."""
     import torch
 
     from dal import engine, parallel
     from dal.forest import Forest
 
-    cfg = CONFIGS[config]
+    cfg = CONFIGS[config] if cfg is None else cfg
     n, d, k = cfg["n"], cfg["d"], cfg["k"]
     lo, hi, _ = parallel.shard_range(n, world, rank)
-    x_host = host_pool(lo, hi, d, cfg["dist"])  # this rank's rows (world 1: the whole pool)
-    x = upload(x_host, dev)
+    x_host, x = cached_pool(n, d, cfg["dist"], lo, hi, dev)  # this rank's rows (world 1: the whole pool)
     forest = Forest.synthetic(cfg["trees"], cfg["depth"], d, seed=1, dist=cfg["dist"])
     excluded = np.arange(N_EXCLUDED)
     unl = torch.arange(N_EXCLUDED, n, device=dev, dtype=torch.int64)
@@ -540,7 +576,8 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
                        "note": "density via the exact O(N*D) identity sum_j<u_i,u_j> = <u_i, sum_j u_j> "
                                "(canonical fp64, same selection); HBM-bound, not the MFMA path"}
                       if sep_ms else None),
-        "roofline": gram_roofline(state.gram, achieved, traffic, gram_ms, gram_ms_max, flops),
+        "roofline": gram_roofline(state.gram, achieved, traffic, gram_ms, gram_ms_max, flops,
+                                  engine.gram_products(state)),
         "roofline_forest": forest_roofline(state.n, d, cfg["trees"], forest_ms, config, world),
         "roofline_topk": topk_roofline(state.n, select_ms, config, world,
                                        engine.LEVEL1_PASSES if state.level1_fast else 0),
@@ -550,7 +587,7 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
         from oracle import dal_oracle as O
 
         of = O.synthetic_forest(cfg["trees"], cfg["depth"], d, seed=1, dist=cfg["dist"])
-        out["cpu_baseline"] = cpu_baseline(x_host, cfg, of)
+        out["cpu_baseline"] = cpu_baseline(x_host, cfg, of, budget_s=cpu if isinstance(cpu, float) else 12.0)
     del state, x
     if world > 1:
         del sel
@@ -558,7 +595,51 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
     return out
 
 
-def bench_div(args, steps, warmup, world, rank, dev, dist, backend):
+def canon_unit(x64: np.ndarray) -> np.ndarray:
+    """u = x / ||x|| with ||x||^2 summed sequentially over features (mul, then
+    add), as the library's canonical fp64 re-rank (numpy; no library code)."""
+    n2 = np.zeros(x64.shape[0])
+    for f in range(x64.shape[1]):
+        n2 = n2 + x64[:, f] * x64[:, f]
+    return x64 / np.sqrt(n2)[:, None]
+
+
+def canon_maxcos(rows64: np.ndarray, lab64: np.ndarray) -> np.ndarray:
+    """Canonical fp64 max-cosine of rows to the labeled rows: cos summed
+    sequentially over features, max over the labeled set."""
+    u, ul = canon_unit(rows64), canon_unit(lab64)
+    S = np.zeros((u.shape[0], ul.shape[0]))
+    for f in range(u.shape[1]):
+        S = S + u[:, f, None] * ul[None, :, f]
+    return S.max(axis=1)
+
+
+def div_self_check(x_dev, lab_host64, lo, m, idx, sc, k, n_sample=4096):
+    """Config-5 selection checked on the host (outside the timed region): the
+    selected scores are the canonical fp64 max-cos of the selected rows, bit
+    for bit; no sampled candidate row outside the selection beats the k-th
+    selected score (ties by index)."""
+    import torch
+
+    idx_h = idx.cpu().numpy()
+    sc_h = sc.cpu().numpy()
+    rows = x_dev[torch.from_numpy(idx_h - lo).to(x_dev.device)].float().cpu().numpy().astype(np.float64)
+    exact = bool(np.array_equal(canon_maxcos(rows, lab_host64).view(np.int64), sc_h.view(np.int64)))
+    sorted_ok = bool(np.all((sc_h[1:] > sc_h[:-1]) | ((sc_h[1:] == sc_h[:-1]) & (idx_h[1:] > idx_h[:-1]))))
+    n_loc = int(x_dev.shape[0])
+    first = max(0, m - lo)
+    pick = np.unique(np.linspace(first, n_loc - 1, min(n_sample, n_loc - first)).round().astype(np.int64))
+    pick = pick[~np.isin(pick + lo, idx_h)]
+    ms = canon_maxcos(x_dev[torch.from_numpy(pick).to(x_dev.device)].float().cpu().numpy().astype(np.float64),
+                      lab_host64)
+    kth, kth_i = sc_h[-1], idx_h[-1]
+    no_better = bool(np.all((ms > kth) | ((ms == kth) & (pick + lo > kth_i))))
+    return {"selected_scores_equal_canonical_fp64": exact, "selection_sorted": sorted_ok,
+            "no_sampled_row_beats_kth": no_better, "sampled_rows": int(pick.size), "k": int(k),
+            "note": "host numpy fp64 restatement (sequential norms and dots) on the bf16 values"}
+
+
+def bench_div(args, steps, warmup, world, rank, dev, dist, backend, cpu=12.0):
     """Config 5: one step = max-cosine of every pool row to the labeled set
     (bf16 MFMA, fp32 accumulate) + exact top-k of the least similar rows."""
     import torch
@@ -589,7 +670,12 @@ def bench_div(args, steps, warmup, world, rank, dev, dist, backend):
 
     for _ in range(warmup):
         step()
-    elapsed, _ = _timed(step, steps, barrier)
+    elapsed, (sel_idx, sel_sc) = _timed(step, steps, barrier)
+    check = div_self_check(x, upload(lab_host, dev).to(torch.bfloat16).float().cpu().numpy().astype(np.float64),
+                           lo, m, sel_idx, sel_sc, k) if world == 1 else None
+    if check is not None and not (check["selected_scores_equal_canonical_fp64"] and check["selection_sorted"]
+                                  and check["no_sampled_row_beats_kth"]):
+        raise SystemExit(f"bench self-check FAILED (config 5): {check}")
     # kernel-only timing of the max-cosine launch on this rank
     L = LabeledSet(lab, dev)
     st = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -620,11 +706,12 @@ def bench_div(args, steps, warmup, world, rank, dev, dist, backend):
                      "traffic": _traffic("5", "maxcos_bytes_per_launch", world), "launch_ms": kms,
                      "algorithmic_flops_per_launch": flops, "pool_bytes_per_launch": (hi - lo) * d * 2,
                      "hbm_frac_of_8TBs": (hi - lo) * d * 2 / (kms * 1e-3) / 8e12},
+        "self_check": check,
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and cpu and not args.no_cpu_baseline:
         xs = x[: 300_000].float().cpu().numpy()  # the bf16 values the GPU scores, as fp32
-        res["cpu_baseline"] = cpu_baseline_div(xs, m, k, n)
+        res["cpu_baseline"] = cpu_baseline_div(xs, m, k, n, budget_s=float(cpu))
     return res
 
 
@@ -675,22 +762,14 @@ def main():
     ap.add_argument("--trees", type=int, default=None, help="override the config's forest size (config 4: T=100)")
     ap.add_argument("--k", type=int, default=None, help="override the config's selection size (config 4: k=1000)")
     args = ap.parse_args()
-    if args.trees is not None or args.k is not None:  # config 4 also at T=100 and k=1000
-        cfg = dict(CONFIGS[args.config])
-        note = []
-        if args.trees is not None and "trees" in cfg:
-            cfg["trees"] = args.trees
-            note.append(f"T={args.trees}")
-        if args.k is not None:
-            cfg["k"] = args.k
-            note.append(f"k={args.k}")
-        cfg["workload"] += f" [override: {', '.join(note)}]"
-        CONFIGS[args.config] = cfg
+    main_cfg = resolve(f"{args.config}" + (f":T{args.trees}" if args.trees is not None else "")
+                       + (f":k{args.k}" if args.k is not None else ""))[1]
     big = args.config in ("4",)
     steps = args.steps if args.steps is not None else (5 if big else 50)
     warmup = args.warmup if args.warmup is not None else (1 if big else 10)
     warm_steps = args.warm_steps if args.warm_steps is not None else (5 if big else 20)
-    extra = args.extra if args.extra is not None else ("2" if args.config == "4" else "")
+    extra = args.extra if args.extra is not None else (DEFAULT_EXTRA if args.config == "4" and
+                                                        args.trees is None and args.k is None else "")
     extra = [c for c in extra.split(",") if c and c != "none"]
 
     import torch
@@ -713,20 +792,30 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    if CONFIGS[args.config].get("mode") == "div":
+    if main_cfg.get("mode") == "div":
         out = bench_div(args, steps, warmup, world, rank, dev, dist, backend)
     else:
-        out = bench_dw(args, args.config, steps, warmup, warm_steps, world, rank, dev, dist, backend)
+        out = bench_dw(args, args.config, steps, warmup, warm_steps, world, rank, dev, dist, backend, cfg=main_cfg)
     if extra:
         out["extra"] = {}
-        for c in extra:
-            if CONFIGS[c].get("mode") == "div":
-                r = bench_div(args, 20, 5, world, rank, dev, dist, backend)
+        for spec in extra:
+            c, cfg, label = resolve(spec)
+            t0 = time.perf_counter()
+            variant = ":" in spec  # config-4 T=100 / k=1000: the same 2M x 256 pool, fewer steps
+            if cfg.get("mode") == "div":
+                r = bench_div(args, 20, 5, world, rank, dev, dist, backend, cpu=8.0)
+            elif variant:
+                r = bench_dw(args, c, 3, 1, 5, world, rank, dev, dist, backend, cpu=False, cfg=cfg)
             else:
-                r = bench_dw(args, c, 20, 5, 20, world, rank, dev, dist, backend, cpu=False)
-            out["extra"][f"config{c}"] = {kk: r[kk] for kk in (
-                "value", "unit", "steps", "ms_per_step", "config", "warm_selection_latency_ms", "self_check",
-                "roofline", "roofline_forest", "roofline_topk") if kk in r}
+                r = bench_dw(args, c, 20, 5, 20, world, rank, dev, dist, backend, cpu=8.0, cfg=cfg)
+            out["extra"][label] = {kk: r[kk] for kk in (
+                "metric", "value", "unit", "steps", "warmup", "ms_per_step", "dtype", "config",
+                "warm_selection_latency_ms", "self_check", "accuracy", "roofline", "roofline_forest",
+                "roofline_topk", "cpu_baseline") if kk in r}
+            out["extra"][label]["wall_s"] = time.perf_counter() - t0
+            if variant:
+                out["extra"][label]["cpu_baseline_note"] = ("the host cost of this variant is the headline "
+                                                            "line's O(N^2) Gram row-sum (cpu_baseline above)")
     if world == 1 and CONFIGS[args.config].get("mode") != "div":
         out.setdefault("extra", {})["rf_train"] = bench_rf_train(dev)
     if rank == 0:

@@ -437,6 +437,12 @@ def _gram_kind(gram) -> str:
     return g
 
 
+def gram_products(state: PoolState) -> int:
+    """fp16 MFMA products per feature pair of the pool's Gram kernel (bench
+    roofline: executed vs algorithmic flops)."""
+    return 3 if state.gram in ("sym", "split") else 1
+
+
 def _as_index(idx, device):
     torch = _torch()
     if isinstance(idx, torch.Tensor):

@@ -86,3 +86,34 @@ def test_cpu_baseline_small_pool():
     r = bench.cpu_baseline(x, cfg, of, budget_s=0.3)
     assert r["value"] > 0 and r["kind"] == "port" and r["cores"] >= 1
     assert r["separable"]["value"] > 0 and "separable" not in r["sample"]
+
+
+def test_config_specs_and_default_extras():
+    """The default config-4 run also measures configs 2, 3, 5 and config 4 at
+    T = 100 and k = 1000."""
+    assert bench.DEFAULT_EXTRA.split(",") == ["2", "3", "5", "4:T100", "4:k1000"]
+    c, cfg, label = bench.resolve("4:T100")
+    assert c == "4" and cfg["trees"] == 100 and cfg["k"] == 100 and label == "config4_T100"
+    c, cfg, label = bench.resolve("4:k1000")
+    assert cfg["trees"] == 10 and cfg["k"] == 1000 and label == "config4_k1000"
+    assert bench.CONFIGS["4"]["trees"] == 10 and bench.CONFIGS["4"]["k"] == 100  # not mutated
+    assert bench.resolve("3")[2] == "config3" and bench.resolve("5")[1]["mode"] == "div"
+
+
+def test_gram_roofline_frac_is_algorithmic():
+    """roofline.frac = algorithmic flops / time / the 2.5 PF dense fp16 peak;
+    the executed MFMA rate (3 products, symmetric pairs once) is separate."""
+    r = bench.gram_roofline("sym", 1125.0, None, 1819.0, 1819.0, 2.048e15, products=3)
+    assert r["peak"] == 2500.0 and abs(r["frac"] - 0.45) < 1e-12
+    assert abs(r["mfma_util_executed"] - 0.675) < 1e-12
+    r2 = bench.gram_roofline("sym", 1600.0, None, 1.0, 1.0, 1.0, products=2)
+    assert abs(r2["mfma_util_executed"] - r2["frac"]) < 1e-12
+
+
+def test_div_self_check_canonical_numpy():
+    """bench's config-5 host check: numpy canonical max-cos equals the oracle's."""
+    rng = np.random.default_rng(3)
+    X = rng.random((300, 16))
+    got = bench.canon_maxcos(X[50:], X[:20])
+    ref, _ = O.max_cosine_canonical(X, np.arange(20))
+    assert np.array_equal(got, ref[50:])

@@ -123,14 +123,13 @@ def test_from_mllib_debug_string_rejects_categorical():
         Forest.from_mllib_debug_string(txt)
 
 
-def test_from_mllib_saved_parquet(tmp_path):
-    """MLlib RandomForestModel.save layout: NodeData rows in Parquet, node ids
-    1 (root), 2i, 2i+1 as MLlib assigns them."""
+def write_mllib_saved(of, path):
+    """Render oracle node arrays in MLlib RandomForestModel.save's layout
+    (NodeData rows in two Parquet part files under path/data; node ids 1
+    (root), 2i, 2i+1 as MLlib assigns them) -- test helper."""
     import pyarrow as pa
     import pyarrow.parquet as pq
 
-    g = load_golden("synthetic_512x64_T10.npz")
-    of = golden_forest(g)
     rows = []
     for t, root in enumerate(of.roots):
         def rec(nd, nid):
@@ -149,9 +148,19 @@ def test_from_mllib_saved_parquet(tmp_path):
                 rec(int(of.left[nd]), 2 * nid)
                 rec(int(of.right[nd]), 2 * nid + 1)
         rec(int(root), 1)
-    (tmp_path / "data").mkdir()
+    import os
+
+    os.makedirs(os.path.join(path, "data"), exist_ok=True)
     half = len(rows) // 2
-    pq.write_table(pa.Table.from_pylist(rows[:half]), tmp_path / "data" / "part-0.parquet")
-    pq.write_table(pa.Table.from_pylist(rows[half:]), tmp_path / "data" / "part-1.parquet")
+    pq.write_table(pa.Table.from_pylist(rows[:half]), os.path.join(path, "data", "part-0.parquet"))
+    pq.write_table(pa.Table.from_pylist(rows[half:]), os.path.join(path, "data", "part-1.parquet"))
+
+
+def test_from_mllib_saved_parquet(tmp_path):
+    """MLlib RandomForestModel.save layout: NodeData rows in Parquet, node ids
+    1 (root), 2i, 2i+1 as MLlib assigns them."""
+    g = load_golden("synthetic_512x64_T10.npz")
+    of = golden_forest(g)
+    write_mllib_saved(of, str(tmp_path))
     F = Forest.from_mllib_saved(str(tmp_path))
     assert np.array_equal(heap_votes(F, g["X"]), O.votes(of, g["X"]))

@@ -137,3 +137,51 @@ def test_config3_full_size_selection_bit_exact(cuda, config3, forced_cap):
     rows = np.random.default_rng(3).choice(np.arange(10, n), 256, replace=False)
     abs_sum = np.abs(U[rows] @ Uc.T).sum(axis=1)
     assert np.all(err[rows] <= 1e-5 * abs_sum)
+
+
+def test_config5_full_size_diversity_selection(cuda):
+    """BASELINE config 5 at full size: 8,000,000 x 128
+    U[0,1) pool (default_rng(0)) rounded to bf16, L = the first 1,024 rows,
+    k = 1000 (similarity.py:34-38 restated as max-cosine to the labeled set).
+    The oracle cannot sweep 8M x 1,024 pairs in seconds, so the selection is
+    pinned by size-independent properties: the selected scores ARE the
+    canonical fp64 max-cos of the selected rows (bit for bit), the kernel's
+    fp32 max-cos is within dal_maxcos_error_bound of the canonical value on
+    4,096 sampled rows, and no sampled unselected row beats the k-th
+    selected score (ties -> lower index)."""
+    import torch
+
+    import bench
+    from dal import _lib
+    from dal import similarity as sim
+
+    n, d, m, k = 8_000_000, 128, 1024, 1000
+    x = torch.from_numpy(bench.host_pool(0, n, d, "uniform")).to(cuda).to(torch.bfloat16)
+    L = np.arange(m)
+    cand = torch.arange(m, n, device=cuda)
+    sel = sim.diversity_select(x, L, k, candidates=cand, device=cuda)
+    idx, sc = _np(sel.indices), _np(sel.selected_scores)
+    assert idx.shape == (k,) and np.all(idx >= m) and np.unique(idx).size == k
+    # canonical fp64 max-cos of the selected rows (oracle on the bf16 values)
+    lab = x[:m].float().cpu().numpy()
+    rows = x[torch.from_numpy(idx).to(cuda)].float().cpu().numpy()
+    ref_sel, _ = O.max_cosine_canonical(np.concatenate([lab, rows]), np.arange(m))
+    assert np.array_equal(ref_sel[m:].view(np.int64), sc.view(np.int64))
+    assert np.all((sc[1:] > sc[:-1]) | ((sc[1:] == sc[:-1]) & (idx[1:] > idx[:-1])))
+    # sampled rows: fp32 kernel value within its bound; nothing better than the k-th
+    pick = np.unique(np.linspace(m, n - 1, 4096).round().astype(np.int64))
+    pick_t = torch.from_numpy(pick).to(cuda)
+    m_gpu, _ = sim.max_cosine(torch.cat([x[:m], x[pick_t]]), np.arange(m), device=cuda)
+    m_gpu = _np(m_gpu)[m:].astype(np.float64)
+    ref_pick, _ = O.max_cosine_canonical(np.concatenate([lab, x[pick_t].float().cpu().numpy()]), np.arange(m))
+    ref_pick = ref_pick[m:]
+    bound = float(_lib.load().dal_maxcos_error_bound(d))
+    assert np.abs(m_gpu - ref_pick).max() <= bound
+    out = ~np.isin(pick, idx)
+    kth, kth_i = sc[-1], idx[-1]
+    assert np.all((ref_pick[out] > kth) | ((ref_pick[out] == kth) & (pick[out] > kth_i)))
+    # the selected rows' fp32 kernel values also sit within the bound
+    sel_mx = _np(sel.scores)[idx - m].astype(np.float64)
+    assert np.abs(sel_mx - sc).max() <= bound
+    del x
+    torch.cuda.empty_cache()
