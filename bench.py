@@ -229,7 +229,8 @@ def gram_roofline(gram, achieved, traffic, gram_ms, gram_ms_max, flops, products
                 "launch_ms_max_over_ranks": gram_ms_max, "algorithmic_flops_per_launch": flops}
     sym = gram == "sym"
     executed = achieved * products / (2.0 if sym else 1.0)
-    names = {3: "h.h, h.l, l.h", 2: "h.h, h.l + exact residual <l_i, block sums>"}
+    names = {3: "h.h, h.l, l.h", 2: "H.H, H.L on the taker side + the exact closed-form remainder "
+                                     "(dal_gram_sym_residual, included in launch_ms)"}
     return {"bound": "mfma",
             "kernel": (f"dal_gram_rowsum_{'sym' if sym else 'split'} ({'symmetric block pairs once; ' if sym else ''}"
                        f"{products} x v_mfma_f32_16x16x32_f16 per 32 features: {names.get(products, '')})"),
@@ -443,11 +444,14 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
 
     for _ in range(warmup):
         step()
-    state.gram_events = []
+    state.gram_events, state.residual_events = [], []
     elapsed, (idx_g, sc_g) = _timed(step, steps, barrier)
     events, state.gram_events = state.gram_events, None
-    # the Gram launches of one step (one, or own-shard + rest when N > 1), averaged over steps
-    gram_ms = sum(a.elapsed_time(b) for a, b in events) / max(steps, 1)
+    res_events, state.residual_events = state.residual_events, []
+    # the density launches of one step (the Gram: one, or own-shard + rest when
+    # N > 1; plus the compensation's closed-form remainder), averaged over steps
+    resid_ms = sum(a.elapsed_time(b) for a, b in res_events) / max(steps, 1)
+    gram_ms = sum(a.elapsed_time(b) for a, b in events) / max(steps, 1) + resid_ms
     elapsed, gram_ms_max = _max_over_ranks([elapsed, gram_ms], world, dist, tdev)
 
     # accuracy (outside the timed region): the timed step's
@@ -526,9 +530,8 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
     rows_local = (hi - lo) - int(np.sum((excluded >= lo) & (excluded < hi)))
     flops = 2.0 * rows_local * (n - N_EXCLUDED) * d
     achieved = flops / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else 0.0
-    traffic = _traffic(config, {"sym": "gram_rowsum_sym_bytes_per_launch",
-                                "split": "gram_rowsum_split_bytes_per_launch"}.get(
-                                    state.gram, "gram_rowsum_bytes_per_launch"), world)
+    traffic = _traffic(config, "gram_csym_bytes_per_launch" if state.gram == "sym"
+                       else "gram_rowsum_bytes_per_launch", world)
     ms_per_step = elapsed * 1000 / steps
     out = {
         "metric": METRIC,
@@ -576,8 +579,8 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
                        "note": "density via the exact O(N*D) identity sum_j<u_i,u_j> = <u_i, sum_j u_j> "
                                "(canonical fp64, same selection); HBM-bound, not the MFMA path"}
                       if sep_ms else None),
-        "roofline": gram_roofline(state.gram, achieved, traffic, gram_ms, gram_ms_max, flops,
-                                  engine.gram_products(state)),
+        "roofline": dict(gram_roofline(state.gram, achieved, traffic, gram_ms, gram_ms_max, flops,
+                                       engine.gram_products(state)), residual_ms=resid_ms),
         "roofline_forest": forest_roofline(state.n, d, cfg["trees"], forest_ms, config, world),
         "roofline_topk": topk_roofline(state.n, select_ms, config, world,
                                        engine.LEVEL1_PASSES if state.level1_fast else 0),

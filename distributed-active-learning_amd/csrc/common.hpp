@@ -20,6 +20,10 @@ __host__ __device__ inline int64_t round_up(int64_t a, int64_t b) { return ceil_
 
 inline hipStream_t as_stream(dal_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Features per slice of the split Gram operand (gram_sym.hip): 128 when
+// d_pad % 128 == 0, 32 for d_pad == 32, else 64.
+int split_ks(int64_t d_pad);
+
 // Order-preserving map of an fp64 score to a uint64 key, smaller = better.
 // -0.0 and +0.0 share a key (the reference compares them equal); NaN sorts
 // after every number (DAL_KEY_NAN) in either direction.

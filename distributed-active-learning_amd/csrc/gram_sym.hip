@@ -1,0 +1,899 @@
+// Symmetric, compensated cosine Gram row-sum: the density d_i = sum_{j not in
+// E} <u_i, u_j> of every pool row on fp16 MFMA at fp32-class accuracy, with S
+// never stored.
+//
+// Reference: final_thesis/density_weighting.py:67-75 (U.multiply(UT) through
+// IndexedRowMatrix/BlockMatrix), :95-100 (drop i,j in L0) and :157-161
+// (groupByKey + sum per row); cosine_similarity.py:29-45 is the same product.
+//
+// Operand (dal_prep_split): every fp32 unit row at scale 2^12 as two fp16
+// terms, H = fp16(2^12 u), L = fp16(2^12 u - H); u~ = H + L carries 2^12 u to
+// 2^-22 relative, every product of two terms is exact in fp32 and lands in
+// units of 2^-24.  Layout [n_pad][d_pad / KS][KS H | KS L].
+//
+// Symmetry.  Rows are grouped in 512-row super blocks.  Each unordered pair
+// {P, Q} is multiplied once: P takes Q iff Q == P (diagonal: row sums only),
+// Q > P with P+Q even, or Q < P with P+Q odd (global indices, so the bits do
+// not depend on the sharding).  The taker's rows are the A operand (register
+// resident), Q's the B operand (LDS-staged); the tile's row sums go to P's rows
+// and its column sums to Q's rows.
+//
+// Compensation.  The A side holds H only: the MFMAs form T_ij = <H_i, u~_j>
+// (two products per feature pair, H.H and H.L), and the exact remainder
+// <L_i, u~_j> of every taken pair is added afterwards in closed form -- for a
+// row r of super block B (dal_gram_sym_residual):
+//   row role (B takes Q):         sum_Q <L_r, sigma~_Q>       = <L_r, R_B>
+//   column role (P takes B, P!=B): sum_P <u~_r, sigma^L_P>     = <u~_r, C_B>
+// with sigma~_Q / sigma^L_Q the sums of u~ / L over Q's rows (exact int64 in
+// units of 2^-24) and R_B, C_B their sums over B's partners (parity-class
+// prefix sums).  d_i is then sum_j <u~_i, u~_j> with nothing dropped: the MFMA
+// work per algorithmic product is 2 fp16 products on half the pairs.
+//
+// Exactness of the row sums (as the earlier kernels): chains are folded to
+// multiples of 2^-32 and added as integers (LDS fp64 below 2^53, int64
+// atomics); the residual is an fp64 dot in a fixed order rounded to 2^-32.
+// The density bits are identical for any grid, column split or GPU count.
+//
+// MI355X design: block = 4 waves x 128 rows (one super block), A fragments
+// (8 row tiles x KS features of H) in registers; 32 KiB B stages in a 2-deep
+// LDS ring filled by global_load_lds_dwordx4 (source-side XOR swizzle ->
+// conflict-free ds_read_b128); two blocks per CU (two waves per SIMD).  Per
+// 16x16 output tile two accumulator chains per row tile (even / odd column
+// tiles) carry the row sums through the MFMAs; a tile's column sums are the
+// growth of its chain's lane total.  KS = 128 for d_pad % 128 == 0 (the H-only
+// A side frees the registers the L fragments held), else 64, or 32 with the
+// column sums from sigma_P MFMAs.
+#include <stdlib.h>
+
+#include <utility>
+#include <vector>
+
+#include "common.hpp"
+
+namespace dal {
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+#define AS3 __attribute__((address_space(3)))
+
+constexpr int kThreads = 256;  // 4 waves
+constexpr int kSB = 512;       // super block rows
+
+__device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// One step of a reduce-scatter over the 16 lanes of a DPP row: lanes whose
+// select bit is clear keep v[k] (k < H) summed with their partner's, lanes
+// whose bit is set keep v[k + H]; CTRL is a DPP permutation pairing each lane
+// with a lane of the opposite bit (row_mirror, row_half_mirror, quad swaps).
+template <int H, int CTRL, int N = 32>
+__device__ __forceinline__ void rs_step(float (&v)[N], bool hi) {
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    const float keep = hi ? v[k + H] : v[k];
+    const float send = hi ? v[k] : v[k + H];
+    v[k] = keep + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, send), CTRL,
+                                                                        0xF, 0xF, false));
+  }
+}
+
+// Reduce-scatter of N values over the 16 lanes of a DPP row (N = 16: lane li
+// ends with the 16-lane sum of value li; N = 8: of value li & 7).
+template <int N>
+__device__ __forceinline__ void row_sum_scatter(float (&v)[N], int li) {
+  if constexpr (N >= 16) {
+    rs_step<N / 2, 0x140, N>(v, li & 8);
+  } else {
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+      v[k] += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v[k]), 0x140, 0xF,
+                                                                   0xF, false));
+  }
+  rs_step<N >= 16 ? 4 : N / 2, 0x141, N>(v, li & 4);
+  rs_step<N >= 16 ? 2 : N / 4, 0x4E, N>(v, li & 2);
+  rs_step<N >= 16 ? 1 : N / 8, 0xB1, N>(v, li & 1);
+}
+
+// Lane id recomputed at the point of use (asm volatile: never hoisted out of
+// a loop), so lane-derived addresses are rematerialised instead of occupying
+// VGPRs across the pair loop (a spill reload's vmcnt wait would drain the DMA).
+__device__ __forceinline__ unsigned fresh_lane() {
+  unsigned v;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
+  return v;
+}
+
+template <int KS>
+struct Cfg {
+  static constexpr int ROWB = KS * 4;               // bytes per operand row of a slice (H + L)
+  static constexpr int SLOTS = ROWB / 16;           // 16-B slots per row
+  static constexpr int HI = KS / 8;                 // slots of the H part
+  static constexpr int STAGE = 32768;               // bytes per LDS stage
+  static constexpr int SC = STAGE / ROWB;           // columns per stage: 64 / 128 / 256
+  static constexpr int SPP = 256 / SC;              // stages per 512 x 256 pair: 4 / 2 / 1
+  static constexpr int FOLD = KS == 128 ? 128 : 256;  // columns per row fold (chains <= 1024 products)
+  static constexpr int SPF = FOLD / SC;             // stages per fold group
+  static constexpr int F4 = STAGE / 16;
+  static constexpr int SWZ = (SLOTS < 16 ? SLOTS : 16) - 1;
+  static constexpr int PIECES = STAGE / (4 * 1024);  // 1-KiB DMA pieces per wave per stage
+  static constexpr int RT = 8;                      // 16-row tiles per wave (128 rows)
+  static constexpr int LG = 4;
+  static constexpr int NKS = KS / 32;               // k-steps of v_mfma_f32_16x16x32_f16
+  static constexpr int NCT = SC / 16;               // column tiles per stage
+  static constexpr bool SIG = KS == 32;             // column sums from sigma_P MFMAs
+  static constexpr int NCH = SIG ? 1 : 2;           // row-sum chains per row tile
+  static_assert(SPF >= 1 && SPP % SPF == 0 && PIECES >= 1 && NKS >= 1, "bad slice");
+};
+
+template <int KS>
+__global__ __launch_bounds__(kThreads, 2) void gram_csym_kernel(
+    const uint16_t* __restrict__ urows, int srow0, int n_srb,
+    const uint16_t* __restrict__ ucols, int jcol0, int j_lo, int j_hi, int skip_lo, int skip_hi,
+    int ns_active, int64_t ldh, int slice_off, int chunk_j, int n_chunks,
+    unsigned long long* __restrict__ acc_out, int contig) {
+  using C = Cfg<KS>;
+  constexpr bool SIG = C::SIG;
+  constexpr int NCH = C::NCH;
+  __shared__ __attribute__((aligned(16))) float4 lds[2 * C::F4];
+  __shared__ double colacc[2][256];
+  __shared__ double rowacc[kSB];
+  // sigma_P (KS 32): per-wave partial sums of the H rows, then the sum split in
+  // two fp16 terms (at 2^-6 of the operand's scale), read as an A fragment
+  __shared__ float sig_part[SIG ? 4 : 1][SIG ? KS : 1];
+  __shared__ f16x8 sig_row[SIG ? 2 * C::HI : 1];
+
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int li = lane & 15, lq = lane >> 4;
+  const int G = gridDim.x, g = blockIdx.x;
+  colacc[0][tid] = 0.0;
+  colacc[1][tid] = 0.0;
+  rowacc[tid] = 0.0;
+  rowacc[tid + 256] = 0.0;
+
+  // Work = the pairs (P, J) over row super blocks P and 256-column blocks J in
+  // [j_lo, j_hi) minus [skip_lo, skip_hi), as segments (P, raw column range
+  // [rlo, rhi)) walked by a raw column cursor r (J = jmap(r)):
+  //  contig: block g owns the g-th 1/G of the P-major raw grid (P, r);
+  //  chunk:  unit u = (P = u % n_srb, column chunk u / n_srb), dealt round-robin
+  //          (all blocks sweep the same column chunks together: L2 / MALL reuse).
+  const int sk_lo = skip_lo > j_lo ? skip_lo : j_lo, sk_hi = skip_hi < j_hi ? skip_hi : j_hi;
+  const int skl = contig && sk_hi > sk_lo ? sk_hi - sk_lo : 0;  // chunk mode skips through takes()
+  const int nje = j_hi - j_lo - skl;
+  const int nre0 = ns_active - srow0, nre = nre0 < n_srb ? (nre0 > 0 ? nre0 : 0) : n_srb;
+  const int64_t raw = static_cast<int64_t>(nre) * nje;
+  const int64_t ka = raw * g / G, kb = raw * (g + 1) / G;
+  const int n_seg = contig ? (kb > ka ? static_cast<int>((kb - 1) / nje - ka / nje) + 1 : 0) : n_srb * n_chunks;
+  const int seg_step = contig ? 1 : G;
+  auto seg_P = [&](int u) { return contig ? srow0 + static_cast<int>(ka / nje) + u : srow0 + u % n_srb; };
+  auto seg_rlo = [&](int u) { return contig ? (u == 0 ? static_cast<int>(ka % nje) : 0) : (u / n_srb) * chunk_j; };
+  auto seg_rhi = [&](int u) {
+    if (contig) return u == n_seg - 1 ? static_cast<int>((kb - 1) % nje) + 1 : nje;
+    const int e = (u / n_srb + 1) * chunk_j;
+    return e < nje ? e : nje;
+  };
+  auto jmap = [&](int r) { return j_lo + r + (j_lo + r >= sk_lo ? skl : 0); };
+  auto takes = [&](int P, int J) -> bool {
+    const int Q = J >> 1;
+    if (J >= skip_lo && J < skip_hi) return false;
+    return Q == P || (Q > P && ((P + Q) & 1) == 0) || (Q < P && ((P + Q) & 1));
+  };
+  auto first_r = [&](int P, int r, int rhi) -> int {
+    if (P >= ns_active) return -1;
+    while (r < rhi && !takes(P, jmap(r))) ++r;
+    return r < rhi ? r : -1;
+  };
+  auto seek = [&](int u, int& r) {
+    while (u < n_seg) {
+      r = first_r(seg_P(u), seg_rlo(u), seg_rhi(u));
+      if (r >= 0) break;
+      u += seg_step;
+    }
+    return u;
+  };
+
+  auto voff = [&](int q) {
+    const int p = (wave * C::PIECES + q) * 64 + static_cast<int>(fresh_lane());
+    const int row = p / C::SLOTS;
+    const int slot = (p % C::SLOTS) ^ (row & C::SWZ);
+    return static_cast<unsigned>(row * ldh * 2 + slot * 16);
+  };
+  const unsigned dst0 = __builtin_amdgcn_readfirstlane(
+      static_cast<unsigned>(reinterpret_cast<uintptr_t>((AS3 float4*)(lds + wave * C::PIECES * 64))));
+  // stage h of 256-column block J into LDS buffer buf.  Inline asm so the
+  // compiler does not track the DMA on vmcnt (block_sync waits for it).
+  auto issue = [&](int buf, int J, int h) {
+    const uint16_t* sbase = ucols + (static_cast<int64_t>(J - jcol0) * 256 + h * C::SC) * ldh + slice_off;
+#pragma unroll
+    for (int q = 0; q < C::PIECES; ++q) {
+      const unsigned dst = dst0 + static_cast<unsigned>(buf * C::STAGE + q * 1024);
+      unsigned keep;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+          "global_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "v"(voff(q)), "s"(dst), "s"(sbase)
+          : "memory");
+    }
+  };
+
+  // resident A fragments: H of rows P*512 + wave*128 + rt*16 + (lane & 15),
+  // features of k-step c and lane group lq
+  f16x8 ah[C::RT][C::NKS];
+  auto load_a = [&](int P) {
+    const uint16_t* pb = urows + static_cast<int64_t>(P - srow0) * kSB * ldh + slice_off;
+    const unsigned fl = fresh_lane();
+    const unsigned lrow = static_cast<unsigned>((wave * 128 + (fl & 15)) * ldh + (fl >> 4) * 8);
+    const unsigned tstep = static_cast<unsigned>(16 * ldh);
+#pragma unroll
+    for (int rt = 0; rt < C::RT; ++rt)
+#pragma unroll
+      for (int c = 0; c < C::NKS; ++c)  // read once per unit: keep the column stages resident in L2
+        ah[rt][c] = __builtin_nontemporal_load(reinterpret_cast<const f16x8*>(pb + lrow + rt * tstep + c * C::LG * 8));
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    if constexpr (SIG) {
+      // this wave's 128 H rows summed per feature (lane order over the row
+      // tiles, then over the 16 lanes of the DPP row)
+      constexpr int V = C::NKS * 8;
+      float sp[V];
+#pragma unroll
+      for (int c = 0; c < C::NKS; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float t = 0.0f;
+#pragma unroll
+          for (int rt = 0; rt < C::RT; ++rt) t += static_cast<float>(ah[rt][c][e]);
+          sp[c * 8 + e] = t;
+        }
+      const int fl2 = static_cast<int>(fresh_lane()), fli = fl2 & 15, flq = fl2 >> 4;
+      row_sum_scatter<V>(sp, fli);
+      if (fli < V) sig_part[wave][(fli >> 3) * 32 + flq * 8 + (fli & 7)] = sp[0];
+    }
+  };
+  // after a block_sync that follows load_a: sigma_P = the four waves' partials
+  // (fixed order), scaled by 2^-6 (exact) and split into two fp16 terms
+  auto build_sigma = [&]() {
+    if constexpr (SIG) {
+      if (tid < KS) {
+        const float sg = ((sig_part[0][tid] + sig_part[1][tid]) + sig_part[2][tid]) + sig_part[3][tid];
+        const float s6 = sg * 0x1p-6f;
+        const _Float16 h = static_cast<_Float16>(s6);
+        const _Float16 l = static_cast<_Float16>(s6 - static_cast<float>(h));
+        reinterpret_cast<_Float16*>(sig_row)[tid] = h;
+        reinterpret_cast<_Float16*>(sig_row)[KS + tid] = l;
+      }
+    }
+  };
+  constexpr float kFold = 0x1p8f;  // units of 2^-24 -> multiples of 2^-32
+
+  // B-fragment LDS offsets (float4 units): slot (k + lq) ^ (li & SWZ) of
+  // column row li, k = c*LG (+ HI for the L half) a multiple of 4; the XOR
+  // splits into a lane part (low 2 bits) and a k part (k ^ (li & SWZ & ~3)),
+  // so two registers cover every k-step and half
+  const int b_base = li * C::SLOTS + (lq ^ (li & 3));
+  const int b_swz = li & C::SWZ & ~3;
+  auto b_off = [&](int c, bool lo_half) { return b_base + ((c * C::LG + (lo_half ? C::HI : 0)) ^ b_swz); };
+
+  f32x4 mc[NCH][C::RT];
+  float tprev[2];
+  f16x8 sgh[SIG ? C::NKS : 1], sgl[SIG ? C::NKS : 1];
+  // one stage of SC columns (col0 = its first column within the pair);
+  // fresh = first stage of a fold group (chains restart).  B fragments go
+  // through two register sets: k-step i+1's are read while k-step i's MFMAs
+  // issue (16 MFMAs of latency cover).
+  auto compute = [&](int buf, float cmul, int cbuf, int col0, bool fresh_stage) {
+    f16x8 bh[2], bl[2];
+    auto load_b = [&](int set, int c, int ct) {
+      bh[set] = __builtin_bit_cast(f16x8, lds[buf * C::F4 + ct * 16 * C::SLOTS + b_off(c, false)]);
+      bl[set] = __builtin_bit_cast(f16x8, lds[buf * C::F4 + ct * 16 * C::SLOTS + b_off(c, true)]);
+    };
+    load_b(0, 0, 0);
+#pragma unroll
+    for (int ct = 0; ct <= C::NCT; ++ct) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (ct < C::NCT) {
+        const int ch = ct % NCH;
+        const bool fresh = fresh_stage && ct < NCH;
+        const bool sig = SIG && (ct & 3) == wave;  // column tile ct's sums: this wave's turn
+        f32x4 sg = {};
+#pragma unroll
+        for (int c = 0; c < C::NKS; ++c) {
+          const int i = ct * C::NKS + c, cur = i & 1;
+          if (c + 1 < C::NKS)
+            load_b(cur ^ 1, c + 1, ct);
+          else if (ct + 1 < C::NCT)
+            load_b(cur ^ 1, 0, ct + 1);
+          const f32x4 zero = {};
+#pragma unroll
+          for (int rt = 0; rt < C::RT; ++rt)
+            mc[ch][rt] = mfma16(ah[rt][c], bh[cur], (c == 0 && fresh) ? zero : mc[ch][rt]);
+#pragma unroll
+          for (int rt = 0; rt < C::RT; ++rt) mc[ch][rt] = mfma16(ah[rt][c], bl[cur], mc[ch][rt]);
+          if (sig) {
+            sg = mfma16(sgh[c], bh[cur], sg);
+            sg = mfma16(sgh[c], bl[cur], sg);
+            sg = mfma16(sgl[c], bh[cur], sg);
+          }
+        }
+        // every output row of the sigma tile is the column sum (units 2^-18)
+        if (sig && lq == 0)
+          colacc[cbuf][col0 + ct * 16 + li] = static_cast<double>(__builtin_rintf(sg[0] * cmul * 64.0f));
+      }
+      if (!SIG && ct > 0) {
+        // tile ct-1's column sums: growth of its chain's lane total
+        const int ch = (ct - 1) & 1;
+        float t0 = mc[ch % NCH][0][0], t1 = mc[ch % NCH][0][1];
+#pragma unroll
+        for (int rt = 0; rt < C::RT; ++rt) {
+#pragma unroll
+          for (int r = rt == 0 ? 2 : 0; r < 4; r += 2) {
+            t0 += mc[ch % NCH][rt][r];
+            t1 += mc[ch % NCH][rt][r + 1];
+          }
+        }
+        const float T = t0 + t1;
+        const float cp = (fresh_stage && ct - 1 < 2) ? T : T - tprev[ch];
+        tprev[ch] = T;
+        atomicAdd(&colacc[cbuf][col0 + (ct - 1) * 16 + li], static_cast<double>(__builtin_rintf(cp * cmul)));
+      }
+      if (ct < C::NCT) {
+        constexpr int NM = 2 * C::RT;  // MFMAs per k-step
+#pragma unroll
+        for (int c = 0; c < C::NKS; ++c) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // next k-step's B
+#pragma unroll
+          for (int i = 0; i < NM; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);    // MFMA
+            if constexpr (!SIG) __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // VALU (epilogue)
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // chains -> LDS row accumulator (exact integer fp64 adds).  A 4-step DPP
+  // reduce-scatter over the 16 column lanes leaves each lane 2 fully summed
+  // rows, added by all 64 lanes at distinct LDS addresses.
+  auto fold_rows = [&]() {
+    float v[32];
+#pragma unroll
+    for (int rt = 0; rt < C::RT; ++rt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[rt * 4 + q] = NCH == 1 ? mc[0][rt][q] : mc[0][rt][q] + mc[NCH - 1][rt][q];
+    rs_step<16, 0x140>(v, li & 8);  // row_mirror: lane i <-> 15 - i
+    rs_step<8, 0x141>(v, li & 4);   // row_half_mirror: i <-> i ^ 7
+    rs_step<4, 0x4E>(v, li & 2);    // quad_perm [2,3,0,1]
+    rs_step<2, 0xB1>(v, li & 1);    // quad_perm [1,0,3,2]
+    const int rt = ((li >> 1) & 1) | (((li >> 2) & 1) << 1) | (((li >> 3) & 1) << 2);
+    const int row = wave * 128 + rt * 16 + 4 * lq + 2 * (li & 1);
+    atomicAdd(&rowacc[row], static_cast<double>(__builtin_rintf(v[0] * kFold)));
+    atomicAdd(&rowacc[row + 1], static_cast<double>(__builtin_rintf(v[1] * kFold)));
+  };
+  auto flush_one = [&](double& slot, int64_t out_row) {
+    const double v = slot;
+    if (v != 0.0) atomicAdd(acc_out + out_row, static_cast<unsigned long long>(static_cast<long long>(v)));
+    slot = 0.0;
+  };
+  auto flush_cols = [&](int cbuf, int Jf) { flush_one(colacc[cbuf][tid], static_cast<int64_t>(Jf) * 256 + tid); };
+  auto flush_rows = [&](int Pf) {
+    flush_one(rowacc[tid], static_cast<int64_t>(Pf) * kSB + tid);
+    flush_one(rowacc[tid + 256], static_cast<int64_t>(Pf) * kSB + tid + 256);
+  };
+  // every barrier waits for this wave's LDS adds and DMA first (hipcc may
+  // omit the lgkmcnt wait at a loop-top barrier after no-return LDS adds)
+  auto block_sync = [&]() {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+
+  int r = -1;
+  int unit = seek(contig ? 0 : g, r);
+  if (unit >= n_seg) return;
+  int P = seg_P(unit), rhi_u = seg_rhi(unit);
+  int J = jmap(r);
+  issue(0, J, 0);
+  load_a(P);
+  bool sig_fresh = true;
+  int cb = 0;       // colacc buffer of the current pair
+  int buf = 0;      // LDS stage buffer of the next stage to compute
+  int flushJ = -1;  // column block whose sums wait in colacc[cb ^ 1]
+  int flushP = -1;  // row super block whose sums wait in rowacc
+
+  while (true) {
+    int nr = first_r(P, r + 1, rhi_u), n_unit = unit;
+    if (nr < 0) n_unit = seek(unit + seg_step, nr);
+    const bool has_next = n_unit < n_seg;
+    const int nP = has_next ? seg_P(n_unit) : -1;
+    const bool new_rows = nP != P;
+    const int nJ = has_next ? jmap(nr) : -1;
+    const bool diag = (J >> 1) == P;
+    const float cmul = diag ? 0.0f : kFold;  // diagonal super block: row sums only
+
+#pragma unroll
+    for (int s = 0; s < C::SPP; ++s) {
+      block_sync();
+      if (s == 0) {
+        if (flushJ >= 0) flush_cols(cb ^ 1, flushJ);
+        if (flushP >= 0) flush_rows(flushP);
+        flushP = -1;
+        if (SIG && sig_fresh) {
+          build_sigma();
+          block_sync();
+          sig_fresh = false;
+#pragma unroll
+          for (int c = 0; c < (SIG ? C::NKS : 0); ++c) {
+            const int flq = static_cast<int>(fresh_lane()) >> 4;
+            sgh[c] = sig_row[c * C::LG + flq];
+            sgl[c] = sig_row[C::HI + c * C::LG + flq];
+          }
+        }
+      }
+      if (s + 1 < C::SPP)
+        issue(buf ^ 1, J, s + 1);
+      else if (has_next)
+        issue(buf ^ 1, nJ, 0);
+      compute(buf, cmul, cb, s * C::SC, s % C::SPF == 0);
+      if (s % C::SPF == C::SPF - 1) fold_rows();
+      buf ^= 1;
+    }
+
+    flushJ = diag ? -1 : J;
+    cb ^= 1;
+    if (new_rows) flushP = P;
+    if (!has_next) break;
+    unit = n_unit;
+    rhi_u = seg_rhi(unit);
+    if (new_rows) {
+      P = nP;
+      load_a(P);
+      sig_fresh = true;
+    }
+    r = nr;
+    J = nJ;
+  }
+  block_sync();
+  if (flushJ >= 0) flush_cols(cb ^ 1, flushJ);
+  if (flushP >= 0) flush_rows(flushP);
+}
+
+// ---------------------------------------------------------------------------
+// Residual of the compensation (see the header).  Three launches:
+//  1. per super block Q: sigma~_Q and sigma^L_Q, exact int64 in units of 2^-24
+//     (every H and L is a multiple of 2^-24 below 2^13);
+//  2. per feature: exclusive prefix sums over super blocks of each parity
+//     class and their totals, giving R_B and C_B for every requested B;
+//  3. per row r of the requested super blocks: acc[r] += rint(2^8 *
+//     (<L_r, R_B> + <u~_r, C_B>)) with the dots in fp64 in a fixed order.
+
+// operand element (H or L half) of feature f of a row
+__device__ __forceinline__ const uint16_t* half_ptr(const uint16_t* row, int f, int ks, bool lo) {
+  return row + (f / ks) * (2 * ks) + (lo ? ks : 0) + (f % ks);
+}
+
+__device__ __forceinline__ long long half_units(uint16_t bits) {  // fp16 value * 2^24, exact
+  return static_cast<long long>(static_cast<float>(__builtin_bit_cast(_Float16, bits)) * 16777216.0f);
+}
+
+// One block per (super block, group of 256 16-byte chunk columns): the
+// super block's 512 operand rows are 512 x CPR 16-byte chunks (CPR = ldh / 8
+// per row: the H and L halves of every slice); thread t always reads chunk
+// column t % CPR (8 H or 8 L halves of one slice) of rows t / CPR, + 256 /
+// CPR, ... -- independent 16-B loads, 8 in flight -- summed exactly in int64,
+// then reduced over the threads of the same column in LDS.
+__global__ __launch_bounds__(256) void csym_sigma_kernel(const uint16_t* __restrict__ ops, int64_t ldh, int ks,
+                                                         int d_pad, long long* __restrict__ sig_u,
+                                                         long long* __restrict__ sig_l) {
+  __shared__ long long red[256][9];  // [thread][8 halves] (+1: bank spread)
+  const int Q = blockIdx.x;
+  const int cpr = static_cast<int>(ldh / 8);      // chunks per row
+  const int cols = cpr < 256 ? cpr : 256;          // chunk columns of this block
+  const int col = blockIdx.y * 256 + threadIdx.x % cols;
+  const int rstep = 256 / cols;                    // rows advanced per round
+  const int r0 = threadIdx.x / cols;
+  long long acc[8] = {};
+  if (col < cpr && r0 < rstep) {
+    const uint4* base = reinterpret_cast<const uint4*>(ops + static_cast<int64_t>(Q) * kSB * ldh) + col;
+    for (int r = r0; r < kSB; r += 8 * rstep) {
+      uint4 q[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q[j] = r + j * rstep < kSB ? base[static_cast<int64_t>(r + j * rstep) * cpr] : uint4{};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t w[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[2 * e] += half_units(static_cast<uint16_t>(w[e] & 0xFFFFu));
+          acc[2 * e + 1] += half_units(static_cast<uint16_t>(w[e] >> 16));
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[threadIdx.x][e] = acc[e];
+  __syncthreads();
+  // thread t < cols finishes chunk column t: sum over the rstep row phases
+  if (threadIdx.x < cols && col < cpr) {
+    long long v[8] = {};
+    for (int p = 0; p < rstep; ++p)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += red[p * cols + threadIdx.x][e];
+    // chunk column -> (slice, half, first feature): the row is [slice][H KS | L KS]
+    const int hpc = ks / 8;                        // chunks per half of a slice
+    const int slice = col / (2 * hpc), within = col % (2 * hpc);
+    const bool lo = within >= hpc;
+    const int f0 = slice * ks + (within % hpc) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int64_t o = static_cast<int64_t>(Q) * d_pad + f0 + e;
+      if (lo) {
+        sig_l[o] = v[e];
+        atomicAdd(reinterpret_cast<unsigned long long*>(sig_u + o), static_cast<unsigned long long>(v[e]));
+      } else {
+        atomicAdd(reinterpret_cast<unsigned long long*>(sig_u + o), static_cast<unsigned long long>(v[e]));
+      }
+    }
+  }
+}
+
+// block = 8 waves; lane = one of 64 features (blockIdx.x * 64 + lane), wave w
+// owns super blocks [w*ns/8, (w+1)*ns/8).  R_B, C_B written as fp64 for B in
+// [b0, b1).
+__global__ __launch_bounds__(512) void csym_scan_kernel(const long long* __restrict__ sig_u,
+                                                         const long long* __restrict__ sig_l, int ns, int d_pad,
+                                                         int b0, int b1, double* __restrict__ rb,
+                                                         double* __restrict__ cb) {
+  constexpr int kW = 8;  // waves
+  __shared__ long long part[kW][4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int f = blockIdx.x * 64 + lane;
+  const bool live = f < d_pad;
+  const int q0 = static_cast<int>(static_cast<int64_t>(ns) * w / kW);
+  const int q1 = static_cast<int>(static_cast<int64_t>(ns) * (w + 1) / kW);
+  // (u~, L) sums per parity class of the super block (even, odd); named
+  // registers, not arrays indexed by q & 1 (those would live in scratch)
+  long long ue = 0, uo = 0, le = 0, lo = 0;
+  if (live) {
+#pragma unroll 8
+    for (int q = q0; q < q1; ++q) {
+      const long long su = sig_u[static_cast<int64_t>(q) * d_pad + f];
+      const long long sl = sig_l[static_cast<int64_t>(q) * d_pad + f];
+      const bool odd = q & 1;
+      ue += odd ? 0 : su;
+      uo += odd ? su : 0;
+      le += odd ? 0 : sl;
+      lo += odd ? sl : 0;
+    }
+  }
+  part[w][0][lane] = ue;
+  part[w][1][lane] = uo;
+  part[w][2][lane] = le;
+  part[w][3][lane] = lo;
+  __syncthreads();
+  // exclusive prefix over the earlier waves' ranges, and the totals
+  long long eue = 0, euo = 0, ele = 0, elo = 0, tue = 0, tuo = 0, tle = 0, tlo = 0;
+  for (int v = 0; v < kW; ++v) {
+    const long long a0 = part[v][0][lane], a1 = part[v][1][lane], a2 = part[v][2][lane], a3 = part[v][3][lane];
+    if (v < w) {
+      eue += a0;
+      euo += a1;
+      ele += a2;
+      elo += a3;
+    }
+    tue += a0;
+    tuo += a1;
+    tle += a2;
+    tlo += a3;
+  }
+  if (!live) return;
+#pragma unroll 4
+  for (int q = q0; q < q1; ++q) {
+    // e* = exclusive prefix (super blocks < q) per class; b = q's class
+    const bool odd = q & 1;
+    if (q >= b0 && q < b1) {
+      // R_B = sum_{Q >= B, same class} + sum_{Q < B, other class} of sigma~;
+      // C_B = sum_{P < B, same class} + sum_{P > B, other class} of sigma^L
+      const long long R = odd ? (tuo - euo + eue) : (tue - eue + euo);
+      const long long Cc = odd ? (elo + tle - ele) : (ele + tlo - elo);
+      rb[static_cast<int64_t>(q - b0) * d_pad + f] = static_cast<double>(R);
+      cb[static_cast<int64_t>(q - b0) * d_pad + f] = static_cast<double>(Cc);
+    }
+    const long long su = sig_u[static_cast<int64_t>(q) * d_pad + f];
+    const long long sl = sig_l[static_cast<int64_t>(q) * d_pad + f];
+    eue += odd ? 0 : su;
+    euo += odd ? su : 0;
+    ele += odd ? 0 : sl;
+    elo += odd ? sl : 0;
+  }
+}
+
+// one wave per row: lane l takes features l, l+64, ... (sequential fp64 per
+// lane, then a fixed butterfly) -- a fixed order, so the bits are the same on
+// every GPU count.  rows: the operand of the requested super blocks.
+__global__ __launch_bounds__(256) void csym_residual_kernel(const uint16_t* __restrict__ rows, int64_t ldh, int ks,
+                                                            int d_pad, int b0, int n_rows,
+                                                            const double* __restrict__ rb,
+                                                            const double* __restrict__ cb,
+                                                            long long* __restrict__ acc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t rr = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (rr >= n_rows) return;
+  const uint16_t* row = rows + rr * ldh;
+  const int64_t B = rr / kSB;  // relative to b0
+  const double* R = rb + B * d_pad;
+  const double* Cc = cb + B * d_pad;
+  double t = 0.0;
+  for (int f = lane; f < d_pad; f += 64) {
+    const double h = static_cast<double>(static_cast<float>(__builtin_bit_cast(_Float16, *half_ptr(row, f, ks, false))));
+    const double l = static_cast<double>(static_cast<float>(__builtin_bit_cast(_Float16, *half_ptr(row, f, ks, true))));
+    t = t + l * R[f];
+    t = t + (h + l) * Cc[f];
+  }
+#pragma unroll
+  for (int sh = 32; sh >= 1; sh >>= 1) t += __shfl_xor(t, sh);
+  // R, C in units of 2^-24 x (split units); value = t * 2^-24 * 2^-24 ... in
+  // fixed point (2^32): t * 2^-24 (operand units^2 = 2^24 x value) * 2^8
+  if (lane == 0 && t != 0.0) acc[static_cast<int64_t>(b0) * kSB + rr] += static_cast<long long>(__builtin_rint(t * 0x1p-16));
+}
+
+// ---------------------------------------------------------------------------
+int device_cus() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return 256;
+  return cus;
+}
+
+// Number of column blocks J in [lo, hi) that super block I takes (O(1)).
+inline int64_t sb_pairs(int64_t I, int64_t lo, int64_t hi) {
+  auto same_parity = [](int64_t a, int64_t b, int64_t p) -> int64_t {
+    if (b <= a) return 0;
+    return (b - p + 1) / 2 - (a - p + 1) / 2;
+  };
+  int64_t n = (lo <= I && I < hi) ? 1 : 0;
+  n += same_parity(lo > I + 1 ? lo : I + 1, hi, I & 1);
+  n += same_parity(lo, hi < I ? hi : I, (I & 1) ^ 1);
+  return n;
+}
+
+// Pairs (P, J) for row super block P over 256-column blocks [a, b).
+inline int64_t pairs_range(int64_t P, int64_t a, int64_t b) {
+  if (b <= a) return 0;
+  auto takes = [P](int64_t Q) { return Q == P || (Q > P && ((P + Q) & 1) == 0) || (Q < P && ((P + Q) & 1)); };
+  const int64_t qa = a >> 1, qb = (b - 1) >> 1;
+  int64_t n = 2 * sb_pairs(P, qa, qb + 1);
+  if ((a & 1) && takes(qa)) --n;
+  if (!((b - 1) & 1) && takes(qb)) --n;
+  return n;
+}
+inline int64_t pairs_skip(int64_t P, int64_t a, int64_t b, int64_t skip_lo, int64_t skip_hi) {
+  const int64_t sa = a > skip_lo ? a : skip_lo, sb = b < skip_hi ? b : skip_hi;
+  return pairs_range(P, a, b) - pairs_range(P, sa, sb);
+}
+
+// Column-chunk count for the round-robin units: the fewest chunks, at least
+// kMinChunks, whose most loaded block has at most 8 % more pairs than the best
+// balance found (exact pair counts; cached per shape).  More chunks = a
+// smaller column working set swept by every block together (MALL hits; 2M x
+// 256: 16 chunks 3.9 % faster than 1), fewer = fewer A loads and row flushes.
+constexpr int64_t kMinChunks = 16;
+int64_t choose_chunks(int64_t srow0, int64_t n_srb, int64_t lo, int64_t hi, int64_t skip_lo, int64_t skip_hi,
+                      int64_t ns_active, int64_t G0) {
+  struct Entry {
+    int64_t k[8];
+    int64_t nc;
+  };
+  static thread_local Entry cache[8] = {};
+  static thread_local int cache_next = 0;
+  const int64_t key[8] = {srow0, n_srb, lo, hi, skip_lo, skip_hi, ns_active, G0};
+  for (const Entry& e : cache) {
+    bool hit = e.nc > 0;
+    for (int i = 0; i < 8 && hit; ++i) hit = e.k[i] == key[i];
+    if (hit) return e.nc;
+  }
+  const int64_t nj = hi - lo;
+  int64_t best_max = -1;
+  std::vector<int64_t> load;
+  std::vector<std::pair<int64_t, int64_t>> cand;
+  int tried = 0;
+  for (int64_t c = 1; c <= nj && tried < 32; ++c) {
+    const int64_t cbk = ceil_div(nj, c), ncc = ceil_div(nj, cbk);
+    if (c > 1 && cbk == ceil_div(nj, c - 1)) continue;
+    ++tried;
+    const int64_t units = n_srb * ncc, G = units < G0 ? units : G0;
+    load.assign(static_cast<size_t>(G), 0);
+    for (int64_t u = 0; u < units; ++u) {
+      const int64_t P = srow0 + u % n_srb;
+      if (P >= ns_active) continue;
+      const int64_t clo = lo + (u / n_srb) * cbk, chi = clo + cbk < hi ? clo + cbk : hi;
+      load[static_cast<size_t>(u % G)] += pairs_skip(P, clo, chi, skip_lo, skip_hi);
+    }
+    int64_t mx = 0;
+    for (int64_t v : load) mx = v > mx ? v : mx;
+    cand.emplace_back(ncc, mx);
+    if (best_max < 0 || mx < best_max) best_max = mx;
+  }
+  int64_t best_nc = -1;
+  for (int pass = 0; pass < 2 && best_nc < 0; ++pass)
+    for (const auto& c : cand)
+      if ((pass || c.first >= kMinChunks) && c.second * 100 <= best_max * 108) {
+        best_nc = c.first;
+        break;
+      }
+  if (best_nc < 0) best_nc = cand.back().first;
+  Entry& e = cache[cache_next];
+  cache_next = (cache_next + 1) % 8;
+  for (int i = 0; i < 8; ++i) e.k[i] = key[i];
+  e.nc = best_nc;
+  return best_nc;
+}
+
+template <int KS>
+int launch_csym(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint16_t* cols, int64_t jcol0,
+                int64_t j_lo, int64_t j_hi, int64_t skip_lo, int64_t skip_hi, int64_t ns_active, int64_t ldh,
+                int slice_off, int64_t* acc, int grid_blocks, hipStream_t stream) {
+  const int G0 = grid_blocks > 0 ? grid_blocks : 2 * device_cus();
+  const int64_t nj = j_hi - j_lo;
+  // contiguous equal shares of the pair grid per block for a small column
+  // operand (<= 32 MB: 100k x 64 is 2-5 % faster), else round-robin column
+  // chunks whose blocks sweep the same column stages together.  Exact integer
+  // accumulation: the schedule never changes the bits.
+  const int contig = nj * 256 * ldh * 2 <= (int64_t{32} << 20);
+  int64_t cbk = nj, n_chunks = 1, G;
+  if (contig) {
+    const int64_t sl = skip_lo > j_lo ? skip_lo : j_lo, sh = skip_hi < j_hi ? skip_hi : j_hi;
+    const int64_t nre = ns_active - srow0 < n_srb ? ns_active - srow0 : n_srb;
+    const int64_t raw = (nre > 0 ? nre : 0) * (nj - (sh > sl ? sh - sl : 0));
+    if (raw <= 0) return DAL_OK;
+    G = raw < G0 ? raw : G0;
+  } else {
+    const int64_t nc = choose_chunks(srow0, n_srb, j_lo, j_hi, skip_lo, skip_hi, ns_active, G0);
+    cbk = ceil_div(nj, nc);
+    n_chunks = ceil_div(nj, cbk);
+    const int64_t n_units = n_srb * n_chunks;
+    G = n_units < G0 ? n_units : G0;
+  }
+  hipLaunchKernelGGL((gram_csym_kernel<KS>), dim3(static_cast<unsigned>(G)), dim3(kThreads), 0, stream, rows,
+                     static_cast<int>(srow0), static_cast<int>(n_srb), cols, static_cast<int>(jcol0),
+                     static_cast<int>(j_lo), static_cast<int>(j_hi), static_cast<int>(skip_lo),
+                     static_cast<int>(skip_hi), static_cast<int>(ns_active), ldh, slice_off, static_cast<int>(cbk),
+                     static_cast<int>(n_chunks), reinterpret_cast<unsigned long long*>(acc), contig);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}
+
+struct ResidualLayout {
+  size_t sig_u, sig_l, rb, cb, total;
+};
+ResidualLayout residual_layout(int64_t ns_active, int64_t n_srb, int64_t d_pad) {
+  ResidualLayout L{};
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o += (bytes + 255) / 256 * 256;
+    return at;
+  };
+  L.sig_u = take(static_cast<size_t>(ns_active * d_pad) * 8);
+  L.sig_l = take(static_cast<size_t>(ns_active * d_pad) * 8);
+  L.rb = take(static_cast<size_t>(n_srb * d_pad) * 8);
+  L.cb = take(static_cast<size_t>(n_srb * d_pad) * 8);
+  L.total = o;
+  return L;
+}
+
+}  // namespace
+
+int split_ks(int64_t d_pad) { return d_pad == 32 ? 32 : (d_pad % 128 == 0 ? 128 : 64); }
+
+}  // namespace dal
+
+using namespace dal;
+
+extern "C" double dal_density_error_bound_sym(int64_t n_cols) {
+  // dal_gram_rowsum_sym + dal_gram_sym_residual against the canonical fp64
+  // density, per density entry (one column j of row i), u = 2^-23 (a
+  // conservative unit roundoff for the MFMA's internal fp32 adds, counted as
+  // sequential adds), products exact (f16 x f16), c = 1 + 2^-8 >= sum_d |h_i
+  // h_j| + |h_i l_j| over sum_d |u_i u_j| <= 1 (Cauchy-Schwarz on unit rows):
+  //   row side   two chains of <= 4 (KS 128) / 8 (KS 64) tiles x 2 KS products
+  //              (one chain of 16 tiles x 64 at KS 32), <= 1024 products, joined
+  //              by one add and 4 cross-lane adds: gamma_1029 * c
+  //   column side  a tile's partial is T_k - T_{k-1}, T = sum of the lane's 16
+  //              chain values: (8 gamma_128 + 15 gamma_15 + u) * c (KS 128: 4
+  //              tiles of 256 products; the same total); sigma form (KS 32):
+  //              (gamma_22 + gamma_96 + 3 * 2^-22) * c
+  //   residual   <L_i, R_B> + <u~_i, C_B> in fp64: below 2^-40 per column
+  //   split + fp32 unit rows  5 * 2^-22;  fixed-point roundings <= 2^-33 each
+  const double u = 1.0 / 8388608.0;  // 2^-23
+  auto gamma = [u](double n) { return n * u / (1.0 - n * u); };
+  const double row = gamma(1029.0);
+  const double col = 8.0 * gamma(128.0) + 15.0 * gamma(15.0) + u;
+  const double c = 1.0 + 1.0 / 256.0;
+  const double s = 1.0 / 4194304.0;  // 2^-22
+  return ((row > col ? row : col) * c + 5.0 * s + 1e-10) * static_cast<double>(n_cols) + 1e-9;
+}
+
+extern "C" int dal_gram_rowsum_sym_skip(const uint16_t* rows, int64_t row_block0, int64_t n_row_blocks,
+                                        const uint16_t* cols, int64_t col_block0, int64_t j_lo, int64_t j_hi,
+                                        int64_t skip_lo, int64_t skip_hi, int64_t nb_active, int64_t d_pad,
+                                        int64_t* acc, int grid_blocks, dal_stream_t stream) {
+  if (!rows || !cols || !acc) return DAL_ERR_ARG;
+  if (row_block0 < 0 || n_row_blocks <= 0 || col_block0 < 0 || nb_active <= 0) return DAL_ERR_SHAPE;
+  if (j_lo < col_block0 || j_hi < j_lo || j_hi > nb_active || skip_hi < skip_lo) return DAL_ERR_SHAPE;
+  if (d_pad != dal_pad_features(d_pad)) return DAL_ERR_SHAPE;
+  if ((row_block0 | n_row_blocks | nb_active) & 1) return DAL_ERR_SHAPE;  // whole 512-row super blocks
+  if ((reinterpret_cast<uintptr_t>(rows) | reinterpret_cast<uintptr_t>(cols)) & 15) return DAL_ERR_SHAPE;
+  if (j_hi == j_lo || row_block0 >= nb_active) return DAL_OK;
+  hipStream_t st = as_stream(stream);
+  const int ks = split_ks(d_pad);
+  const int64_t ldh = 2 * d_pad;
+  for (int64_t off = 0; off < d_pad; off += ks) {
+    const int so = static_cast<int>(2 * off);  // halves: slice s starts at s * 2 * KS
+    const int64_t s0 = row_block0 / 2, ns = n_row_blocks / 2, na = nb_active / 2;
+    int rc;
+    if (ks == 32)
+      rc = launch_csym<32>(rows, s0, ns, cols, col_block0, j_lo, j_hi, skip_lo, skip_hi, na, ldh, so, acc,
+                           grid_blocks, st);
+    else if (ks == 64)
+      rc = launch_csym<64>(rows, s0, ns, cols, col_block0, j_lo, j_hi, skip_lo, skip_hi, na, ldh, so, acc,
+                           grid_blocks, st);
+    else
+      rc = launch_csym<128>(rows, s0, ns, cols, col_block0, j_lo, j_hi, skip_lo, skip_hi, na, ldh, so, acc,
+                            grid_blocks, st);
+    if (rc != DAL_OK) return rc;
+  }
+  return DAL_OK;
+}
+
+extern "C" int dal_gram_rowsum_sym(const uint16_t* rows, int64_t row_block0, int64_t n_row_blocks,
+                                   const uint16_t* cols, int64_t col_block0, int64_t j_lo, int64_t j_hi,
+                                   int64_t nb_active, int64_t d_pad, int64_t* acc, int grid_blocks,
+                                   dal_stream_t stream) {
+  return dal_gram_rowsum_sym_skip(rows, row_block0, n_row_blocks, cols, col_block0, j_lo, j_hi, 0, 0, nb_active,
+                                  d_pad, acc, grid_blocks, stream);
+}
+
+extern "C" size_t dal_gram_sym_residual_workspace_bytes(int64_t nb_active, int64_t n_row_blocks, int64_t d_pad) {
+  if (nb_active <= 0 || n_row_blocks <= 0 || d_pad <= 0) return 0;
+  return residual_layout(nb_active / 2, n_row_blocks / 2, d_pad).total;
+}
+
+extern "C" int dal_gram_sym_residual(const uint16_t* ops, int64_t nb_active, int64_t row_block0, int64_t n_row_blocks,
+                                     int64_t d_pad, int64_t* acc, void* ws, size_t ws_bytes, dal_stream_t stream) {
+  if (!ops || !acc || !ws) return DAL_ERR_ARG;
+  if (nb_active <= 0 || row_block0 < 0 || n_row_blocks <= 0 || ((row_block0 | n_row_blocks | nb_active) & 1))
+    return DAL_ERR_SHAPE;
+  if (d_pad != dal_pad_features(d_pad) || (reinterpret_cast<uintptr_t>(ops) & 15) ||
+      (reinterpret_cast<uintptr_t>(ws) & 255))
+    return DAL_ERR_SHAPE;
+  const int64_t na = nb_active / 2, s0 = row_block0 / 2;
+  int64_t ns = n_row_blocks / 2;
+  if (s0 >= na) return DAL_OK;
+  if (s0 + ns > na) ns = na - s0;  // padding super blocks past the pool hold no rows
+  const ResidualLayout L = residual_layout(na, n_row_blocks / 2, d_pad);
+  if (ws_bytes < L.total) return DAL_ERR_SHAPE;
+  hipStream_t st = as_stream(stream);
+  unsigned char* w = static_cast<unsigned char*>(ws);
+  long long* sig_u = reinterpret_cast<long long*>(w + L.sig_u);
+  long long* sig_l = reinterpret_cast<long long*>(w + L.sig_l);
+  double* rb = reinterpret_cast<double*>(w + L.rb);
+  double* cb = reinterpret_cast<double*>(w + L.cb);
+  const int ks = split_ks(d_pad);
+  const int64_t ldh = 2 * d_pad;
+  if (hipMemsetAsync(sig_u, 0, static_cast<size_t>(na * d_pad) * 8, st) != hipSuccess) return DAL_ERR_HIP;
+  hipLaunchKernelGGL(csym_sigma_kernel,
+                     dim3(static_cast<unsigned>(na), static_cast<unsigned>(ceil_div(ldh / 8, 256))), dim3(256), 0, st,
+                     ops, ldh, ks, static_cast<int>(d_pad), sig_u, sig_l);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  hipLaunchKernelGGL(csym_scan_kernel, dim3(static_cast<unsigned>(ceil_div(d_pad, 64))), dim3(512), 0, st, sig_u,
+                     sig_l, static_cast<int>(na), static_cast<int>(d_pad), static_cast<int>(s0),
+                     static_cast<int>(s0 + ns), rb, cb);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  const int64_t n_rows = ns * kSB;
+  hipLaunchKernelGGL(csym_residual_kernel, dim3(static_cast<unsigned>(ceil_div(n_rows, 4))), dim3(256), 0, st,
+                     ops + s0 * kSB * ldh, ldh, ks, static_cast<int>(d_pad), static_cast<int>(s0),
+                     static_cast<int>(n_rows), rb, cb, reinterpret_cast<long long*>(acc));
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}

@@ -61,14 +61,14 @@ SIGNATURES = {
     "dal_split_f16": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p]),
     "dal_prep_split": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64, c_int64,
                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "dal_gram_rowsum_split": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_void_p, c_int,
-                                      c_void_p]),
-    "dal_density_error_bound_split": (c_double, [c_int64]),
     "dal_density_error_bound_sym": (c_double, [c_int64]),
     "dal_gram_rowsum_sym": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64, c_int64,
                                     c_int64, c_int64, c_void_p, c_int, c_void_p]),
     "dal_gram_rowsum_sym_skip": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64, c_int64,
                                          c_int64, c_int64, c_int64, c_int64, c_void_p, c_int, c_void_p]),
+    "dal_gram_sym_residual_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
+    "dal_gram_sym_residual": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p, c_void_p,
+                                      c_size_t, c_void_p]),
     "dal_forest_score": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32,
                                  c_int32, c_void_p, c_void_p, c_int, c_double, c_void_p, c_double,
                                  c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -159,6 +159,7 @@ class PoolState:
         self._acc_pre = None  # density accumulator already zeroed by the prep kernel
         self._ws_clean = {}   # (n, k, cap) -> workspace whose top-k header is zero (dal_dw_step)
         self.gram_events = None  # list -> (start, end) HIP events around each Gram call
+        self.residual_events = []  # (start, end) HIP events around each residual call (with gram_events)
         self.forest_events = None  # list -> (start, end) HIP events around each forest-score call
         self.select_events = None  # list -> (start, end) HIP events around each dal_dw_select call
         self.cap_scale = 1  # re-rank candidate capacity multiplier, kept after an overflow
@@ -224,7 +225,7 @@ class PoolState:
     def gram_operand(self, with_partials: bool = True, acc_zero=None):
         """The density GEMM's operand for this shard's rows: the fp32 unit rows
         (gram "f32") or their two-term fp16 split [n_pad, 2*d_pad] (gram
-        "split", dal_split_f16).  All-gathered as is in the multi-GPU path.
+        "sym", dal_prep_split).  All-gathered as is in the multi-GPU path.
         with_partials: the fused prep also writes the canonical column-sum
         partials (else they are left to colsum_partials()).  acc_zero: an
         int64 [n_pad] density accumulator to zero (by the prep kernel when it
@@ -235,7 +236,7 @@ class PoolState:
                 acc_zero.zero_()
             return u
         zeroed = False
-        if self._split is None:  # "split" and "sym" share the operand
+        if self._split is None:
             torch = _torch()
             self._split = torch.empty((self.n_pad, 2 * self.d_pad), dtype=torch.int16, device=self.device)
             if self._u is not None:
@@ -304,6 +305,8 @@ class PoolState:
             cols = op if u_cols is None else u_cols
             ncp = self.n_pad if n_cols_pad is None else int(n_cols_pad)
             self.gram_accumulate(acc, cols, ncp)
+            if self.gram == "sym":
+                self.gram_residual(acc, op)
             if u_cols is not None:
                 return acc
             self._density = acc
@@ -342,15 +345,37 @@ class PoolState:
                      _stream(self.device))
         elif skip is not None:
             raise ValueError("a skipped column range needs gram 'sym'")
-        elif self.gram == "f32":
-            call("dal_gram_rowsum", _ptr(op), self.n_pad, _ptr(cols), int(n_cols_pad), self.d_pad,
-                 self.d_pad, _ptr(acc), int(grid_blocks), _stream(self.device))
         else:
-            call("dal_gram_rowsum_split", _ptr(op), self.n_pad, _ptr(cols), int(n_cols_pad),
+            call("dal_gram_rowsum", _ptr(op), self.n_pad, _ptr(cols), int(n_cols_pad), self.d_pad,
                  self.d_pad, _ptr(acc), int(grid_blocks), _stream(self.device))
         if ev is not None:
             ev[1].record()
             self.gram_events.append(ev)
+        return acc
+
+    def gram_residual(self, acc, ops):
+        """Complete the compensated symmetric Gram (gram "sym"): add the exact
+        remainder of the H-only A side for this shard's rows into acc (global
+        row index).  ``ops``: the operand of EVERY active row (this pool's, or
+        the gathered one on several GPUs)."""
+        torch = _torch()
+        lib = _lib.load()
+        nb = self.nb_active()
+        rb0, nrb = self.row_base // 256, self.n_pad // 256
+        if rb0 >= nb or self.n == 0:
+            return acc
+        wsb = int(lib.dal_gram_sym_residual_workspace_bytes(nb, nrb, self.d_pad))
+        ws, wsp = workspace(wsb, self.device)
+        ev = None
+        if self.gram_events is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        call("dal_gram_sym_residual", _ptr(ops), nb, rb0, nrb, self.d_pad, _ptr(acc), wsp, wsb,
+             _stream(self.device))
+        if ev is not None:
+            ev[1].record()
+            self.residual_events.append(ev)
+        del ws
         return acc
 
     def events_off(self) -> bool:
@@ -420,15 +445,16 @@ class PoolState:
             raise _lib.DalError("truncated top-k level 1 overflowed and was not re-run")
 
 
-GRAM_KINDS = ("sym", "split", "f32")
+GRAM_KINDS = ("sym", "f32")
 
 
 def _gram_kind(gram) -> str:
     """Density GEMM kernel: "sym" (default; fp16 MFMA on the two-term split,
-    three products, each symmetric block pair once), "split" (same arithmetic,
-    every block pair) or "f32" (fp32 MFMA).  DAL_GRAM in the environment
-    overrides the default.  All are within their rigorous bound of the
-    canonical density and give the same (bit-exact) selection."""
+    each symmetric block pair once, H-only taker side + exact closed-form
+    remainder) or "f32" (fp32 MFMA on the unit rows, every pair: the
+    plain-precision reference kernel).  DAL_GRAM in the environment overrides
+    the default.  Both are within their rigorous bound of the canonical
+    density and give the same (bit-exact) selection."""
     import os
 
     g = gram if gram is not None else os.environ.get("DAL_GRAM", "sym")
@@ -440,7 +466,7 @@ def _gram_kind(gram) -> str:
 def gram_products(state: PoolState) -> int:
     """fp16 MFMA products per feature pair of the pool's Gram kernel (bench
     roofline: executed vs algorithmic flops)."""
-    return 3 if state.gram in ("sym", "split") else 1
+    return 2 if state.gram == "sym" else 1
 
 
 def _as_index(idx, device):
@@ -531,15 +557,13 @@ def topk_keys(keys, k: int, idx_base: int = 0):
 
 
 def density_error(state: PoolState) -> float:
-    """Bound on |d_gemm - d_canonical| (rigorous; dal_density_error_bound,
-    _split or _sym, by the pool's Gram kernel)."""
+    """Bound on |d_gemm - d_canonical| (rigorous; dal_density_error_bound or
+    _sym, by the pool's Gram kernel)."""
     n_cols = max(state.n_total - state.n_excluded_global(), 1)
     lib = _lib.load()
     if state.gram == "f32":
         return float(lib.dal_density_error_bound(n_cols))
-    if state.gram == "sym":
-        return float(lib.dal_density_error_bound_sym(n_cols))
-    return float(lib.dal_density_error_bound_split(n_cols))
+    return float(lib.dal_density_error_bound_sym(n_cols))
 
 
 def candidate_cap(n: int, k: int) -> int:

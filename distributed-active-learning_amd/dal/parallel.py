@@ -12,8 +12,9 @@ remainder).  Two exchanges, both all-gathers over ``torch.distributed``
 
   1. the shards' Gram operands (fp16 split [shard, 2*d_pad] by default, or
      fp32 unit rows) and the canonical fp64 column-sum partials -> every rank
-     holds U (the density needs every column) -- replaces the BlockMatrix
-     shuffle.  The operand all-gather runs asynchronously on RCCL's stream
+     holds U (the density needs every column; the symmetric kernel's
+     closed-form remainder needs every super block's row sums) -- replaces
+     the BlockMatrix shuffle.  The operand all-gather runs asynchronously on RCCL's stream
      while each rank multiplies its rows by its OWN shard's columns (CUs
      reserved for RCCL), then by the rest (ShardedSelector.exchange_density);
   2. each rank's exact local top-k (key, index, score) -> an identical
@@ -191,6 +192,8 @@ class ShardedSelector:
                 for c0, c1 in other_column_ranges(self.rank, self.world, self.shard):
                     st.gram_accumulate(acc, u_full[c0:c1], c1 - c0, col_row0=c0)
         if st.gram == "sym":
+            if st.n:  # the compensation's closed-form remainder of this rank's rows
+                st.gram_residual(acc, u_full)
             acc = comm.reduce_scatter_sum(acc)
         self.set_density(acc)
         return u_full, parts_full
@@ -207,6 +210,8 @@ class ShardedSelector:
         acc = self._new_acc()
         if self.state.n:
             self.state.gram_accumulate(acc, u_full, int(u_full.shape[0]), col_row0=0)
+            if self.state.gram == "sym":
+                self.state.gram_residual(acc, u_full)
         return acc
 
     def set_density(self, acc_local):

@@ -142,19 +142,13 @@ int dal_gram_rowsum(const float* u_rows, int64_t n_rows_pad, const float* u_cols
                     int64_t n_cols_pad, int64_t d_pad, int64_t ld, int64_t* acc,
                     int grid_blocks, dal_stream_t stream);
 
-/* ---- (a2-a4) the same row-sum on fp16 MFMA with a two-term split ------
- * Same contract and replaced reference lines as dal_gram_rowsum, at the fp16
- * matrix-core rate.  dal_split_f16 writes each normalised fp32 row u (from
+/* ---- (a2-a4) the same row-sum on fp16 MFMA: symmetric + compensated -------
+ * Same replaced reference lines as dal_gram_rowsum, at the fp16 matrix-core
+ * rate.  dal_split_f16 writes each normalised fp32 row u (from
  * dal_normalize_rows, ld >= d_pad) at scale 2^12 as H = fp16(2^12 u),
  * L = fp16(2^12 u - H) (RNE) in the layout [n_pad][d_pad / KS][KS H halves |
- * KS L halves], KS = 32 if d_pad == 32 else 64 (dal_split_f16_halves(n_pad,
- * d_pad) halves in all); dal_gram_rowsum_split then accumulates
- * acc[i] += round(sum_j <u_i,u_j> * 2^32) from three v_mfma_f32_16x16x32_f16
- * products (H.H, H.L, L.H, all in units of 2^-24) per 32 features, folded
- * exactly per 256-column group (bit-identical for any grid,
- * column split or GPU count).  Rigorous bound: dal_density_error_bound_split.
- * n_rows_pad % 256 == 0, n_cols_pad % 512 == 0; grid_blocks <= 0 selects
- * two blocks per CU. */
+ * KS L halves], KS = 128 if d_pad % 128 == 0, 32 if d_pad == 32, else 64
+ * (dal_split_f16_halves(n_pad, d_pad) halves in all). */
 int64_t dal_split_f16_halves(int64_t n_pad, int64_t d_pad);
 int dal_split_f16(const float* u, int64_t n_pad, int64_t d_pad, int64_t ld, uint16_t* out,
                   dal_stream_t stream);
@@ -168,39 +162,46 @@ int dal_split_f16(const float* u, int64_t n_pad, int64_t d_pad, int64_t ld, uint
 int dal_prep_split(const float* x, int64_t n, int64_t d, int64_t ldx, const uint8_t* row_flags,
                    int64_t n_pad, int64_t d_pad, uint16_t* out, double* norm64, double* partials,
                    int64_t* acc_zero, int32_t* dev_status, dal_stream_t stream);
-int dal_gram_rowsum_split(const uint16_t* rows, int64_t n_rows_pad, const uint16_t* cols,
-                          int64_t n_cols_pad, int64_t d_pad, int64_t* acc, int grid_blocks,
-                          dal_stream_t stream);
-double dal_density_error_bound_split(int64_t n_cols);
-/* Symmetric (SYRK-style) form of dal_gram_rowsum_split: S = U U^T is
- * symmetric, so each unordered pair of 256-row blocks {I, J} is multiplied
- * once and gives the row sums of S_IJ (-> acc rows of I) and its column sums
- * (-> acc rows of J): half the MFMA work.  Row block I takes column block J
- * iff J == I, or J > I and I+J even, or J < I and I+J odd (global block
- * indices, so the bits do not depend on the sharding).  rows: the operand of
- * global row blocks [row_block0, row_block0 + n_row_blocks); cols: the operand
- * whose first block is global block col_block0; only column blocks
- * [j_lo, j_hi) are processed (j_hi <= nb_active = pad512(N_total) / 256), so
- * a caller can split the columns over several calls.  acc is indexed by
- * GLOBAL row (>= nb_active * 256 entries, zeroed by the caller); on several
- * GPUs the per-rank accs are summed (reduce-scatter).  Per 16x16 tile the
- * three products share one fp32 accumulator; the row sums ride in two MFMA
- * accumulator chains per pair (even / odd column tiles) and a tile's column
- * sums are the growth of its chain's lane total.  Each pair's sums are rounded
- * to multiples of 2^-32 and added exactly (int64), so the bits do not depend on
- * the grid, the column split or the GPU count.  Rigorous bound on
- * |d - d_canonical|: dal_density_error_bound_sym. */
+/* Symmetric (SYRK-style), compensated Gram row-sum (ABI v5).  S = U U^T is
+ * symmetric: rows are grouped in 512-row super blocks (pairs of 256-row
+ * blocks) and each unordered pair {P, Q} is multiplied once, giving the row
+ * sums of S_PQ (-> acc rows of P) and its column sums (-> acc rows of Q).
+ * P takes Q iff Q == P, or Q > P and P+Q even, or Q < P and P+Q odd (global
+ * indices, so the bits do not depend on the sharding).  The taker's side is
+ * H only: per 32 features two v_mfma_f32_16x16x32_f16 (H.H, H.L) form
+ * <H_i, H_j + L_j>; the exact remainder sum <L_i, H_j + L_j> of every taken
+ * pair is added in closed form by dal_gram_sym_residual -- acc holds the
+ * density only after BOTH (any order; integer adds).  rows: the operand of
+ * global 256-row blocks [row_block0, row_block0 + n_row_blocks) (even
+ * counts); cols: the operand whose first block is global block col_block0;
+ * column blocks [j_lo, j_hi) minus [skip_lo, skip_hi) are processed (j_hi <=
+ * nb_active = pad512(N_total) / 256), so a caller can split the columns over
+ * several calls.  acc is indexed by GLOBAL row (>= nb_active * 256 entries,
+ * zeroed by the caller); on several GPUs the per-rank accs are summed
+ * (reduce-scatter).  Chains are folded to multiples of 2^-32 and added
+ * exactly (int64): the bits do not depend on the grid, the column split or
+ * the GPU count.  Rigorous bound on |d - d_canonical| of the completed
+ * density: dal_density_error_bound_sym. */
 int dal_gram_rowsum_sym(const uint16_t* rows, int64_t row_block0, int64_t n_row_blocks,
                         const uint16_t* cols, int64_t col_block0, int64_t j_lo, int64_t j_hi,
                         int64_t nb_active, int64_t d_pad, int64_t* acc, int grid_blocks,
                         dal_stream_t stream);
-/* The same, skipping column blocks [skip_lo, skip_hi) (already processed, e.g.
- * a GPU's own shard run beside the operand all-gather): one launch for all
- * the other columns.  Row blocks must be even (512-row super blocks). */
 int dal_gram_rowsum_sym_skip(const uint16_t* rows, int64_t row_block0, int64_t n_row_blocks,
                              const uint16_t* cols, int64_t col_block0, int64_t j_lo, int64_t j_hi,
                              int64_t skip_lo, int64_t skip_hi, int64_t nb_active, int64_t d_pad,
                              int64_t* acc, int grid_blocks, dal_stream_t stream);
+/* The compensation term of dal_gram_rowsum_sym for the rows of global blocks
+ * [row_block0, row_block0 + n_row_blocks) (even), ADDED into acc (global
+ * row index): acc[r] += rint(2^32 * (<L_r, R_B> + <H_r + L_r, C_B>)), B = r's
+ * super block, R_B = sum over the super blocks B takes of their (H + L) row
+ * sums, C_B = sum over the other super blocks that take B of their L row sums
+ * (exact int64 sums in units of 2^-24; fp64 dots in a fixed order).  ops: the
+ * operand of EVERY active row (nb_active * 256 rows: the gathered operand on
+ * several GPUs).  Three launches, O(N * D); workspace from
+ * dal_gram_sym_residual_workspace_bytes (256-byte aligned). */
+size_t dal_gram_sym_residual_workspace_bytes(int64_t nb_active, int64_t n_row_blocks, int64_t d_pad);
+int dal_gram_sym_residual(const uint16_t* ops, int64_t nb_active, int64_t row_block0, int64_t n_row_blocks,
+                          int64_t d_pad, int64_t* acc, void* ws, size_t ws_bytes, dal_stream_t stream);
 double dal_density_error_bound_sym(int64_t n_cols);
 
 /* ---- (a5-a10) forest votes + uncertainty / density-weighted score ------

@@ -1,12 +1,12 @@
 """Pin the round-1 race fix in the emitted gfx950 ISA (no GPU needed).
 
-The symmetric Gram kernel (gram_sym2_kernel, csrc/gram_split.hip) flushes
+The symmetric Gram kernel (gram_csym_kernel, csrc/gram_sym.hip) flushes
 LDS fp64 row/column partials that other waves add with no-return ds_add_f64.
 hipcc once emitted no lgkmcnt wait at a loop-top __syncthreads, and another
 wave's flush read a column partial before the add landed (a lost partial,
 seen once at 500k x 256).  The fix puts `s_waitcnt vmcnt(0) lgkmcnt(0)` in
 front of every barrier; this test disassembles libdal.so's gfx950 code object
-and asserts that, for every s_barrier of every gram_sym2_kernel instance (and
+and asserts that, for every s_barrier of every gram_csym_kernel instance (and
 of the max-cosine kernels, which use the same LDS-DMA ring pattern), the
 nearest preceding wait on the LDS counter is lgkmcnt(0) and no LDS
 instruction sits between it and the barrier.  A compiler change that drops
@@ -83,8 +83,8 @@ def _check(body):
 
 def test_every_gram_barrier_waits_for_lds():
     funcs = _functions(_disassemble())
-    grams = {k: v for k, v in funcs.items() if "gram_sym2_kernel" in k}
-    assert grams, "gram_sym2_kernel not found in libdal.so"
+    grams = {k: v for k, v in funcs.items() if "gram_csym_kernel" in k}
+    assert len(grams) == 3, "gram_csym_kernel<32|64|128> not found in libdal.so"
     for name, body in grams.items():
         n, bad = _check(body)
         assert n > 0, name

@@ -36,17 +36,17 @@ def test_library_exports_every_header_symbol():
 
 def test_host_helpers():
     lib = _lib.load()
-    assert lib.dal_abi_version() == 4
+    assert lib.dal_abi_version() == 5
     assert lib.dal_pad_rows(1) == 512 and lib.dal_pad_rows(100000) == 100352
     assert [lib.dal_pad_features(d) for d in (1, 30, 33, 64, 65, 128, 129, 256, 500, 784)] == \
         [32, 32, 64, 64, 128, 128, 256, 256, 512, 1024]
     assert lib.dal_status_string(-2).decode().startswith("shape")
     b = lib.dal_density_error_bound(100000)
     assert 1.0 < b < 10.0  # ~3.1e-5 * N
-    bs = lib.dal_density_error_bound_split(100000)
-    assert b < bs < 20.0  # ~1.25e-4 * N (conservative MFMA accumulation model)
     bsym = lib.dal_density_error_bound_sym(100000)
-    assert bs < bsym < 30.0  # ~2.1e-4 * N (chained accumulators: longer fp32 chains)
+    assert b < bsym < 20.0  # ~1.25e-4 * N (chains of <= 1,024 fp32 adds, conservative MFMA model)
+    assert lib.dal_gram_sym_residual_workspace_bytes(392, 392, 64) == 2 * 196 * 64 * 8 + 2 * 196 * 64 * 8
+    assert lib.dal_gram_sym_residual_workspace_bytes(0, 2, 64) == 0
     assert lib.dal_split_f16_halves(512, 64) == 512 * 128
     assert lib.dal_topk_workspace_bytes(1 << 21, 1000) > 0
 
@@ -62,10 +62,13 @@ def test_host_argument_validation_without_gpu():
     assert lib.dal_gram_rowsum(p, 100, p, 512, 64, 64, p, 0, None) == -2
     assert lib.dal_gram_rowsum(p, 256, p, 500, 64, 64, p, 0, None) == -2
     assert lib.dal_gram_rowsum(p, 256, p, 512, 48, 64, p, 0, None) == -2
-    assert lib.dal_gram_rowsum_split(None, 256, None, 512, 64, None, 0, None) == -1
-    assert lib.dal_gram_rowsum_split(p, 100, p, 512, 64, p, 0, None) == -2
-    assert lib.dal_gram_rowsum_split(p, 256, p, 500, 64, p, 0, None) == -2
-    assert lib.dal_gram_rowsum_split(p, 256, p, 512, 48, p, 0, None) == -2
+    assert lib.dal_gram_rowsum_sym_skip(None, 0, 2, p, 0, 0, 2, 0, 0, 2, 64, p, 0, None) == -1
+    assert lib.dal_gram_rowsum_sym_skip(p, 0, 3, p, 0, 0, 2, 0, 0, 4, 64, p, 0, None) == -2  # odd row blocks
+    assert lib.dal_gram_rowsum_sym_skip(p, 0, 2, p, 0, 0, 6, 0, 0, 4, 64, p, 0, None) == -2  # j_hi > nb_active
+    assert lib.dal_gram_rowsum_sym_skip(p, 0, 2, p, 0, 0, 2, 0, 0, 2, 48, p, 0, None) == -2  # d_pad
+    assert lib.dal_gram_sym_residual(None, 2, 0, 2, 64, p, p, 1 << 20, None) == -1
+    assert lib.dal_gram_sym_residual(p, 2, 1, 2, 64, p, p, 1 << 20, None) == -2   # odd block
+    assert lib.dal_gram_sym_residual(p, 2, 0, 2, 64, p, p, 16, None) == -2        # workspace too small
     assert lib.dal_split_f16(None, 512, 64, 64, None, None) == -1
     assert lib.dal_split_f16(p, 500, 64, 64, p, None) == -2
     assert lib.dal_topk(p, 10, 11, 0, p, 1 << 20, p, p, None) == -2
