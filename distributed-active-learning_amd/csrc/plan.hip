@@ -240,6 +240,28 @@ extern "C" int dal_dw_plan_run(dal_dw_plan_t* p, const int64_t* unl, int64_t n_u
   return DAL_OK;
 }
 
+extern "C" int dal_dw_plan_launch(dal_dw_plan_t* p, const int64_t* unl, int64_t n_unl, dal_stream_t stream) {
+  if (!p || (!unl && n_unl)) return DAL_ERR_ARG;
+  hipStream_t st = as_stream(stream);
+  const DeviceGuard guard(st);
+  if (!guard.ok() || guard.device() != p->device) return DAL_ERR_ARG;
+  const uint32_t step = ++p->step;
+  hipKernelNodeParams np = p->mark_params;
+  int64_t row_base = p->row_base, n = p->n;
+  uint32_t* stamp = p->stamp;
+  uint32_t* step_dev = p->stamp + p->n;
+  void* kargs[7] = {&unl, &n_unl, const_cast<uint32_t*>(&step), &row_base, &n, &stamp, &step_dev};
+  np.kernelParams = kargs;
+  np.extra = nullptr;
+  if (hipGraphExecKernelNodeSetParams(p->exec, p->mark_node, &np) != hipSuccess) return DAL_ERR_HIP;
+  volatile PlanSlot* slot = p->slot;
+  slot->out[0] = nullptr;  // no publishing: the outputs stay in the plan's static buffers
+  slot->out[1] = nullptr;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  if (hipGraphLaunch(p->exec, st) != hipSuccess) return DAL_ERR_HIP;
+  return DAL_OK;
+}
+
 extern "C" void dal_dw_plan_destroy(dal_dw_plan_t* p) {
   if (!p) return;
   if (p->timing && p->runs)

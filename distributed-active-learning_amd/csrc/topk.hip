@@ -891,6 +891,7 @@ __global__ __launch_bounds__(256) void publish_kernel(const int64_t* __restrict_
 // false (nothing written) when the bucket never shrinks that far (many equal
 // keys): the caller sorts everything.  Block-uniform.
 constexpr int64_t kSelMin = 1024;    // below this the full bitonic is cheap
+constexpr int64_t kRankMax = 512;    // at most this many: rank selection, no sorting network
 constexpr int64_t kSelMaxK = 1536;   // k + kSelSmall must fit the sort arrays
 constexpr int kSelSmall = 512;
 
@@ -1015,6 +1016,55 @@ __global__ __launch_bounds__(kSortThreads) void sort_kernel(const uint64_t* __re
   // below its bucket plus the bucket itself (<= kSelSmall) are sorted -- the
   // full bitonic over 4,096 keys is LDS-bound (~95 us).  Same result: every
   // key of the top k lies in the sorted subset.
+  if (m <= kRankMax) {
+    // short lists (the common case: ~100-300 candidates): rank selection.  The
+    // (key, index) pairs are distinct, so every element's rank -- the count of
+    // smaller pairs, read as LDS broadcasts -- is its output position: two
+    // barriers instead of the bitonic network's log^2 m stages.
+    for (int i = tid; i < m; i += kSortThreads) {
+      sk[i] = keys[i];
+      si[i] = idx[i];
+      if (PAY) sp[i] = pay[i];
+    }
+    __syncthreads();
+    if (tail.clear) {  // every thread read the header above
+      for (int64_t w = tid; w < tail.clear_words; w += kSortThreads) tail.clear[w] = 0u;
+    }
+    int64_t* const di = s_dest[0];
+    double* const ds = reinterpret_cast<double*>(s_dest[1]);
+    const int64_t kk = k < m ? k : m;
+    for (int e = tid; e < m; e += kSortThreads) {
+      const unsigned long long ke = sk[e];
+      const long long ie = si[e];
+      int r = 0;
+#pragma unroll 4
+      for (int j = 0; j < m; ++j) {
+        const unsigned long long kj = sk[j];
+        r += kj < ke || (kj == ke && si[j] < ie);
+      }
+      if (r < kk) {
+        if (out_keys) out_keys[r] = ke;
+        out_idx[r] = ie;
+        if (PAY && out_pay) out_pay[r] = sp[e];
+        if (di) di[r] = ie;
+        if (PAY && ds) ds[r] = sp[e];
+      }
+    }
+    if (PAY && h) {
+      for (int64_t i = kk + tid; i < k; i += kSortThreads) {
+        if (out_keys) out_keys[i] = DAL_KEY_NONE;
+        out_idx[i] = -1;
+        if (out_pay) out_pay[i] = __builtin_nan("");
+        if (di) di[i] = -1;
+        if (ds) ds[i] = __builtin_nan("");
+      }
+    }
+    if (tail.status_mirror) {
+      __syncthreads();
+      if (tid == 0) publish_status(tail.status, tail.status_mirror);
+    }
+    return;
+  }
   bool loaded = false;
   if (PAY && h && m > kSelMin && k <= kSelMaxK && k < m) loaded = select_compact(keys, idx, pay, m, k, sk, si, sp, m);
   int mp = 2;

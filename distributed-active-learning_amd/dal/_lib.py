@@ -92,6 +92,7 @@ SIGNATURES = {
                                    c_void_p, c_int64, c_int64, c_int32, c_void_p, c_size_t, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "dal_dw_plan_run": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "dal_dw_plan_launch": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
     "dal_dw_plan_destroy": (None, [c_void_p]),
     "dal_maxcos_label_rows_granule": (c_int64, [c_int64]),
     "dal_maxcos_error_bound": (c_double, [c_int64]),

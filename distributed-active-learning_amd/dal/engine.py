@@ -810,7 +810,12 @@ class WarmStepGraph:
     copies the selection out and reads the status word.  A different forest
     is copied into the static heap arrays first."""
 
-    def __init__(self, state: PoolState, forest: Forest, k: int, beta: float, cap: int, passes: int):
+    def __init__(self, state: PoolState, forest: Forest, k: int, beta: float, cap: int, passes: int,
+                 colsum=None, packed=None):
+        """colsum: the canonical column sum to re-rank against (default the
+        pool's own; a shard passes the global one).  packed: an int64 [3k+1]
+        row receiving (selected keys | indices | score bits | status) -- the
+        multi-GPU top-k all-gather row -- instead of the plan's own buffers."""
         import ctypes
 
         torch = _torch()
@@ -827,21 +832,32 @@ class WarmStepGraph:
         self.scores = torch.empty(n, dtype=torch.float64, device=dev)
         self.keys_lo = torch.empty(n, dtype=torch.int64, device=dev)
         self.keys_hi = torch.empty(n, dtype=torch.int64, device=dev)
-        # selected indices and scores side by side: one copy hands them out
-        self.out_pair = torch.empty(2 * k, dtype=torch.int64, device=dev)
-        self.out_keys = torch.empty(k, dtype=torch.int64, device=dev)
+        self.packed = packed
+        if packed is None:
+            # selected indices and scores side by side: one copy hands them out
+            self.out_pair = torch.empty(2 * k, dtype=torch.int64, device=dev)
+            self.out_keys = torch.empty(k, dtype=torch.int64, device=dev)
+            status = state.status
+        else:
+            if packed.dtype != torch.int64 or tuple(packed.shape) != (3 * k + 1,) or not packed.is_contiguous():
+                raise ValueError("packed must be a contiguous int64 [3k+1] tensor")
+            packed.zero_()  # the status slot's upper half stays zero
+            self.out_keys, self.out_pair = packed[:k], packed[k:3 * k]
+            status = packed[3 * k:].view(torch.int32)[:1]  # low half of the last word (little endian)
+        self.status = status
         self._last = None  # weak reference to the Selection that still reads votes / scores
         lib = _lib.load()
         self.wsb = int(lib.dal_dw_step_workspace_bytes(n, k, cap))
         self.ws, self.wsp = workspace(self.wsb, dev)
-        self._keep = (state.density_fixed(), state.colsum(), state.norms(), state.flags, state.x)
+        self._keep = (state.density_fixed(), state.colsum() if colsum is None else colsum, state.norms(),
+                      state.flags, state.x)
         dens, colsum, norm64 = self._keep[:3]
         plan = ctypes.c_void_p()
         call("dal_dw_plan_create", _ptr(state.x), n, state.d, state.d, _ptr(self.inner), _ptr(self.leaf),
              self.n_trees, self.depth, _ptr(self.lut), _ptr(dens), float(density_error(state)), _ptr(state.flags),
              _ptr(self.flags), float(beta), state.row_base, _ptr(norm64), _ptr(colsum), k, cap, passes, self.wsp,
              self.wsb, _ptr(self.votes), _ptr(self.scores), _ptr(self.keys_lo), _ptr(self.keys_hi),
-             _ptr(self.out_pair), _ptr(self.out_keys), _ptr(state.status), _stream(dev), ctypes.byref(plan))
+             _ptr(self.out_pair), _ptr(self.out_keys), _ptr(status), _stream(dev), ctypes.byref(plan))
         self.plan = plan
         self._status = ctypes.c_int32()
         self._status_ref = ctypes.byref(self._status)
@@ -871,6 +887,16 @@ class WarmStepGraph:
         if rc:
             _lib.check(rc, "dal_dw_plan_run")
         return self.votes, self.scores, idx, sc, self._status.value
+
+    def launch(self, forest: Forest, unl):
+        """Refresh and replay on the current stream WITHOUT waiting (the
+        outputs land in ``packed``); the caller reads the status later."""
+        if forest is not self.forest_ref:
+            inner, leaf = forest.device(self.state.device)
+            self.inner.copy_(inner)
+            self.leaf.copy_(leaf)
+            self.forest_ref = forest
+        call("dal_dw_plan_launch", self.plan, unl.data_ptr(), int(unl.shape[0]), _raw_stream(self.state.device))
 
 
 def _density_step_graph(state: PoolState, unl, forest: Forest, kk: int, beta: float) -> Selection:

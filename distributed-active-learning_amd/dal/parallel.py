@@ -101,6 +101,8 @@ class ShardedSelector:
                                n_total=self.n_total, n_pad=self.shard, gram=gram)
         self._density = None
         self._parts_full = None  # all ranks' canonical column-sum partials (cached with the density)
+        self._colsum = None      # the global canonical column sum reduced from them (cached)
+        self._plans = {}         # warm-step plans by (T, depth, k, beta, cap, level-1 passes)
         self.cap_scale = 1      # re-rank candidate capacity multiplier (grown on overflow)
 
     def index_tensor(self, unlabeled_idx):
@@ -128,6 +130,39 @@ class ShardedSelector:
         self.state.clear_caches()
         self._density = None
         self._parts_full = None
+        self._colsum = None
+        self._plans = {}
+
+    def global_colsum(self, partials_full):
+        """The canonical column sum s = sum_{j not in E} u_j over EVERY rank's
+        rows, reduced once from the gathered partials and cached (a warm-step
+        plan captures its address)."""
+        if self._colsum is None or partials_full is not self._parts_full:
+            cs = self.state.colsum(partials_full)
+            if partials_full is not self._parts_full:
+                return cs
+            self._colsum = cs
+        return self._colsum
+
+    def warm_plan(self, forest, k: int, beta: float):
+        """This rank's warm local step (density cached) as a dal_dw_plan whose
+        outputs land in one packed row [keys k | indices k | score bits k |
+        status]: launched without a host wait, all-gathered and merged
+        stream-ordered (engine.WarmStepGraph with ``packed``)."""
+        from .engine import WarmStepGraph, candidate_cap, level1_passes
+
+        torch = __import__("torch")
+        st = self.state
+        base = candidate_cap(st.n, k) if st.cap_base is None else max(int(k), int(st.cap_base))
+        cap = int(min(st.n, base * self.cap_scale))
+        passes = level1_passes(st, st.n, k, cap)
+        key = (forest.n_trees, forest.depth, int(k), float(beta), cap, passes)
+        g = self._plans.get(key)
+        if g is None:
+            packed = torch.empty(3 * int(k) + 1, dtype=torch.int64, device=st.device)
+            g = self._plans[key] = WarmStepGraph(st, forest, int(k), beta, cap, passes,
+                                                 colsum=self.global_colsum(self._parts_full), packed=packed)
+        return g
 
     # ---- phase A: local normalisation + canonical partials ------------
     def prep(self):
@@ -249,7 +284,7 @@ class ShardedSelector:
         # they fill the local list last and never survive a merge that has k
         kk = min(k, st.n)
         if mode == "dw" and density_mode == "separable":
-            colsum = st.colsum(partials_full)
+            colsum = self.global_colsum(partials_full)
             lut_dev = device_lut("entropy", forest.n_trees, st.device)
             votes, sc, kys, _ = forest_score(st, forest, lut_dev, flags, DAL_DESCENDING,
                                              density=st.density_exact(colsum), beta=beta)
@@ -257,7 +292,7 @@ class ShardedSelector:
             s = sc[i - st.row_base]
         elif mode == "dw":
             dens = self.local_density(u_full)
-            colsum = st.colsum(partials_full)
+            colsum = self.global_colsum(partials_full)
             lut_dev = device_lut("entropy", forest.n_trees, st.device)
             if st.events_off():  # one fused call (dal_dw_step), as the single-GPU step
                 _, _, i, s, kk_keys = dw_step_local(st, forest, flags, dens, lut_dev, kk, beta, colsum,
@@ -395,12 +430,24 @@ def select(sel: ShardedSelector, comm, unlabeled_idx, forest, k: int, mode: str 
             else:
                 parts_full = comm.all_gather(parts)
             sel._parts_full = parts_full
+            sel._colsum = None  # derived from the partials, as the plans' captured column sum
+            sel._plans = {}
         parts_full = sel._parts_full
+    n_unl_global = int(unl.shape[0])  # single source of truth for the candidate count
+    stt = getattr(sel, "state", None)  # (the CPU tests' oracle shards have none)
+    if (stt is not None and mode == "dw" and density_mode == "gram" and u_full is None
+            and sel._density is not None and sort_fn is hip_sort_positions and sel.world * k <= _lib.DAL_SORT_CAP and stt.use_graphs
+            and stt.events_off() and stt.n >= k and unl.is_cuda):
+        # warm step (density cached): the local step is one plan replay whose
+        # outputs ARE the packed all-gather row; no host wait before the merge
+        plan = sel.warm_plan(forest, k, beta)
+        plan.launch(forest, unl)
+        out, st = merge_row(comm, plan.packed, k, all_valid=n_unl_global >= k)
+        return _finish(sel, comm, unlabeled_idx, forest, k, mode, strategy, beta, sort_fn, density_mode, out, st)
     top = sel.local_select(u_full, parts_full, unl, forest, k, mode, strategy, beta, density_mode)
     # every rank's status word (zero-norm rows, re-rank capacity overflow)
     # rides in the top-k all-gather and is read once, after the merge is
     # queued: the step's one host sync, and every rank sees the same bits
-    n_unl_global = int(unl.shape[0])  # single source of truth for the candidate count
     if sort_fn is hip_sort_positions and sel.world * k <= _lib.DAL_SORT_CAP and top.keys.is_cuda:
         out, st = merge_packed(comm, top, sel.status_word(), k, all_valid=n_unl_global >= k)
     else:
@@ -409,6 +456,11 @@ def select(sel: ShardedSelector, comm, unlabeled_idx, forest, k: int, mode: str 
         st = 0
         for v in st_all.tolist():
             st |= int(v)
+    return _finish(sel, comm, unlabeled_idx, forest, k, mode, strategy, beta, sort_fn, density_mode, out, st)
+
+
+def _finish(sel, comm, unlabeled_idx, forest, k, mode, strategy, beta, sort_fn, density_mode, out, st):
+    """Act on the OR of every rank's status word (identical on all ranks)."""
     if mode != "dw":
         st &= ~_lib.DAL_FLAG_ZERO_NORM  # a zero row only matters to the cosine density
     if st & _lib.DAL_FLAG_ZERO_NORM:
@@ -447,11 +499,19 @@ def merge_packed(comm, top: LocalTopk, status, k: int, all_valid: bool = False):
     device).  Returns ((indices, scores), status) -- the status read is the
     step's one host sync."""
     torch = __import__("torch")
+    packed = torch.cat([top.keys, top.idx, top.scores.view(torch.int64), status.reshape(1).to(torch.int64)])
+    return merge_row(comm, packed, k, all_valid)
+
+
+def merge_row(comm, packed, k: int, all_valid: bool = False):
+    """All-gather this rank's packed row int64 [3k+1] (keys | indices | score
+    bits | status) and merge the rows with dal_topk_merge; returns ((indices,
+    scores), OR of the status words)."""
+    torch = __import__("torch")
     from .engine import _ptr, _stream
     from ._lib import call
 
-    dev = top.keys.device
-    packed = torch.cat([top.keys, top.idx, top.scores.view(torch.int64), status.reshape(1).to(torch.int64)])
+    dev = packed.device
     w = int(packed.shape[0])
     g = comm.all_gather(packed.reshape(1, w))  # [P, 3k + 1]
     n_ranks = int(g.shape[0])

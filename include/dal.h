@@ -323,6 +323,13 @@ int dal_dw_plan_create(const float* x, int64_t n, int64_t d, int64_t ldx, const 
                        dal_dw_plan_t** plan);
 int dal_dw_plan_run(dal_dw_plan_t* plan, const int64_t* unl, int64_t n_unl, int64_t* out_idx,
                     double* out_scores, int32_t* status, dal_stream_t stream);
+/* The plan's replay WITHOUT the host wait (ABI v5): refreshes the row marks,
+ * launches the graph on ``stream`` and returns.  The outputs stay in the
+ * buffers given at creation (out_keys, out_pair = selected indices | score
+ * bits, dev_status) -- e.g. one packed row [keys k | indices k | score bits
+ * k | status] that a multi-GPU caller all-gathers and merges stream-ordered,
+ * reading the status once after the merge. */
+int dal_dw_plan_launch(dal_dw_plan_t* plan, const int64_t* unl, int64_t n_unl, dal_stream_t stream);
 void dal_dw_plan_destroy(dal_dw_plan_t* plan);
 
 /* ---- (a12, config 5) max-cosine to a labeled set -----------------------

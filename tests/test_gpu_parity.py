@@ -748,6 +748,51 @@ def test_exchange_density_async_producer_bit_identical(cuda, world):
     assert np.array_equal(_np(sc), o_sc)
 
 
+class _OneRankComm:
+    """A world-size-1 communicator without a process group (gathers copy)."""
+
+    overlaps = False
+
+    def all_gather(self, t):
+        return t.clone()
+
+    def all_gather_start(self, t):
+        return t.clone(), None
+
+    def wait(self, work):
+        assert work is None
+
+    def reduce_scatter_sum(self, t):
+        return t
+
+
+def test_sharded_warm_plan_across_iterations(cuda):
+    """The sharded warm step as a per-rank plan (dal_dw_plan_launch: the
+    local step's outputs are the packed all-gather row, no host wait before
+    the merge) over AL iterations with a shrinking unlabeled set and a new
+    forest each time, against the oracle (density_weighting.py:133-176)."""
+    from dal import parallel
+    from dal.forest import Forest
+
+    n, d, k = 20_000, 64, 50
+    X = O.synthetic_pool(n, d, seed=77)
+    E = np.arange(10)
+    sel = parallel.ShardedSelector(X, n, 0, 1, excluded=E, device=cuda)
+    comm = _OneRankComm()
+    unl = np.arange(10, n)
+    dens = O.density_canonical(X, E)
+    for it in range(4):
+        F = Forest.synthetic(10, 4, d, seed=1 + it)
+        of = O.synthetic_forest(10, 4, d, seed=1 + it)
+        idx, sc = parallel.select(sel, comm, unl, F, k, mode="dw")
+        _, o_idx, o_sc = O.density_select(X, unl, of, k, 1.0, E, density=dens)
+        assert np.array_equal(_np(idx), o_idx), it
+        assert np.array_equal(_np(sc), o_sc), it
+        if it:
+            assert sel._plans, "warm steps must run through the plan"
+        unl = np.setdiff1d(unl, o_idx)
+
+
 # ------------------------------------------------ separable density -------
 @pytest.mark.parametrize("name", ["synthetic_512x64_T10.npz", "synthetic_4096x256_T10.npz",
                                   "synthetic_1500x30_T100.npz", "checkerboard2x2.npz"])
