@@ -70,6 +70,9 @@ struct TopkHdr {
   // one 64-bit atomic per block sweep
   unsigned long long packed;
   unsigned long long pad2;
+  // dw_level1_fused_kernel: grid-barrier arrival counters (one per radix
+  // pass) and the final arrival counter (the last block sorts)
+  unsigned int bar[kPasses + 2];
 };
 
 struct TopkLayout {
@@ -481,6 +484,7 @@ __device__ __forceinline__ bool dw_canonical_score_wave(const DwRerank& R, int64
 // the row's features fetched 64 at a time); e = lut[vote] passed in when the
 // LUT is held in lanes (n_lut > 0).  For waves with many candidates, where
 // one wave-wide pass per candidate would serialise them.
+template <int kChunk = 64>
 __device__ __forceinline__ bool dw_canonical_score_lane(const DwRerank& R, int64_t i, double& s, double e_in,
                                                         int n_lut) {
   const uint8_t fl = R.flags ? R.flags[i] : DAL_ROW_CANDIDATE;
@@ -491,7 +495,6 @@ __device__ __forceinline__ bool dw_canonical_score_lane(const DwRerank& R, int64
   const double nr = R.norm64[i];
   const float* xr = R.x + i * R.ldx;
   double acc = 0.0;
-  constexpr int kChunk = 64;
   int f0 = 0;
   for (; f0 + kChunk <= R.d; f0 += kChunk) {
     float xv[kChunk];
@@ -577,93 +580,6 @@ __global__ __launch_bounds__(kRadixThreads) void threshold_append_kernel(
     unsigned long long t = 0;
     for (int w = 0; w < kRadixThreads / 64; ++w) t += red[w];
     atomicAdd(&h->total_lt, t);
-  }
-}
-
-// dal_dw_step's candidate search + re-rank: one key per thread (block-uniform
-// grid-stride sweeps), the first keys and the LUT fetched before the level-1
-// state is resolved.  Per sweep the block reserves its candidate slots and
-// counts its rows under tau with ONE packed 64-bit atomic (TopkHdr::packed),
-// issued before the candidates are scored so its round trip overlaps them.
-// A wave with <= 2 candidates scores each with all 64 lanes
-// (dw_canonical_score_wave); with more, each lane scores its own
-// (dw_canonical_score_lane) -- the same operations in the same order either way.
-__global__ __launch_bounds__(kRadixThreads) void append_rerank_kernel(
-    const uint64_t* __restrict__ keys_lo, const uint64_t* __restrict__ keys_hi, int64_t n, int64_t idx_base,
-    int passes, TopkHdr* __restrict__ h, int64_t* __restrict__ cidx, int64_t cap, AppendRerank AR, int n_lut) {
-  constexpr int kWaves = kRadixThreads / 64;
-  __shared__ uint32_t scan[kWaves];
-  __shared__ unsigned s_wc[kWaves], s_wb[kWaves];
-  __shared__ unsigned long long s_old;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kRadixThreads;
-  int64_t b = static_cast<int64_t>(blockIdx.x) * kRadixThreads;
-  int64_t i = b + tid;
-  unsigned long long lo = i < n ? keys_lo[i] : DAL_KEY_NONE;
-  unsigned long long hi = i < n ? keys_hi[i] : DAL_KEY_NONE;
-  const double lut_lane = lane < n_lut ? AR.R.lut[lane] : 0.0;
-  unsigned long long prefix, krem;
-  resolve_digit(h, passes - 1, prefix, krem, scan);
-  const int sh = digit_shift(passes - 1);
-  const unsigned long long tau = prefix | (sh ? ((1ull << sh) - 1ull) : 0ull);
-  if (blockIdx.x == 0 && tid == 0) h->kstar = tau;
-  const unsigned long long lt_mask = (1ull << lane) - 1ull;
-  for (;;) {  // block-uniform
-    const bool valid = i < n;
-    const bool cand = valid && hi <= tau && hi != DAL_KEY_NONE;
-    const unsigned long long cm = __ballot(cand);
-    const unsigned long long bm = __ballot(valid && lo <= tau);
-    if (lane == 0) {
-      s_wc[w] = static_cast<unsigned>(__popcll(cm));
-      s_wb[w] = static_cast<unsigned>(__popcll(bm));
-    }
-    __syncthreads();
-    unsigned before = 0, tot_c = 0, tot_b = 0;
-#pragma unroll
-    for (int q = 0; q < kWaves; ++q) {
-      if (q < w) before += s_wc[q];
-      tot_c += s_wc[q];
-      tot_b += s_wb[q];
-    }
-    unsigned long long old = 0;
-    if (tid == 0 && (tot_c | tot_b))
-      old = atomicAdd(&h->packed, (static_cast<unsigned long long>(tot_b) << 32) | tot_c);
-    double my_s = 0.0;
-    bool my_ok = false;
-    if (cm) {
-      if (__popcll(cm) > 2) {
-        const int v = cand ? AR.R.votes[i] : 0;
-        const double e = n_lut ? __shfl(lut_lane, v) : 0.0;  // every lane active here
-        if (cand) my_ok = dw_canonical_score_lane(AR.R, i, my_s, e, n_lut);
-      } else {
-        for (unsigned long long t = cm; t;) {
-          const int l = __ffsll(static_cast<long long>(t)) - 1;
-          t &= t - 1;
-          double sc;
-          const bool ok = dw_canonical_score_wave(AR.R, i - lane + l, sc, lut_lane, n_lut);
-          if (lane == l) {
-            my_s = sc;
-            my_ok = ok;
-          }
-        }
-      }
-    }
-    if (tid == 0) s_old = old;
-    __syncthreads();
-    if (cand) {
-      const int64_t pos = static_cast<int64_t>(static_cast<unsigned>(s_old & 0xFFFFFFFFull)) + before +
-                          __popcll(cm & lt_mask);
-      if (pos < cap) {
-        cidx[pos] = idx_base + i;
-        AR.cpay[pos] = my_s;
-        AR.ckey[pos] = my_ok ? score_key(my_s, DAL_DESCENDING) : DAL_KEY_NONE;
-      }
-    }
-    b += stride;
-    if (b >= n) break;
-    i = b + tid;
-    lo = i < n ? keys_lo[i] : DAL_KEY_NONE;
-    hi = i < n ? keys_hi[i] : DAL_KEY_NONE;
   }
 }
 
@@ -987,15 +903,13 @@ __device__ bool select_compact(const uint64_t* __restrict__ keys, const int64_t*
   return true;
 }
 
+// The sort tail as a block-level device function (kSortThreads threads): the
+// body of sort_kernel, also run by the last block of dw_level1_fused_kernel.
 template <bool PAY>
-__global__ __launch_bounds__(kSortThreads) void sort_kernel(const uint64_t* __restrict__ keys,
-                                                            const int64_t* __restrict__ idx,
-                                                            const double* __restrict__ pay,
-                                                            const TopkHdr* __restrict__ h,
-                                                            int64_t n_static, int64_t k,
-                                                            uint64_t* __restrict__ out_keys,
-                                                            int64_t* __restrict__ out_idx,
-                                                            double* __restrict__ out_pay, SortTail tail) {
+__device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t* __restrict__ idx,
+                               const double* __restrict__ pay, const TopkHdr* __restrict__ h, int64_t n_static,
+                               int64_t k, uint64_t* __restrict__ out_keys, int64_t* __restrict__ out_idx,
+                               double* __restrict__ out_pay, const SortTail& tail) {
   constexpr int CAP = PAY ? DAL_SORT_CAP_PAYLOAD : DAL_SORT_CAP;
   __shared__ unsigned long long sk[CAP];
   __shared__ long long si[CAP];
@@ -1141,6 +1055,244 @@ __global__ __launch_bounds__(kSortThreads) void sort_kernel(const uint64_t* __re
   }
 }
 
+template <bool PAY>
+__global__ __launch_bounds__(kSortThreads) void sort_kernel(const uint64_t* __restrict__ keys,
+                                                            const int64_t* __restrict__ idx,
+                                                            const double* __restrict__ pay,
+                                                            const TopkHdr* __restrict__ h,
+                                                            int64_t n_static, int64_t k,
+                                                            uint64_t* __restrict__ out_keys,
+                                                            int64_t* __restrict__ out_idx,
+                                                            double* __restrict__ out_pay, SortTail tail) {
+  sort_tail_body<PAY>(keys, idx, pay, h, n_static, k, out_keys, out_idx, out_pay, tail);
+}
+
+// ------------------------------------------------ fused level 1 (one launch) ----
+// The truncated level 1 + candidate append with in-place canonical re-rank +
+// the final sort in ONE launch: `passes` radix histogram sweeps over the
+// pessimistic keys, each closed by a grid barrier (every block then resolves
+// the digit itself from the global histogram), the append sweep (rows whose
+// optimistic key is <= tau, re-ranked by their wave), and the block that
+// arrives last sorts the candidates (sort_tail_body) and clears the header.
+// The grid is at most half the CUs with one block per CU (the sort arrays
+// take ~100 KiB of LDS), so every block of the launch is resident even with
+// a second process on the GPU; a barrier still unmet after ~0.1 s raises
+// DAL_FLAG_SAMPLE_MISS and the blocks finish, so the launch always drains
+// (the caller re-runs with the exact level 1).  Requires a zero header.
+constexpr int kFuseThreads = kSortThreads;  // 1024: the last block runs the sort tail
+constexpr unsigned kSpinLimit = 1u << 17;
+
+// all blocks of the grid: every earlier global write/atomic of this block is
+// complete and visible (release) before the arrival; after the wait an
+// acquire makes the other blocks' writes visible to every wave of the block.
+// Returns false when the wait timed out (the result is then discarded).
+__device__ bool grid_barrier(unsigned int* ctr, unsigned int G, int32_t* status) {
+  __shared__ int s_ok;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int ok = 1;
+    unsigned spins = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < G) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > kSpinLimit) {
+        ok = 0;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!ok) atomicOr(status, DAL_FLAG_SAMPLE_MISS);
+    s_ok = ok;
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
+// resolve_digit for kFuseThreads threads (2 bins each)
+__device__ void resolve_digit_fused(const TopkHdr* h, int p, unsigned long long& prefix, unsigned long long& krem) {
+  constexpr int BPT = kBins / kFuseThreads;
+  constexpr int W = kFuseThreads / 64;
+  __shared__ uint32_t sh[W];
+  __shared__ unsigned long long s_pre, s_krem;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const unsigned long long kr = h->krem[p];
+  const int nb = digit_bins(p);
+  uint32_t c[BPT];
+  uint32_t tot = 0;
+#pragma unroll
+  for (int j = 0; j < BPT; ++j) {
+    const int b = tid * BPT + j;
+    c[j] = b < nb ? h->hist[p][b] : 0u;
+    tot += c[j];
+  }
+  uint32_t x = tot;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[w] = x;
+  __syncthreads();
+  uint32_t excl = x - tot;
+  for (int i = 0; i < w; ++i) excl += sh[i];
+  if (excl < kr && excl + tot >= kr) {
+    uint32_t run = excl;
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      if (run < kr && run + c[j] >= kr) {
+        s_pre = h->prefix[p] | (static_cast<unsigned long long>(tid * BPT + j) << digit_shift(p));
+        s_krem = kr - run;
+      }
+      run += c[j];
+    }
+  }
+  __syncthreads();
+  prefix = s_pre;
+  krem = s_krem;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kFuseThreads) void dw_level1_fused_kernel(
+    const uint64_t* __restrict__ keys_lo, const uint64_t* __restrict__ keys_hi, int64_t n, int64_t k,
+    int64_t idx_base, int passes, TopkHdr* __restrict__ h, int64_t* __restrict__ cidx, int64_t cap, AppendRerank AR,
+    int n_lut, int32_t* __restrict__ status, uint64_t* __restrict__ out_keys, int64_t* __restrict__ out_idx,
+    double* __restrict__ out_scores, SortTail tail) {
+  constexpr int W = kFuseThreads / 64;
+  __shared__ uint32_t hist[kBins];
+  __shared__ unsigned s_wc[W], s_wb[W];
+  __shared__ unsigned long long s_old;
+  __shared__ unsigned s_last;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const unsigned G = gridDim.x;
+  const int64_t stride = static_cast<int64_t>(G) * kFuseThreads;
+  const int64_t i0 = static_cast<int64_t>(blockIdx.x) * kFuseThreads + tid;
+  bool ok = true;
+  unsigned long long prefix = 0, krem = static_cast<unsigned long long>(k);
+  // ---- radix passes: histogram of digit p among keys matching the prefix
+  for (int p = 0; p < passes; ++p) {
+    if (p > 0) resolve_digit_fused(h, p - 1, prefix, krem);
+    if (blockIdx.x == 0 && tid == 0) {
+      h->prefix[p] = prefix;
+      h->krem[p] = krem;
+    }
+#pragma unroll
+    for (int j = 0; j < kBins / kFuseThreads; ++j) hist[j * kFuseThreads + tid] = 0;
+    __syncthreads();
+    const int shift = digit_shift(p);
+    const unsigned long long dmask = static_cast<unsigned long long>(digit_bins(p) - 1);
+    const unsigned long long hmask = p == 0 ? 0ull : (~0ull << (64 - kDigitBits * p));
+    for (int64_t ib = i0 - tid; ib < n; ib += 4 * stride) {  // 4 keys per thread in flight (block-uniform trip)
+      unsigned long long kb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t i = ib + j * stride + tid;
+        kb[j] = i < n ? keys_lo[i] : 0ull;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool valid = ib + j * stride + tid < n && (kb[j] & hmask) == prefix;
+        const unsigned bin = static_cast<unsigned>((kb[j] >> shift) & dmask);
+        const unsigned long long vm = __ballot(valid);
+        if (vm) {
+          const int first = __ffsll(static_cast<long long>(vm)) - 1;
+          const unsigned b0 = __shfl(bin, first);
+          const unsigned long long m0 = __ballot(valid && bin == b0);
+          if (lane == first) atomicAdd(&hist[b0], static_cast<unsigned>(__popcll(m0)));
+          if (valid && bin != b0) atomicAdd(&hist[bin], 1u);
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kBins / kFuseThreads; ++j) {
+      const int b = j * kFuseThreads + tid;
+      const uint32_t v = hist[b];
+      if (v) atomicAdd(&h->hist[p][b], v);
+    }
+    ok = grid_barrier(&h->bar[p], G, status) && ok;
+  }
+  resolve_digit_fused(h, passes - 1, prefix, krem);
+  const int sh = digit_shift(passes - 1);
+  const unsigned long long tau = prefix | (sh ? ((1ull << sh) - 1ull) : 0ull);
+  if (blockIdx.x == 0 && tid == 0) h->kstar = tau;
+  // ---- append sweep with the in-place canonical re-rank (append_rerank_kernel)
+  const double lut_lane = lane < n_lut ? AR.R.lut[lane] : 0.0;
+  const unsigned long long lt_mask = (1ull << lane) - 1ull;
+  for (int64_t b = static_cast<int64_t>(blockIdx.x) * kFuseThreads; ok && b < n; b += stride) {  // block-uniform
+    const int64_t i = b + tid;
+    const bool valid = i < n;
+    const unsigned long long lo = valid ? keys_lo[i] : DAL_KEY_NONE;
+    const unsigned long long hi = valid ? keys_hi[i] : DAL_KEY_NONE;
+    const bool cand = valid && hi <= tau && hi != DAL_KEY_NONE;
+    const unsigned long long cm = __ballot(cand);
+    const unsigned long long bm = __ballot(valid && lo <= tau);
+    if (lane == 0) {
+      s_wc[w] = static_cast<unsigned>(__popcll(cm));
+      s_wb[w] = static_cast<unsigned>(__popcll(bm));
+    }
+    __syncthreads();
+    unsigned before = 0, tot_c = 0, tot_b = 0;
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      if (q < w) before += s_wc[q];
+      tot_c += s_wc[q];
+      tot_b += s_wb[q];
+    }
+    if (tid == 0) s_old = (tot_c | tot_b) ? atomicAdd(&h->packed, (static_cast<unsigned long long>(tot_b) << 32) | tot_c)
+                                          : 0ull;
+    double my_s = 0.0;
+    bool my_ok = false;
+    if (cm) {
+      if (__popcll(cm) > 2) {
+        const int v = cand ? AR.R.votes[i] : 0;
+        const double e = n_lut ? __shfl(lut_lane, v) : 0.0;
+        if (cand) my_ok = dw_canonical_score_lane<16>(AR.R, i, my_s, e, n_lut);
+      } else {
+        for (unsigned long long t = cm; t;) {
+          const int l = __ffsll(static_cast<long long>(t)) - 1;
+          t &= t - 1;
+          double sc;
+          const bool okl = dw_canonical_score_wave(AR.R, i - lane + l, sc, lut_lane, n_lut);
+          if (lane == l) {
+            my_s = sc;
+            my_ok = okl;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (cand) {
+      const int64_t pos = static_cast<int64_t>(static_cast<unsigned>(s_old & 0xFFFFFFFFull)) + before +
+                          __popcll(cm & lt_mask);
+      if (pos < cap) {
+        cidx[pos] = idx_base + i;
+        AR.cpay[pos] = my_s;
+        AR.ckey[pos] = my_ok ? score_key(my_s, DAL_DESCENDING) : DAL_KEY_NONE;
+      }
+    }
+    __syncthreads();  // s_wc / s_old are rewritten by the next sweep
+  }
+  // ---- the last block to arrive sorts the candidates
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(&h->bar[kPasses + 1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old == G - 1;
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!s_last) return;
+  sort_tail_body<true>(AR.ckey, cidx, AR.cpay, h, int64_t{0}, k, out_keys, out_idx, out_scores, tail);
+}
+
 // Zero the header with a kernel rather than hipMemsetAsync: the select is
 // replayed inside hipGraphs (engine.WarmStepGraph), where a captured memset
 // node did not clear the header on every replay (observed on gfx950 / ROCm 7).
@@ -1156,6 +1308,30 @@ static_assert(sizeof(TopkHdr) % 4 == 0, "header is whole words");
 void zero_header(TopkHdr* h, hipStream_t st) {
   hipLaunchKernelGGL(zero_words_kernel, dim3(static_cast<unsigned>(ceil_div(kHdrWords, 256 * 4))), dim3(256), 0, st,
                      reinterpret_cast<uint32_t*>(h), kHdrWords);
+}
+
+// dw_level1_fused_kernel's grid: ~4 keys per thread per sweep, at most half
+// the CUs (one block per CU: every block resident even beside a second
+// process on the GPU -- the grid barriers need the whole grid running).
+int fused_grid(int64_t n) {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 2)
+    cus = 2;
+  const int64_t g = ceil_div(n, static_cast<int64_t>(kFuseThreads) * 4);
+  const int64_t gmax = cus / 2;
+  return static_cast<int>(g < 1 ? 1 : (g > gmax ? gmax : g));
+}
+
+int launch_fused_level1(const uint64_t* keys_lo, const uint64_t* keys_hi, int64_t n, int64_t k, int64_t idx_base,
+                        int passes, TopkHdr* h, int64_t* cidx, int64_t cap, const AppendRerank& AR, int n_lut,
+                        int32_t* status, uint64_t* out_keys, int64_t* out_idx, double* out_scores,
+                        const SortTail& tail, hipStream_t st) {
+  hipLaunchKernelGGL(dw_level1_fused_kernel, dim3(static_cast<unsigned>(fused_grid(n))), dim3(kFuseThreads), 0, st,
+                     keys_lo, keys_hi, n, k, idx_base, passes, h, cidx, cap, AR, n_lut, status, out_keys, out_idx,
+                     out_scores, tail);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
 }
 
 // Radix passes 0 .. passes-1 (zero: clear the header first).
@@ -1303,6 +1479,34 @@ extern "C" int dal_dw_select(const uint64_t* keys_lo, const uint64_t* keys_hi, c
     return DAL_ERR_ARG;
   if (d < 1 || ldx < d) return DAL_ERR_SHAPE;
   hipStream_t st = as_stream(stream);
+  if (level1_passes > 0) {
+    // truncated level 1: header zero + ONE fused launch (radix passes with grid
+    // barriers, append with the in-place canonical re-rank, last-block sort)
+    if (n < 1 || k < 1 || k > n || cap < k) return DAL_ERR_SHAPE;
+    if (level1_passes >= kPasses || cap > DAL_SORT_CAP_PAYLOAD) return DAL_ERR_ARG;
+    if (k > DAL_SORT_CAP) return DAL_ERR_CAPACITY;
+    if (ws_bytes < rerank_ws_bytes(n, k, cap) || (reinterpret_cast<uintptr_t>(ws) & 255)) return DAL_ERR_SHAPE;
+    const TopkLayout L1 = topk_layout(n, cap);
+    char* base = static_cast<char*>(ws);
+    TopkHdr* h1 = reinterpret_cast<TopkHdr*>(base + L1.hdr);
+    zero_header(h1, st);
+    if (colsum_ready && hipStreamWaitEvent(st, reinterpret_cast<hipEvent_t>(colsum_ready), 0) != hipSuccess)
+      return DAL_ERR_HIP;
+    const DwRerank R{x, static_cast<int>(d), ldx, norm64, colsum, lut, votes, row_flags, beta};
+    SortTail tail;
+    tail.cap = cap;
+    tail.need_k = k;
+    tail.status = dev_status;
+    tail.clear = reinterpret_cast<uint32_t*>(h1);
+    tail.clear_words = kHdrWords;
+    tail.packed = true;
+    // (the LUT size is not an argument of dal_dw_select: no lane-held LUT)
+    return launch_fused_level1(keys_lo, keys_hi, n, k, idx_base, level1_passes, h1,
+                               reinterpret_cast<int64_t*>(base + L1.cidx), cap,
+                               AppendRerank{R, reinterpret_cast<uint64_t*>(base + L1.ckey),
+                                            reinterpret_cast<double*>(base + L1.cpay)},
+                               0, dev_status, out_keys, out_idx, out_scores, tail, st);
+  }
   bool wait_failed = false;
   auto rerank = [&](TopkHdr* h, uint64_t* ckey, int64_t* cidx, double* cpay, int64_t cp, int64_t need_k) {
     // the only consumer of colsum: join its producer stream here, not before the call
@@ -1376,21 +1580,13 @@ int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_
                                density_err, row_flags, beta, DAL_DESCENDING, votes, scores, keys_lo, keys_hi, hooks,
                                st);
   if (rc) return rc;
-  rc = run_radix(keys_lo, n, k, h1, st, level1_passes, false);
-  if (rc) return rc;
   if (colsum_ready && hipStreamWaitEvent(st, reinterpret_cast<hipEvent_t>(colsum_ready), 0) != hipSuccess)
     return DAL_ERR_HIP;
   uint64_t* ckey = reinterpret_cast<uint64_t*>(base + L1.ckey);
   int64_t* cidx = reinterpret_cast<int64_t*>(base + L1.cidx);
   double* cpay = reinterpret_cast<double*>(base + L1.cpay);
   const DwRerank R{x, static_cast<int>(d), ldx, norm64, colsum, lut, votes, row_flags, beta};
-  // one key per thread where possible: a wave scores its candidates one after
-  // another, so the fewer rows a wave sweeps, the shorter its longest chain
-  const int64_t blocks = std::min<int64_t>(ceil_div(n, kRadixThreads), 2048);
   const int n_lut = n_trees < 64 ? n_trees + 1 : 0;  // LUT held in lanes when it fits a wave
-  hipLaunchKernelGGL(append_rerank_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kRadixThreads), 0, st, keys_lo,
-                     keys_hi, n, idx_base, static_cast<int>(level1_passes), h1, cidx, cap, AppendRerank{R, ckey, cpay},
-                     n_lut);
   SortTail tail;
   tail.cap = cap;
   tail.need_k = k;
@@ -1400,10 +1596,10 @@ int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_
   tail.out_slot = out_slot;
   tail.status_mirror = status_mirror;
   tail.packed = true;
-  hipLaunchKernelGGL(sort_kernel<true>, dim3(1), dim3(kSortThreads), 0, st, ckey, cidx, cpay, h1, int64_t{0}, k,
-                     out_keys, out_idx, out_scores, tail);
-  DAL_RETURN_IF_LAUNCH_FAILED();
-  return DAL_OK;
+  // the level-1 radix passes, the append with the in-place canonical re-rank
+  // and the final sort: ONE launch after the forest score
+  return launch_fused_level1(keys_lo, keys_hi, n, k, idx_base, static_cast<int>(level1_passes), h1, cidx, cap,
+                             AppendRerank{R, ckey, cpay}, n_lut, dev_status, out_keys, out_idx, out_scores, tail, st);
 }
 
 }  // namespace dal

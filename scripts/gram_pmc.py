@@ -1,0 +1,28 @@
+"""The density Gram (dal_gram_rowsum_sym + dal_gram_sym_residual) at one
+shape, a few launches, for rocprofv3 --pmc / --kernel-trace (one counter
+group per run).  usage: python scripts/gram_pmc.py NxD [reps]"""
+import os
+import sys
+
+REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(REPO, "distributed-active-learning_amd"))
+sys.path.insert(0, REPO)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from dal.engine import PoolState  # noqa: E402
+
+dev = torch.device("cuda:0")
+n, d = (int(v) for v in sys.argv[1].split("x"))
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+x = bench.upload(bench.host_pool(0, n, d, "normal" if d == 30 else "uniform"), dev)
+st = PoolState(x, excluded=np.arange(10), device=dev)
+op = st.gram_operand()
+acc = torch.zeros(st.n_pad, dtype=torch.int64, device=dev)
+for _ in range(reps):
+    acc.zero_()
+    st.gram_accumulate(acc, op, st.n_pad)
+    st.gram_residual(acc, op)
+torch.cuda.synchronize()
+print("ok", n, d, reps, int(acc[100]))

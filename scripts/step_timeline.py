@@ -43,6 +43,8 @@ if __name__ == "__main__":
     import bench
 
     dev = torch.device("cuda:0")
+    if len(sys.argv) > 2:  # step_timeline.py warm|cold CONFIG
+        os.environ["TL_CONFIG"] = sys.argv[2]
     n, d = (int(v) for v in os.environ.get("TL_SHAPE", "100000x64").split("x"))
     trees, dist = 10, "uniform"
     if os.environ.get("TL_CONFIG"):  # a BASELINE config of bench.py (pool, forest)
