@@ -60,6 +60,27 @@ __host__ __device__ constexpr int digit_bins(int p) {
   return 1 << (64 - kDigitBits * p - digit_shift(p));
 }
 
+// Agent-scope relaxed loads / stores (global_load / global_store ... sc1):
+// the hand-offs between blocks of dw_level1_fused_kernel (histograms, level-1
+// state, candidates) are written and read only this way, so no release /
+// acquire fence is needed around its grid barriers (MI355X_MICROARCH.md,
+// "Valid forms": sc1 stores or agent atomics, vmcnt(0) + a workgroup barrier
+// before one lane's arrival, an sc1 poll, sc1 loads after a barrier).
+template <class T>
+__device__ __forceinline__ T ld_sc1(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double(ld_sc1(reinterpret_cast<const long long*>(p)));
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  st_sc1(reinterpret_cast<long long*>(p), __double_as_longlong(v));
+}
+
 struct TopkHdr {
   uint32_t hist[kPasses][kBins];
   unsigned long long prefix[kPasses + 1];
@@ -823,7 +844,7 @@ __device__ bool select_compact(const uint64_t* __restrict__ keys, const int64_t*
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     const int64_t e = tid + static_cast<int64_t>(j) * kSortThreads;
-    key[j] = e < m ? keys[e] : 0ull;
+    key[j] = e < m ? ld_sc1(keys + e) : 0ull;
   }
   unsigned long long prefix = 0, mask = 0;
   unsigned int krem = static_cast<unsigned int>(k), neq = static_cast<unsigned int>(m);
@@ -894,8 +915,8 @@ __device__ bool select_compact(const uint64_t* __restrict__ keys, const int64_t*
     if (take) {
       const unsigned p = base + static_cast<unsigned>(__popcll(tm & ((1ull << lane) - 1ull)));
       sk[p] = key[j];
-      si[p] = idx[e];
-      sp[p] = pay[e];
+      si[p] = ld_sc1(idx + e);
+      sp[p] = ld_sc1(pay + e);
     }
   }
   __syncthreads();
@@ -917,10 +938,10 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
   __shared__ int64_t* s_dest[2];
   const int tid = threadIdx.x;
   if (tid < 2) s_dest[tid] = load_out_slot(tail.out_slot, tid);  // host round trips, overlapping the sort
-  const unsigned long long packed = tail.packed ? h->packed : 0ull;
+  const unsigned long long packed = tail.packed ? ld_sc1(&h->packed) : 0ull;
   int64_t m = !h ? n_static : tail.packed ? static_cast<int64_t>(packed & 0xFFFFFFFFull)
-                                          : static_cast<int64_t>(h->cand_count);
-  const unsigned long long total_lt = !h ? 0ull : tail.packed ? (packed >> 32) : h->total_lt;
+                                          : static_cast<int64_t>(ld_sc1(&h->cand_count));
+  const unsigned long long total_lt = !h ? 0ull : tail.packed ? (packed >> 32) : ld_sc1(&h->total_lt);
   if (tail.need_k && tid == 0 && (total_lt < static_cast<unsigned long long>(tail.need_k) || m > tail.cap))
     atomicOr(tail.status, DAL_FLAG_SAMPLE_MISS);
   if (tail.cap && m > tail.cap) m = tail.cap;
@@ -936,9 +957,9 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
     // smaller pairs, read as LDS broadcasts -- is its output position: two
     // barriers instead of the bitonic network's log^2 m stages.
     for (int i = tid; i < m; i += kSortThreads) {
-      sk[i] = keys[i];
-      si[i] = idx[i];
-      if (PAY) sp[i] = pay[i];
+      sk[i] = ld_sc1(keys + i);
+      si[i] = ld_sc1(idx + i);
+      if (PAY) sp[i] = ld_sc1(pay + i);
     }
     __syncthreads();
     if (tail.clear) {  // every thread read the header above
@@ -991,9 +1012,9 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
         if (PAY) sp[i] = 0.0;
       }
     } else if (i < m) {
-      sk[i] = keys[i];
-      si[i] = idx[i];
-      if (PAY) sp[i] = pay[i];
+      sk[i] = ld_sc1(keys + i);
+      si[i] = ld_sc1(idx + i);
+      if (PAY) sp[i] = ld_sc1(pay + i);
     } else {
       sk[i] = ~0ull;
       si[i] = 0x7FFFFFFFFFFFFFFFll;
@@ -1082,29 +1103,26 @@ __global__ __launch_bounds__(kSortThreads) void sort_kernel(const uint64_t* __re
 constexpr int kFuseThreads = kSortThreads;  // 1024: the last block runs the sort tail
 constexpr unsigned kSpinLimit = 1u << 17;
 
-// all blocks of the grid: every earlier global write/atomic of this block is
-// complete and visible (release) before the arrival; after the wait an
-// acquire makes the other blocks' writes visible to every wave of the block.
-// Returns false when the wait timed out (the result is then discarded).
+// All blocks of the grid: every global store / atomic of this block issued
+// before the call is complete (vmcnt(0) in every wave, then a workgroup
+// barrier) before one lane's arrival; the wait is an sc1 poll, and the
+// blocks read the handed-off words with sc1 loads only.  Returns false when
+// the wait timed out (the caller then discards the launch's result).
 __device__ bool grid_barrier(unsigned int* ctr, unsigned int G, int32_t* status) {
   __shared__ int s_ok;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int ok = 1;
     unsigned spins = 0;
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < G) {
+    while (ld_sc1(ctr) < G) {
       __builtin_amdgcn_s_sleep(2);
       if (++spins > kSpinLimit) {
         ok = 0;
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!ok) atomicOr(status, DAL_FLAG_SAMPLE_MISS);
     s_ok = ok;
   }
@@ -1119,14 +1137,14 @@ __device__ void resolve_digit_fused(const TopkHdr* h, int p, unsigned long long&
   __shared__ uint32_t sh[W];
   __shared__ unsigned long long s_pre, s_krem;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const unsigned long long kr = h->krem[p];
+  const unsigned long long kr = ld_sc1(&h->krem[p]);
   const int nb = digit_bins(p);
   uint32_t c[BPT];
   uint32_t tot = 0;
 #pragma unroll
   for (int j = 0; j < BPT; ++j) {
     const int b = tid * BPT + j;
-    c[j] = b < nb ? h->hist[p][b] : 0u;
+    c[j] = b < nb ? ld_sc1(&h->hist[p][b]) : 0u;
     tot += c[j];
   }
   uint32_t x = tot;
@@ -1143,7 +1161,7 @@ __device__ void resolve_digit_fused(const TopkHdr* h, int p, unsigned long long&
 #pragma unroll
     for (int j = 0; j < BPT; ++j) {
       if (run < kr && run + c[j] >= kr) {
-        s_pre = h->prefix[p] | (static_cast<unsigned long long>(tid * BPT + j) << digit_shift(p));
+        s_pre = ld_sc1(&h->prefix[p]) | (static_cast<unsigned long long>(tid * BPT + j) << digit_shift(p));
         s_krem = kr - run;
       }
       run += c[j];
@@ -1162,8 +1180,6 @@ __global__ __launch_bounds__(kFuseThreads) void dw_level1_fused_kernel(
     double* __restrict__ out_scores, SortTail tail) {
   constexpr int W = kFuseThreads / 64;
   __shared__ uint32_t hist[kBins];
-  __shared__ unsigned s_wc[W], s_wb[W];
-  __shared__ unsigned long long s_old;
   __shared__ unsigned s_last;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const unsigned G = gridDim.x;
@@ -1175,8 +1191,8 @@ __global__ __launch_bounds__(kFuseThreads) void dw_level1_fused_kernel(
   for (int p = 0; p < passes; ++p) {
     if (p > 0) resolve_digit_fused(h, p - 1, prefix, krem);
     if (blockIdx.x == 0 && tid == 0) {
-      h->prefix[p] = prefix;
-      h->krem[p] = krem;
+      st_sc1(&h->prefix[p], prefix);
+      st_sc1(&h->krem[p], krem);
     }
 #pragma unroll
     for (int j = 0; j < kBins / kFuseThreads; ++j) hist[j * kFuseThreads + tid] = 0;
@@ -1218,75 +1234,115 @@ __global__ __launch_bounds__(kFuseThreads) void dw_level1_fused_kernel(
   const int sh = digit_shift(passes - 1);
   const unsigned long long tau = prefix | (sh ? ((1ull << sh) - 1ull) : 0ull);
   if (blockIdx.x == 0 && tid == 0) h->kstar = tau;
-  // ---- append sweep with the in-place canonical re-rank (append_rerank_kernel)
+  // ---- append with the in-place canonical re-rank: rows whose optimistic
+  // key is <= tau.  The block's rows (4 per thread per super-sweep) are
+  // counted first, the block reserves its slots with ONE packed atomic
+  // (candidates | rows with pessimistic key <= tau), then a second sweep
+  // (L2-hot keys) scores and writes the candidates -- one atomic round trip
+  // per block instead of one per sweep.
+  constexpr int J = 4;
+  constexpr int kMaxSw = 32;  // super-sweeps per count / write round
+  __shared__ unsigned s_cnt[kMaxSw * W];
+  __shared__ unsigned s_wsum[W];
+  __shared__ unsigned long long s_base;
   const double lut_lane = lane < n_lut ? AR.R.lut[lane] : 0.0;
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
-  for (int64_t b = static_cast<int64_t>(blockIdx.x) * kFuseThreads; ok && b < n; b += stride) {  // block-uniform
-    const int64_t i = b + tid;
-    const bool valid = i < n;
-    const unsigned long long lo = valid ? keys_lo[i] : DAL_KEY_NONE;
-    const unsigned long long hi = valid ? keys_hi[i] : DAL_KEY_NONE;
-    const bool cand = valid && hi <= tau && hi != DAL_KEY_NONE;
-    const unsigned long long cm = __ballot(cand);
-    const unsigned long long bm = __ballot(valid && lo <= tau);
-    if (lane == 0) {
-      s_wc[w] = static_cast<unsigned>(__popcll(cm));
-      s_wb[w] = static_cast<unsigned>(__popcll(bm));
+  const int64_t b_first = static_cast<int64_t>(blockIdx.x) * kFuseThreads;
+  const int64_t sw_rows = J * stride;  // rows between a thread's super-sweeps
+  for (int64_t r0 = b_first; ok && r0 < n; r0 += kMaxSw * sw_rows) {  // block-uniform
+    const int n_sw = static_cast<int>(std::min<int64_t>(kMaxSw, ceil_div(n - r0, sw_rows)));
+    // count pass
+    unsigned below_w = 0;
+    for (int sw = 0; sw < n_sw; ++sw) {
+      const int64_t base_i = r0 + sw * sw_rows + tid;
+      unsigned cw = 0;
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int64_t i = base_i + j * stride;
+        const bool valid = i < n;
+        const unsigned long long lo = valid ? keys_lo[i] : DAL_KEY_NONE;
+        const unsigned long long hi = valid ? keys_hi[i] : DAL_KEY_NONE;
+        cw += static_cast<unsigned>(__popcll(__ballot(valid && hi <= tau && hi != DAL_KEY_NONE)));
+        below_w += static_cast<unsigned>(__popcll(__ballot(valid && lo <= tau)));
+      }
+      if (lane == 0) s_cnt[sw * W + w] = cw;
+    }
+    if (lane == 0) s_wsum[w] = below_w;
+    __syncthreads();
+    // exclusive scan of the (super-sweep, wave) counts, row-major: thread e
+    const int ne = n_sw * W;
+    unsigned cnt_e = tid < ne ? s_cnt[tid] : 0u;
+    unsigned x = cnt_e;
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    __shared__ unsigned s_wtot[W];
+    if (lane == 63) s_wtot[w] = x;
+    __syncthreads();
+    unsigned excl = x - cnt_e;
+    for (int q = 0; q < w; ++q) excl += s_wtot[q];
+    if (tid == 0) {
+      unsigned tot_c = 0, tot_b = 0;
+      for (int q = 0; q < W; ++q) {
+        tot_c += s_wtot[q];
+        tot_b += s_wsum[q];
+      }
+      s_base = (tot_c | tot_b) ? atomicAdd(&h->packed, (static_cast<unsigned long long>(tot_b) << 32) | tot_c) : 0ull;
     }
     __syncthreads();
-    unsigned before = 0, tot_c = 0, tot_b = 0;
-#pragma unroll
-    for (int q = 0; q < W; ++q) {
-      if (q < w) before += s_wc[q];
-      tot_c += s_wc[q];
-      tot_b += s_wb[q];
-    }
-    if (tid == 0) s_old = (tot_c | tot_b) ? atomicAdd(&h->packed, (static_cast<unsigned long long>(tot_b) << 32) | tot_c)
-                                          : 0ull;
-    double my_s = 0.0;
-    bool my_ok = false;
-    if (cm) {
-      if (__popcll(cm) > 2) {
-        const int v = cand ? AR.R.votes[i] : 0;
-        const double e = n_lut ? __shfl(lut_lane, v) : 0.0;
-        if (cand) my_ok = dw_canonical_score_lane<16>(AR.R, i, my_s, e, n_lut);
-      } else {
-        for (unsigned long long t = cm; t;) {
-          const int l = __ffsll(static_cast<long long>(t)) - 1;
-          t &= t - 1;
-          double sc;
-          const bool okl = dw_canonical_score_wave(AR.R, i - lane + l, sc, lut_lane, n_lut);
-          if (lane == l) {
-            my_s = sc;
-            my_ok = okl;
+    if (tid < ne) s_cnt[tid] = excl;  // (every thread read its count above)
+    __syncthreads();
+    const int64_t base = static_cast<int64_t>(static_cast<unsigned>(s_base & 0xFFFFFFFFull));
+    // write pass: the same rows in the same order
+    for (int sw = 0; sw < n_sw; ++sw) {
+      const int64_t base_i = r0 + sw * sw_rows + tid;
+      int64_t pos = base + s_cnt[sw * W + w];
+#pragma unroll 1
+      for (int j = 0; j < J; ++j) {
+        const int64_t i = base_i + j * stride;
+        const bool valid = i < n;
+        const unsigned long long hi = valid ? keys_hi[i] : DAL_KEY_NONE;
+        const bool cand = valid && hi <= tau && hi != DAL_KEY_NONE;
+        const unsigned long long cm = __ballot(cand);
+        if (!cm) continue;
+        double my_s = 0.0;
+        bool my_ok = false;
+        if (__popcll(cm) > 2) {
+          const int v = cand ? AR.R.votes[i] : 0;
+          const double e = n_lut ? __shfl(lut_lane, v) : 0.0;
+          if (cand) my_ok = dw_canonical_score_lane<8>(AR.R, i, my_s, e, n_lut);
+        } else {
+          for (unsigned long long t = cm; t;) {
+            const int l = __ffsll(static_cast<long long>(t)) - 1;
+            t &= t - 1;
+            double sc;
+            const bool okl = dw_canonical_score_wave(AR.R, i - lane + l, sc, lut_lane, n_lut);
+            if (lane == l) {
+              my_s = sc;
+              my_ok = okl;
+            }
           }
         }
+        if (cand) {
+          const int64_t p = pos + __popcll(cm & lt_mask);
+          if (p < cap) {
+            st_sc1(cidx + p, static_cast<int64_t>(idx_base + i));
+            st_sc1(AR.cpay + p, my_s);
+            st_sc1(AR.ckey + p, static_cast<uint64_t>(my_ok ? score_key(my_s, DAL_DESCENDING) : DAL_KEY_NONE));
+          }
+        }
+        pos += __popcll(cm);
       }
     }
-    __syncthreads();
-    if (cand) {
-      const int64_t pos = static_cast<int64_t>(static_cast<unsigned>(s_old & 0xFFFFFFFFull)) + before +
-                          __popcll(cm & lt_mask);
-      if (pos < cap) {
-        cidx[pos] = idx_base + i;
-        AR.cpay[pos] = my_s;
-        AR.ckey[pos] = my_ok ? score_key(my_s, DAL_DESCENDING) : DAL_KEY_NONE;
-      }
-    }
-    __syncthreads();  // s_wc / s_old are rewritten by the next sweep
+    __syncthreads();  // s_cnt / s_base are rewritten by the next round
   }
   // ---- the last block to arrive sorts the candidates
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned old = __hip_atomic_fetch_add(&h->bar[kPasses + 1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = old == G - 1;
-    if (s_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    s_last = old == G - 1;  // the returned value: every other block's stores are complete
   }
   __syncthreads();
   if (!s_last) return;
