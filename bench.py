@@ -85,8 +85,8 @@ def resolve(spec: str):
 POOL_SEED = 0
 DATA_NOTE = ("synthetic: numpy default_rng(0) pool of the BASELINE.md shape (rows of a shard generated "
              "by PCG64 advance, identical for every GPU count); forest synthetic (default_rng(1))")
-# K3 (dal_dw_select level 1) algorithmic bytes per row: the radix select reads
-# the pessimistic key once per pass; the ordered compaction reads both
+# K3 (dal_dw_select exact level 1) algorithmic bytes per row: the radix select
+# reads the pessimistic key once per pass; the ordered compaction reads both
 # interval keys twice (count, write).
 TOPK_RADIX_PASSES = 6
 
@@ -285,16 +285,17 @@ def forest_roofline(n_rows, d, trees, forest_ms, config, world):
 def topk_roofline(n_rows, select_ms, config, world, level1_passes=0):
     """K3 (dal_dw_select).  Exact level 1: radix select of the k-th
     pessimistic key (6 passes x 8 B per row) + ordered compaction (count and
-    write: both interval keys, 2 x 16 B per row).  Truncated level 1 (the
-    engine default on pools whose candidates fit 4,096 slots): 2 radix passes
-    (2 x 8 B) + one append pass over both keys (16 B).  The exact fp64 re-rank
-    and the one-block sort touch O(candidates) bytes."""
+    write: both interval keys, 2 x 16 B per row).  Fast level 1 (the engine
+    default on pools whose candidates fit 4,096 slots): both interval keys read
+    once for the row-group minima (16 B per row); the threshold, the scan of
+    the groups that can hold candidates, the exact fp64 re-rank and the
+    one-block sort touch O(groups + candidates) bytes."""
     if not select_ms:
         return None
     if level1_passes:
-        per_row = 8 * level1_passes + 16
-        kernel = (f"dal_dw_select ({level1_passes}-digit radix bound + candidate append + fp64 re-rank + "
-                  "sort)")
+        per_row = 16
+        kernel = ("dal_dw_select (fast level 1: row-group minima -> tau = k-th group minimum -> candidate append "
+                  "with in-place fp64 re-rank -> last-block sort; 2 launches)")
     else:
         per_row = 8 * TOPK_RADIX_PASSES + 32
         kernel = "dal_dw_select (radix select + interval compaction + fp64 re-rank + sort)"
@@ -304,7 +305,7 @@ def topk_roofline(n_rows, select_ms, config, world, level1_passes=0):
             "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
             "traffic": _traffic(config, "dw_select_bytes_per_launch", world), "launch_ms": select_ms,
             "algorithmic_bytes_per_launch": nbytes, "bytes_per_row": per_row,
-            "note": "one C-ABI call (several dependent launches), HIP events on the launch stream, warm steps"}
+            "note": "one C-ABI call, HIP events on the launch stream, warm steps"}
 
 
 # ----------------------------------------------------------- workloads --
@@ -551,7 +552,7 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
                    "parallelism": f"row-shard dp{world} (RCCL all-gather)" if world > 1 else "single GPU"},
         "selection_latency_ms": ms_per_step,
         "warm_selection_latency_ms": warm_ms,
-        "warm_path": ("hipGraph replay (votes/score -> sampled or radix candidate search -> fp64 re-rank -> "
+        "warm_path": ("hipGraph replay (votes/score + row-group minima -> candidate search -> fp64 re-rank -> "
                       "sort) + input refresh, one status read" if world == 1 and state.use_graphs
                       else "eager launches"),
         "warm_rows_per_s": (n_scored / (warm_ms * 1e-3)) if warm_ms else None,

@@ -97,13 +97,26 @@ __device__ __forceinline__ double row_sq_norm_bf16(const uint16_t* __restrict__ 
 //                base_flags[r] | (stamp[r] == *step_id ? DAL_ROW_CANDIDATE : 0),
 //                written to row_flags for the step's later kernels -- the
 //                unlabeled rows were stamped by the plan's mark kernel, so no
-//                per-step copy of the base flags.
+//                per-step copy of the base flags;
+//   gmin         (nullable; the fast level 1 of the top-k, topk.hip) block b
+//                folds the minimum (pessimistic, optimistic) keys of its rows
+//                into group g = b / group_blocks: gmin[g] / gmin[n_groups + g],
+//                stored inverted (~key, so a zero word reads DAL_KEY_NONE) --
+//                a plain store when group_blocks == 1, else an atomic max on a
+//                buffer the top-k leaves zero.
 struct ForestStepHooks {
   int32_t* status_reset = nullptr;
   const uint8_t* base_flags = nullptr;
   const uint32_t* stamp = nullptr;
   const uint32_t* step_id = nullptr;
+  uint64_t* gmin = nullptr;
+  int group_blocks = 1;
+  int64_t n_groups = 0;
 };
+
+// Rows per block of dal_forest_score's kernel for this shape (the row
+// groups of ForestStepHooks::gmin are whole blocks).
+int forest_rows_per_block(const float* x, int64_t d, int64_t ldx, int32_t n_trees);
 
 int forest_score_launch(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
                         const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,

@@ -21,8 +21,6 @@
 // flight (ILP over trees).  Votes are integers; the score comes from an fp64
 // look-up table indexed by v, so US scores are exact fp64 and identical to the
 // reference's Python float arithmetic.
-#include <cstdlib>
-
 #include "common.hpp"
 
 namespace dal {
@@ -213,36 +211,110 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
   }
   // row's TPR threads are consecutive lanes
   for (int o = 1; o < tpr; o <<= 1) v += __shfl_xor(v, o);
-  if (!live || sub != 0) return;
-
-  const uint8_t fl = pre ? fl_pre : A.flags ? row_flag(A, row) : DAL_ROW_CANDIDATE;
-  if (A.hooks.base_flags) const_cast<uint8_t*>(A.flags)[row] = fl;  // the step's flags for the later kernels
-  const double e = A.lut[v];
-  double s, err = 0.0;
-  if (A.dkind) {
-    const long long draw = pre ? dens_pre : static_cast<const long long*>(A.density)[row];
-    double d = A.dkind == 1 ? from_fixed(draw) : __builtin_bit_cast(double, draw);
-    if (fl & DAL_ROW_EXCLUDED) d = __builtin_nan("");
-    s = e * density_pow(d, A.beta);
-    if (A.dkind == 1 && e == e && e != 0.0 && d == d) {
-      err = fabs(e) * density_pow_err(d, A.derr, A.beta);
-      // keep the interval ends distinct from s after rounding
-      err = fmax(err, fabs(s) * 4.5e-16);
+  unsigned long long klo = DAL_KEY_NONE, khi = DAL_KEY_NONE;
+  if (live && sub == 0) {
+    const uint8_t fl = pre ? fl_pre : A.flags ? row_flag(A, row) : DAL_ROW_CANDIDATE;
+    if (A.hooks.base_flags) const_cast<uint8_t*>(A.flags)[row] = fl;  // the step's flags for the later kernels
+    const double e = A.lut[v];
+    double s, err = 0.0;
+    if (A.dkind) {
+      const long long draw = pre ? dens_pre : static_cast<const long long*>(A.density)[row];
+      double d = A.dkind == 1 ? from_fixed(draw) : __builtin_bit_cast(double, draw);
+      if (fl & DAL_ROW_EXCLUDED) d = __builtin_nan("");
+      s = e * density_pow(d, A.beta);
+      if (A.dkind == 1 && e == e && e != 0.0 && d == d) {
+        err = fabs(e) * density_pow_err(d, A.derr, A.beta);
+        // keep the interval ends distinct from s after rounding
+        err = fmax(err, fabs(s) * 4.5e-16);
+      }
+    } else {
+      s = e;
     }
-  } else {
-    s = e;
+    A.votes[row] = v;
+    A.scores[row] = s;
+    if (fl & DAL_ROW_CANDIDATE) {
+      klo = score_key(pessimistic(s, err, A.order), A.order);
+      khi = score_key(optimistic(s, err, A.order), A.order);
+    }
+    A.keys[row] = klo;
+    if (A.keys_hi) A.keys_hi[row] = khi;
   }
-  A.votes[row] = v;
-  A.scores[row] = s;
-  const bool cand = fl & DAL_ROW_CANDIDATE;
-  A.keys[row] = cand ? score_key(pessimistic(s, err, A.order), A.order) : DAL_KEY_NONE;
-  if (A.keys_hi) A.keys_hi[row] = cand ? score_key(optimistic(s, err, A.order), A.order) : DAL_KEY_NONE;
+  if (!A.hooks.gmin) return;  // kernel-uniform
+  // the block's minimum keys -> its row group (the top-k's fast level 1)
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long a = __shfl_xor(klo, o), b = __shfl_xor(khi, o);
+    klo = a < klo ? a : klo;
+    khi = b < khi ? b : khi;
+  }
+  __shared__ unsigned long long s_min[2][kForestThreads / 64];
+  if ((tid & 63) == 0) {
+    s_min[0][tid >> 6] = klo;
+    s_min[1][tid >> 6] = khi;
+  }
+  __syncthreads();
+  if (tid == 0) {
+#pragma unroll
+    for (int w = 1; w < kForestThreads / 64; ++w) {
+      klo = s_min[0][w] < klo ? s_min[0][w] : klo;
+      khi = s_min[1][w] < khi ? s_min[1][w] : khi;
+    }
+    const int64_t g = blockIdx.x / A.hooks.group_blocks;
+    unsigned long long* lo_g = reinterpret_cast<unsigned long long*>(A.hooks.gmin) + g;
+    unsigned long long* hi_g = lo_g + A.hooks.n_groups;
+    if (A.hooks.group_blocks == 1) {
+      *lo_g = ~klo;
+      *hi_g = ~khi;
+    } else {
+      if (klo != DAL_KEY_NONE) atomicMax(lo_g, ~klo);
+      if (khi != DAL_KEY_NONE) atomicMax(hi_g, ~khi);
+    }
+  }
 }
 
 }  // namespace
 }  // namespace dal
 
 namespace dal {
+
+namespace {
+struct ForestTiling {
+  int R;        // rows per block
+  bool x_lds;   // pool rows staged in LDS
+  bool dma;     // ... by LDS-DMA (wide rows)
+};
+
+ForestTiling forest_tiling(const float* x, int64_t d, int64_t ldx, int32_t n_trees) {
+  // rows per block: stage up to ~16 KiB of pool rows in LDS.  Small tiles keep
+  // more blocks (and their loads) resident per CU: at 2M x 256 a 16 KiB tile
+  // runs 0.52 ms vs 0.60 (32 KiB) / 0.85 (96 KiB) / 0.75 (8 KiB); neutral at
+  // 100k x 64 and 284,807 x 30
+  ForestTiling T{256, true, false};
+  // LDS-DMA staging for wide rows (d % 4 == 0, ldx % 4 == 0, 16-B-aligned
+  // pool; narrow rows leave most lanes of each DMA instruction idle: 2M x 32 x
+  // 100: 264 -> 290 us, 100k x 64: 18.4 -> 19.8) holds no registers: 32 KiB
+  // tiles there (2M x 256: 441 -> 411 us; 64 KiB 1248)
+  T.dma = d >= 128 && d % 4 == 0 && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0;
+  const int64_t tile_cap = T.dma ? 33280 : 16640;
+  while (T.R > 16 && static_cast<int64_t>(T.R) * (d + 1) * 4 > tile_cap) T.R >>= 1;
+  // wide rows: 16 rows may exceed the preferred tile; LDS staging up to 64 KiB
+  if (static_cast<int64_t>(T.R) * (d + 1) * 4 > 65536) {
+    T.x_lds = false;
+    T.dma = false;
+    T.R = 256;
+  }
+  // many trees (config 3: T = 100): spread a row's trees over more lanes --
+  // the traversal's dependent LDS round trips, not HBM, bound that case
+  const int tpr_min = n_trees >= 64 ? 2 : 1;  // config 3: 60.7 -> 51.8 us (4: 53.5, 8: 60.9)
+  if (T.x_lds) {
+    while (T.R > 1 && kForestThreads / T.R < tpr_min) T.R >>= 1;
+  }
+  return T;
+}
+}  // namespace
+
+int forest_rows_per_block(const float* x, int64_t d, int64_t ldx, int32_t n_trees) {
+  return forest_tiling(x, d, ldx, n_trees).R;
+}
 
 int forest_score_launch(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
                         const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
@@ -255,51 +327,27 @@ int forest_score_launch(const float* x, int64_t n, int64_t d, int64_t ldx, const
   if (n < 0 || d < 1 || ldx < d || n_trees < 1) return DAL_ERR_SHAPE;
   if (depth < 1 || depth > DAL_MAX_TREE_DEPTH) return DAL_ERR_UNSUPPORTED;
   if (n == 0) return DAL_OK;
+  const ForestTiling T = forest_tiling(x, d, ldx, n_trees);
+  const int R = T.R, tpr = kForestThreads / R;
+  const int64_t blocks = ceil_div(n, R);
+  if (hooks_in.gmin &&
+      (hooks_in.group_blocks < 1 || ceil_div(blocks, hooks_in.group_blocks) != hooks_in.n_groups))
+    return DAL_ERR_ARG;
   ForestArgs A{x, n, static_cast<int>(d), ldx, reinterpret_cast<const int2*>(inner), leaf, n_trees,
                depth, lut, density_kind ? density : nullptr, density_kind, density_err, row_flags, beta,
                order, votes, scores, keys, keys_hi, hooks_in};
-  // rows per block: stage up to ~16 KiB of pool rows in LDS.  Small tiles keep
-  // more blocks (and their loads) resident per CU: at 2M x 256 a 16 KiB tile
-  // runs 0.52 ms vs 0.60 (32 KiB) / 0.85 (96 KiB) / 0.75 (8 KiB); neutral at
-  // 100k x 64 and 284,807 x 30 (scripts/gpu_job63.sh, gpu_job64.sh)
-  int R = 256;
-  bool x_lds = true;
-  // LDS-DMA staging (wide rows, below) holds no registers: 32 KiB tiles there
-  // (2M x 256: 441 -> 411 us; 64 KiB 1248)
-  const bool dma_rows = d >= 128 && d % 4 == 0 && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0;
-  int64_t tile_cap = dma_rows ? 33280 : 16640;
-  if (const char* e = getenv("DAL_FOREST_TILE_BYTES")) tile_cap = atoll(e);  // timing knob (A/B runs)
-  while (R > 16 && static_cast<int64_t>(R) * (d + 1) * 4 > tile_cap) R >>= 1;
-  // wide rows: 16 rows may exceed the preferred tile; LDS staging up to 64 KiB
-  if (static_cast<int64_t>(R) * (d + 1) * 4 > 65536) {
-    x_lds = false;
-    R = 256;
-  }
-  // many trees (config 3: T = 100): spread a row's trees over more lanes --
-  // the traversal's dependent LDS round trips, not HBM, bound that case
-  int tpr_min = n_trees >= 64 ? 2 : 1;  // config 3: 60.7 -> 51.8 us (4: 53.5, 8: 60.9)
-  if (const char* e = getenv("DAL_FOREST_TPR")) tpr_min = atoi(e);  // timing knob (A/B runs)
-  if (x_lds) {
-    while (R > 1 && kForestThreads / R < tpr_min) R >>= 1;
-  }
-  const int tpr = kForestThreads / R;
+  // 16-B staging writes into rows padded to d + 4 words (conflict-free), and
+  // the row leader's flag and density loaded with the tile
   const bool vec4 = (d % 4 == 0) && (ldx % 4 == 0) && (reinterpret_cast<uintptr_t>(x) % 16 == 0);
-  bool pad4 = vec4;
-  if (const char* e = getenv("DAL_FOREST_PAD4")) pad4 = vec4 && atoi(e) != 0;  // timing knob (A/B runs)
-  bool pre = true;
-  if (const char* e = getenv("DAL_FOREST_PREFETCH")) pre = atoi(e) != 0;  // timing knob (A/B runs)
-  // LDS-DMA staging for wide rows (pad4: d % 4 == 0, ldx % 4 == 0, 16-B-aligned pool); narrow rows
-  // leave most lanes of each DMA instruction idle (2M x 32 x 100: 264 -> 290 us, 100k x 64: 18.4 -> 19.8)
-  bool dma = pad4 && d >= 128;
-  if (const char* e = getenv("DAL_FOREST_DMA")) dma = dma && atoi(e) != 0;  // timing knob (A/B runs)
-  const int x_floats = x_lds ? R * static_cast<int>(d + (pad4 ? 4 : 1)) : 0;
+  const bool pad4 = vec4, pre = true;
+  const int x_floats = T.x_lds ? R * static_cast<int>(d + (pad4 ? 4 : 1)) : 0;
   const int64_t n_inner = (int64_t{1} << depth) - 1, n_leaf = int64_t{1} << depth;
   const int64_t f_bytes = n_trees * (n_inner * 8 + n_leaf);
-  bool f_lds = f_bytes <= 65536;
-  if (const char* e = getenv("DAL_FOREST_FLDS")) f_lds = f_lds && atoi(e) != 0;  // timing knob (A/B runs)
+  // forest nodes from LDS whenever they fit (from global memory measured
+  // slower at every shape: 2M x 256 521 -> 566 us, config 3 46.6 -> 89.8 us)
+  const bool f_lds = f_bytes <= 65536;
   const int xf = static_cast<int>(round_up(x_floats, 4));  // forest region 16-B aligned
   size_t smem = static_cast<size_t>(xf) * 4 + (f_lds ? static_cast<size_t>(f_bytes) : 0);
-  const int64_t blocks = ceil_div(n, R);
   if (smem == 0) smem = 16;
   const dim3 grid(static_cast<unsigned>(blocks));
 #define DAL_FOREST_LAUNCH(XL, FL)                                                                   \
@@ -309,10 +357,10 @@ int forest_score_launch(const float* x, int64_t n, int64_t d, int64_t ldx, const
         hipSuccess)                                                                                 \
       return DAL_ERR_HIP;                                                                           \
     hipLaunchKernelGGL((forest_score_kernel<XL, FL>), grid, dim3(kForestThreads), smem, st, A, R,  \
-                       tpr, xf, vec4, pad4, pre, dma);                                                            \
+                       tpr, xf, vec4, pad4, pre, T.dma);                                            \
   } while (0)
-  if (x_lds && f_lds) DAL_FOREST_LAUNCH(true, true);
-  else if (x_lds) DAL_FOREST_LAUNCH(true, false);
+  if (T.x_lds && f_lds) DAL_FOREST_LAUNCH(true, true);
+  else if (T.x_lds) DAL_FOREST_LAUNCH(true, false);
   else if (f_lds) DAL_FOREST_LAUNCH(false, true);
   else DAL_FOREST_LAUNCH(false, false);
 #undef DAL_FOREST_LAUNCH

@@ -18,22 +18,28 @@
 //   sort             one 1024-thread block, bitonic on (key, index) in LDS.
 // HBM-bound: each pass reads 8 B/row.
 //
-// Truncated level 1 of the interval selections (dal_dw_select with
-// level1_passes = p in 1..5; small pools, where the 6 dependent radix
-// launches and the 3-launch ordered compaction are latency, not bytes):
-//   p x radix_hist   the first p digits of the k-th smallest pessimistic key
-//                    K: K lies in the resolved bucket, so tau = the bucket's
-//                    upper edge (prefix | all-ones below) satisfies tau >= K
-//                    and >= k pessimistic keys are <= tau;
-//   threshold_append every row whose OPTIMISTIC key is <= tau joins the
-//                    candidates (ballot + one atomic per wave; order does not
-//                    matter: the candidates are sorted by (exact key, row)).
+// Fast level 1 of the interval selections (dal_dw_select / dal_dw_step /
+// dal_maxcos_select with level1_passes > 0; cap <= DAL_SORT_CAP_PAYLOAD):
+//   row-group minima  the pool is cut into <= kMaxGroups row groups and each
+//                     group's minimum pessimistic and optimistic keys are
+//                     kept (written by dal_dw_step's score kernel itself, or by
+//                     one group_min_kernel pass);
+//   summary_select    every block derives tau = the k-th smallest group
+//                     minimum (a block radix select over <= 4096 keys); any k
+//                     keys of the pool bound the k-th smallest key K from above,
+//                     so tau >= K.  Only groups whose optimistic minimum is
+//                     <= tau are scanned; every row whose OPTIMISTIC key is
+//                     <= tau joins the candidates (with the density-weighted
+//                     selections, its canonical fp64 score is computed in
+//                     place) and the block that finishes last sorts them.
 // {optimistic <= tau} contains {optimistic <= K}, the exact path's candidate
-// set, so the selection is the same; 2 digits resolve a DW score to ~2^-11
-// relative, about the width of its density interval, so the candidate set
-// stays small.  More than cap candidates raises DAL_FLAG_SAMPLE_MISS (the
-// caller re-runs with level1_passes = 0).
+// set, so the selection is the same.  When the top-k rows lie in distinct
+// groups (k << groups) tau is within a few ranks of K, so the candidates are
+// about the rows whose score interval reaches the k-th score.  More than cap
+// candidates raises DAL_FLAG_SAMPLE_MISS (the caller re-runs with
+// level1_passes = 0).
 #include <algorithm>
+#include <cstddef>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -61,11 +67,11 @@ __host__ __device__ constexpr int digit_bins(int p) {
 }
 
 // Agent-scope relaxed loads / stores (global_load / global_store ... sc1):
-// the hand-offs between blocks of dw_level1_fused_kernel (histograms, level-1
-// state, candidates) are written and read only this way, so no release /
-// acquire fence is needed around its grid barriers (MI355X_MICROARCH.md,
-// "Valid forms": sc1 stores or agent atomics, vmcnt(0) + a workgroup barrier
-// before one lane's arrival, an sc1 poll, sc1 loads after a barrier).
+// the hand-off from the blocks of summary_select_kernel to the one that
+// arrives last (candidates, their count) is written and read only this way,
+// so no release / acquire fence is needed (MI355X_MICROARCH.md, "Valid
+// forms": sc1 stores or agent atomics, vmcnt(0) + a workgroup barrier before
+// one lane's arrival, sc1 loads after it).
 template <class T>
 __device__ __forceinline__ T ld_sc1(const T* p) {
   return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -82,18 +88,16 @@ __device__ __forceinline__ void st_sc1(double* p, double v) {
 }
 
 struct TopkHdr {
-  uint32_t hist[kPasses][kBins];
+  // fast level 1 (summary_select_kernel): candidate count, the blocks'
+  // arrival counter and tau -- the words a fast-path call needs zero
+  unsigned int cand_count, arrive;
+  unsigned long long kstar;
+  // exact path
+  unsigned long long kfinal, total_lt, total_eq;
+  unsigned int overflow, pad0;
   unsigned long long prefix[kPasses + 1];
   unsigned long long krem[kPasses + 1];
-  unsigned long long kstar, kfinal, total_lt, total_eq;
-  unsigned int cand_count, overflow, pad0, pad1;
-  // append_rerank_kernel: (rows with pessimistic key <= tau) << 32 | candidates,
-  // one 64-bit atomic per block sweep
-  unsigned long long packed;
-  unsigned long long pad2;
-  // dw_level1_fused_kernel: grid-barrier arrival counters (one per radix
-  // pass) and the final arrival counter (the last block sorts)
-  unsigned int bar[kPasses + 2];
+  uint32_t hist[kPasses][kBins];
 };
 
 struct TopkLayout {
@@ -537,84 +541,23 @@ __device__ __forceinline__ bool dw_canonical_score_lane(const DwRerank& R, int64
   return true;
 }
 
-// ---------------------------------------------------- truncated level 1 ----
-// dal_dw_step's fused re-rank target (append_rerank_kernel).
+// Re-rank target of summary_select_kernel's density-weighted form.
 struct AppendRerank {
   DwRerank R;
   uint64_t* ckey;
   double* cpay;
 };
 
-__global__ __launch_bounds__(kRadixThreads) void threshold_append_kernel(
-    const uint64_t* __restrict__ keys_lo, const uint64_t* __restrict__ keys_hi, int64_t n, int64_t idx_base,
-    int passes, TopkHdr* __restrict__ h, int64_t* __restrict__ cidx, int64_t cap) {
-  __shared__ uint32_t scan[kRadixThreads / 64];
-  __shared__ unsigned long long red[kRadixThreads / 64];
-  unsigned long long prefix, krem;
-  resolve_digit(h, passes - 1, prefix, krem, scan);
-  const int sh = digit_shift(passes - 1);
-  const unsigned long long tau = prefix | (sh ? ((1ull << sh) - 1ull) : 0ull);
-  const int tid = threadIdx.x, lane = tid & 63;
-  if (blockIdx.x == 0 && tid == 0) h->kstar = tau;
-  unsigned long long below = 0;
-  constexpr int kIlp = 8;  // keys per thread per sweep: their loads go out together
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kRadixThreads;
-  for (int64_t b0 = static_cast<int64_t>(blockIdx.x) * kRadixThreads; b0 < n; b0 += kIlp * stride) {
-    unsigned long long lo[kIlp], hi[kIlp];
-#pragma unroll
-    for (int j = 0; j < kIlp; ++j) {
-      const int64_t i = b0 + j * stride + tid;
-      lo[j] = i < n ? keys_lo[i] : DAL_KEY_NONE;
-      hi[j] = i < n ? keys_hi[i] : DAL_KEY_NONE;
-    }
-    bool cand[kIlp];
-    unsigned int nc = 0;
-#pragma unroll
-    for (int j = 0; j < kIlp; ++j) {
-      below += b0 + j * stride + tid < n && lo[j] <= tau;
-      cand[j] = hi[j] <= tau && hi[j] != DAL_KEY_NONE;
-      nc += cand[j];
-    }
-    // one slot reservation per wave and sweep for all its candidates
-    unsigned int incl = nc;
-    for (int o = 1; o < 64; o <<= 1) {
-      const unsigned int y = __shfl_up(incl, o);
-      if (lane >= o) incl += y;
-    }
-    const unsigned int tot = __shfl(incl, 63);
-    if (!tot) continue;
-    unsigned int base = 0;
-    if (lane == 0) base = atomicAdd(&h->cand_count, tot);
-    int64_t pos = static_cast<int64_t>(__shfl(base, 0)) + (incl - nc);
-#pragma unroll
-    for (int j = 0; j < kIlp; ++j) {
-      if (cand[j]) {
-        if (pos < cap) cidx[pos] = idx_base + b0 + j * stride + tid;
-        ++pos;
-      }
-    }
-  }
-  for (int o = 32; o > 0; o >>= 1) below += __shfl_xor(below, o);
-  if (lane == 0) red[tid >> 6] = below;
-  __syncthreads();
-  if (tid == 0) {
-    unsigned long long t = 0;
-    for (int w = 0; w < kRadixThreads / 64; ++w) t += red[w];
-    atomicAdd(&h->total_lt, t);
-  }
-}
-
 // One wave per candidate slot (dw_canonical_score_wave).
 __global__ __launch_bounds__(256) void rerank_kernel(const TopkHdr* __restrict__ h, int64_t idx_base, DwRerank R,
                                                      uint64_t* __restrict__ ckey,
                                                      const int64_t* __restrict__ cidx,
                                                      double* __restrict__ cpay, int64_t cap,
-                                                     int64_t need_k, int32_t* __restrict__ status) {
+                                                     bool cap_miss, int32_t* __restrict__ status) {
   const int64_t c = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   const bool lead = (threadIdx.x & 63) == 0;
-  if (need_k && c == 0 && lead &&
-      (h->total_lt < static_cast<unsigned long long>(need_k) || h->cand_count > cap))
-    atomicOr(status, DAL_FLAG_SAMPLE_MISS);  // truncated level 1 over capacity: the caller re-runs exactly
+  if (cap_miss && c == 0 && lead && h->cand_count > cap)
+    atomicOr(status, DAL_FLAG_SAMPLE_MISS);  // fast level 1 over capacity: the caller re-runs exactly
   if (c >= cap) return;
   if (c >= h->cand_count) {
     if (lead) ckey[c] = DAL_KEY_NONE;
@@ -650,16 +593,15 @@ __global__ __launch_bounds__(256) void rerank_maxcos_kernel(const TopkHdr* __res
                                                             int64_t m, uint64_t* __restrict__ ckey,
                                                             const int64_t* __restrict__ cidx,
                                                             double* __restrict__ cpay, int64_t cap,
-                                                            int64_t need_k, int32_t* __restrict__ status) {
+                                                            bool cap_miss, int32_t* __restrict__ status) {
   __shared__ double su[256][kRrC];  // [f][candidate]
   __shared__ double rb[4][kRrC];
   __shared__ long long ra[4][kRrC];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t c0 = static_cast<int64_t>(blockIdx.x) * kRrC;
   const int64_t count = h->cand_count;
-  if (need_k && c0 == 0 && tid == 0 &&
-      (h->total_lt < static_cast<unsigned long long>(need_k) || h->cand_count > cap))
-    atomicOr(status, DAL_FLAG_SAMPLE_MISS);  // truncated level 1 over capacity: the caller re-runs exactly
+  if (cap_miss && c0 == 0 && tid == 0 && h->cand_count > cap)
+    atomicOr(status, DAL_FLAG_SAMPLE_MISS);  // fast level 1 over capacity: the caller re-runs exactly
   if (c0 >= count) {
     if (tid < kRrC && c0 + tid < cap) ckey[c0 + tid] = DAL_KEY_NONE;
     return;
@@ -772,11 +714,12 @@ __global__ __launch_bounds__(256) void gather_selected_kernel(const int64_t* __r
 }
 
 // ---------------------------------------------------------------- sort ----
-// Fused-step tail (dal_dw_step): the truncated level 1's capacity check
-// (need_k > 0: fewer than k pessimistic keys <= tau or more than cap
-// candidates -> DAL_FLAG_SAMPLE_MISS), the candidate count clamped to cap, and
-// the level-1 header cleared once every thread has read it, so the next call
-// (a replayed hipGraph) starts from a zero header without a memset launch.
+// Fast-level-1 tail (summary_select_kernel): the candidate capacity check
+// (more than cap candidates -> DAL_FLAG_SAMPLE_MISS: the caller re-runs with
+// the exact level 1), and the words the next call needs zero -- the level-1
+// counters and, when the score kernel folded its group minima with atomics,
+// the minima -- cleared once every thread has read them, so a replayed
+// hipGraph starts clean without a memset launch.
 // Plan publishing (dal_dw_plan_run): out_slot points at two host-mapped
 // words holding the device addresses the selected indices and scores are
 // also written to (fresh tensors per step; NULL: none), status_mirror at a
@@ -784,13 +727,14 @@ __global__ __launch_bounds__(256) void gather_selected_kernel(const int64_t* __r
 // after its stream sync, with no copy launches after the graph.
 struct SortTail {
   int64_t cap = 0;
-  int64_t need_k = 0;
+  bool cap_miss = false;
   int32_t* status = nullptr;
   uint32_t* clear = nullptr;
   int64_t clear_words = 0;
+  uint32_t* clear2 = nullptr;
+  int64_t clear2_words = 0;
   int64_t* const* out_slot = nullptr;
   int32_t* status_mirror = nullptr;
-  bool packed = false;  // counts in TopkHdr::packed (append_rerank_kernel)
 };
 
 __device__ __forceinline__ int64_t* load_out_slot(int64_t* const* slot, int which) {
@@ -925,7 +869,7 @@ __device__ bool select_compact(const uint64_t* __restrict__ keys, const int64_t*
 }
 
 // The sort tail as a block-level device function (kSortThreads threads): the
-// body of sort_kernel, also run by the last block of dw_level1_fused_kernel.
+// body of sort_kernel, also run by the last block of summary_select_kernel.
 template <bool PAY>
 __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t* __restrict__ idx,
                                const double* __restrict__ pay, const TopkHdr* __restrict__ h, int64_t n_static,
@@ -938,12 +882,8 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
   __shared__ int64_t* s_dest[2];
   const int tid = threadIdx.x;
   if (tid < 2) s_dest[tid] = load_out_slot(tail.out_slot, tid);  // host round trips, overlapping the sort
-  const unsigned long long packed = tail.packed ? ld_sc1(&h->packed) : 0ull;
-  int64_t m = !h ? n_static : tail.packed ? static_cast<int64_t>(packed & 0xFFFFFFFFull)
-                                          : static_cast<int64_t>(ld_sc1(&h->cand_count));
-  const unsigned long long total_lt = !h ? 0ull : tail.packed ? (packed >> 32) : ld_sc1(&h->total_lt);
-  if (tail.need_k && tid == 0 && (total_lt < static_cast<unsigned long long>(tail.need_k) || m > tail.cap))
-    atomicOr(tail.status, DAL_FLAG_SAMPLE_MISS);
+  int64_t m = !h ? n_static : static_cast<int64_t>(ld_sc1(&h->cand_count));
+  if (tail.cap_miss && tid == 0 && m > tail.cap) atomicOr(tail.status, DAL_FLAG_SAMPLE_MISS);
   if (tail.cap && m > tail.cap) m = tail.cap;
   if (m > CAP) m = CAP;
   // Large candidate lists (config 3: ~4,000): a block radix select of the
@@ -964,6 +904,7 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
     __syncthreads();
     if (tail.clear) {  // every thread read the header above
       for (int64_t w = tid; w < tail.clear_words; w += kSortThreads) tail.clear[w] = 0u;
+      for (int64_t w = tid; w < tail.clear2_words; w += kSortThreads) tail.clear2[w] = 0u;
     }
     int64_t* const di = s_dest[0];
     double* const ds = reinterpret_cast<double*>(s_dest[1]);
@@ -1048,6 +989,7 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
   }
   if (tail.clear) {  // every thread read the header before the first barrier above
     for (int64_t w = tid; w < tail.clear_words; w += kSortThreads) tail.clear[w] = 0u;
+    for (int64_t w = tid; w < tail.clear2_words; w += kSortThreads) tail.clear2[w] = 0u;
   }
   int64_t* const di = s_dest[0];  // written before the first barrier
   double* const ds = reinterpret_cast<double*>(s_dest[1]);
@@ -1088,261 +1030,260 @@ __global__ __launch_bounds__(kSortThreads) void sort_kernel(const uint64_t* __re
   sort_tail_body<PAY>(keys, idx, pay, h, n_static, k, out_keys, out_idx, out_pay, tail);
 }
 
-// ------------------------------------------------ fused level 1 (one launch) ----
-// The truncated level 1 + candidate append with in-place canonical re-rank +
-// the final sort in ONE launch: `passes` radix histogram sweeps over the
-// pessimistic keys, each closed by a grid barrier (every block then resolves
-// the digit itself from the global histogram), the append sweep (rows whose
-// optimistic key is <= tau, re-ranked by their wave), and the block that
-// arrives last sorts the candidates (sort_tail_body) and clears the header.
-// The grid is at most half the CUs with one block per CU (the sort arrays
-// take ~100 KiB of LDS), so every block of the launch is resident even with
-// a second process on the GPU; a barrier still unmet after ~0.1 s raises
-// DAL_FLAG_SAMPLE_MISS and the blocks finish, so the launch always drains
-// (the caller re-runs with the exact level 1).  Requires a zero header.
-constexpr int kFuseThreads = kSortThreads;  // 1024: the last block runs the sort tail
-constexpr unsigned kSpinLimit = 1u << 17;
+// ------------------------------------- fast level 1 (row-group minima) ----
+constexpr int kMaxGroups = 4096;             // row groups of the fast level 1
+constexpr int kSumThreads = kSortThreads;    // 1024: the last block runs the sort tail
 
-// All blocks of the grid: every global store / atomic of this block issued
-// before the call is complete (vmcnt(0) in every wave, then a workgroup
-// barrier) before one lane's arrival; the wait is an sc1 poll, and the
-// blocks read the handed-off words with sc1 loads only.  Returns false when
-// the wait timed out (the caller then discards the launch's result).
-__device__ bool grid_barrier(unsigned int* ctr, unsigned int G, int32_t* status) {
-  __shared__ int s_ok;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int ok = 1;
-    unsigned spins = 0;
-    while (ld_sc1(ctr) < G) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > kSpinLimit) {
-        ok = 0;
-        break;
-      }
-    }
-    if (!ok) atomicOr(status, DAL_FLAG_SAMPLE_MISS);
-    s_ok = ok;
-  }
-  __syncthreads();
-  return s_ok != 0;
-}
+// ginv[g] = ~(minimum pessimistic key of group g), ginv[ng + g] = ~(minimum
+// optimistic key): inverted so that a zeroed buffer reads DAL_KEY_NONE and an
+// atomic max folds a minimum.  Group g = rows [g * group_rows, ...).
+struct GroupSummary {
+  const uint64_t* ginv;
+  int64_t ng;
+  int64_t group_rows;
+};
 
-// resolve_digit for kFuseThreads threads (2 bins each)
-__device__ void resolve_digit_fused(const TopkHdr* h, int p, unsigned long long& prefix, unsigned long long& krem) {
-  constexpr int BPT = kBins / kFuseThreads;
-  constexpr int W = kFuseThreads / 64;
-  __shared__ uint32_t sh[W];
-  __shared__ unsigned long long s_pre, s_krem;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const unsigned long long kr = ld_sc1(&h->krem[p]);
-  const int nb = digit_bins(p);
-  uint32_t c[BPT];
-  uint32_t tot = 0;
+// tau = the k-th smallest of the groups' minimum pessimistic keys (NONE when
+// k > ng): k group minima are k keys of the pool, so at least k keys are
+// <= tau, i.e. tau >= K.  Block radix select (8-bit digits MSB first, up to
+// 4 keys per thread in registers) until the k-th key's bucket holds <= 64
+// keys, which one wave then ranks.  Every block computes it (no grid sync).
+__device__ unsigned long long group_threshold(const GroupSummary& S, int64_t k) {
+  constexpr int PER = kMaxGroups / kSumThreads;
+  __shared__ unsigned int hist[256];
+  __shared__ unsigned long long s_prefix, s_tau;
+  __shared__ unsigned int s_krem, s_cnt, s_n;
+  __shared__ unsigned long long s_bucket[64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (k > S.ng) return DAL_KEY_NONE;
+  unsigned long long key[PER];
 #pragma unroll
-  for (int j = 0; j < BPT; ++j) {
-    const int b = tid * BPT + j;
-    c[j] = b < nb ? ld_sc1(&h->hist[p][b]) : 0u;
-    tot += c[j];
+  for (int j = 0; j < PER; ++j) {
+    const int64_t g = tid + static_cast<int64_t>(j) * kSumThreads;
+    key[j] = g < S.ng ? ~S.ginv[g] : 0ull;
   }
-  uint32_t x = tot;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) sh[w] = x;
-  __syncthreads();
-  uint32_t excl = x - tot;
-  for (int i = 0; i < w; ++i) excl += sh[i];
-  if (excl < kr && excl + tot >= kr) {
-    uint32_t run = excl;
-#pragma unroll
-    for (int j = 0; j < BPT; ++j) {
-      if (run < kr && run + c[j] >= kr) {
-        s_pre = ld_sc1(&h->prefix[p]) | (static_cast<unsigned long long>(tid * BPT + j) << digit_shift(p));
-        s_krem = kr - run;
-      }
-      run += c[j];
-    }
-  }
-  __syncthreads();
-  prefix = s_pre;
-  krem = s_krem;
-  __syncthreads();
-}
-
-__global__ __launch_bounds__(kFuseThreads) void dw_level1_fused_kernel(
-    const uint64_t* __restrict__ keys_lo, const uint64_t* __restrict__ keys_hi, int64_t n, int64_t k,
-    int64_t idx_base, int passes, TopkHdr* __restrict__ h, int64_t* __restrict__ cidx, int64_t cap, AppendRerank AR,
-    int n_lut, int32_t* __restrict__ status, uint64_t* __restrict__ out_keys, int64_t* __restrict__ out_idx,
-    double* __restrict__ out_scores, SortTail tail) {
-  constexpr int W = kFuseThreads / 64;
-  __shared__ uint32_t hist[kBins];
-  __shared__ unsigned s_last;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const unsigned G = gridDim.x;
-  const int64_t stride = static_cast<int64_t>(G) * kFuseThreads;
-  const int64_t i0 = static_cast<int64_t>(blockIdx.x) * kFuseThreads + tid;
-  bool ok = true;
-  unsigned long long prefix = 0, krem = static_cast<unsigned long long>(k);
-  // ---- radix passes: histogram of digit p among keys matching the prefix
-  for (int p = 0; p < passes; ++p) {
-    if (p > 0) resolve_digit_fused(h, p - 1, prefix, krem);
-    if (blockIdx.x == 0 && tid == 0) {
-      st_sc1(&h->prefix[p], prefix);
-      st_sc1(&h->krem[p], krem);
-    }
-#pragma unroll
-    for (int j = 0; j < kBins / kFuseThreads; ++j) hist[j * kFuseThreads + tid] = 0;
+  auto live = [&](int j) { return tid + static_cast<int64_t>(j) * kSumThreads < S.ng; };
+  unsigned long long prefix = 0, mask = 0;
+  unsigned int krem = static_cast<unsigned int>(k), cnt = static_cast<unsigned int>(S.ng);
+  for (int pass = 0; pass < 8 && cnt > 64; ++pass) {
+    const int shift = 56 - 8 * pass;
+    if (tid < 256) hist[tid] = 0u;
     __syncthreads();
-    const int shift = digit_shift(p);
-    const unsigned long long dmask = static_cast<unsigned long long>(digit_bins(p) - 1);
-    const unsigned long long hmask = p == 0 ? 0ull : (~0ull << (64 - kDigitBits * p));
-    for (int64_t ib = i0 - tid; ib < n; ib += 4 * stride) {  // 4 keys per thread in flight (block-uniform trip)
-      unsigned long long kb[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t i = ib + j * stride + tid;
-        kb[j] = i < n ? keys_lo[i] : 0ull;
+    for (int j = 0; j < PER; ++j) {
+      const bool valid = live(j) && (key[j] & mask) == prefix;
+      const unsigned bin = static_cast<unsigned>((key[j] >> shift) & 255ull);
+      const unsigned long long vm = __ballot(valid);
+      if (vm) {  // the wave's most common bin (the first valid lane's) with one atomic
+        const int first = __ffsll(static_cast<long long>(vm)) - 1;
+        const unsigned b0 = __shfl(bin, first);
+        const unsigned long long m0 = __ballot(valid && bin == b0);
+        if (lane == first) atomicAdd(&hist[b0], static_cast<unsigned>(__popcll(m0)));
+        if (valid && bin != b0) atomicAdd(&hist[bin], 1u);
       }
+    }
+    __syncthreads();
+    if (tid < 64) {  // one wave: 4 bins per lane, inclusive scan, locate krem
+      unsigned c[4], tot = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const bool valid = ib + j * stride + tid < n && (kb[j] & hmask) == prefix;
-        const unsigned bin = static_cast<unsigned>((kb[j] >> shift) & dmask);
-        const unsigned long long vm = __ballot(valid);
-        if (vm) {
-          const int first = __ffsll(static_cast<long long>(vm)) - 1;
-          const unsigned b0 = __shfl(bin, first);
-          const unsigned long long m0 = __ballot(valid && bin == b0);
-          if (lane == first) atomicAdd(&hist[b0], static_cast<unsigned>(__popcll(m0)));
-          if (valid && bin != b0) atomicAdd(&hist[bin], 1u);
+      for (int q = 0; q < 4; ++q) {
+        c[q] = hist[lane * 4 + q];
+        tot += c[q];
+      }
+      unsigned x = tot;
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+      }
+      unsigned run = x - tot;
+      if (run < krem && run + tot >= krem) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (run < krem && run + c[q] >= krem) {
+            s_prefix = prefix | (static_cast<unsigned long long>(lane * 4 + q) << shift);
+            s_krem = krem - run;
+            s_cnt = c[q];
+          }
+          run += c[q];
         }
       }
     }
     __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kBins / kFuseThreads; ++j) {
-      const int b = j * kFuseThreads + tid;
-      const uint32_t v = hist[b];
-      if (v) atomicAdd(&h->hist[p][b], v);
-    }
-    ok = grid_barrier(&h->bar[p], G, status) && ok;
+    prefix = s_prefix;
+    krem = s_krem;
+    cnt = s_cnt;
+    mask |= 255ull << shift;
   }
-  resolve_digit_fused(h, passes - 1, prefix, krem);
-  const int sh = digit_shift(passes - 1);
-  const unsigned long long tau = prefix | (sh ? ((1ull << sh) - 1ull) : 0ull);
-  if (blockIdx.x == 0 && tid == 0) h->kstar = tau;
-  // ---- append with the in-place canonical re-rank: rows whose optimistic
-  // key is <= tau.  The block's rows (4 per thread per super-sweep) are
-  // counted first, the block reserves its slots with ONE packed atomic
-  // (candidates | rows with pessimistic key <= tau), then a second sweep
-  // (L2-hot keys) scores and writes the candidates -- one atomic round trip
-  // per block instead of one per sweep.
-  constexpr int J = 4;
-  constexpr int kMaxSw = 32;  // super-sweeps per count / write round
-  __shared__ unsigned s_cnt[kMaxSw * W];
-  __shared__ unsigned s_wsum[W];
-  __shared__ unsigned long long s_base;
-  const double lut_lane = lane < n_lut ? AR.R.lut[lane] : 0.0;
-  const unsigned long long lt_mask = (1ull << lane) - 1ull;
-  const int64_t b_first = static_cast<int64_t>(blockIdx.x) * kFuseThreads;
-  const int64_t sw_rows = J * stride;  // rows between a thread's super-sweeps
-  for (int64_t r0 = b_first; ok && r0 < n; r0 += kMaxSw * sw_rows) {  // block-uniform
-    const int n_sw = static_cast<int>(std::min<int64_t>(kMaxSw, ceil_div(n - r0, sw_rows)));
-    // count pass
-    unsigned below_w = 0;
-    for (int sw = 0; sw < n_sw; ++sw) {
-      const int64_t base_i = r0 + sw * sw_rows + tid;
-      unsigned cw = 0;
+  if (mask == ~0ull) return prefix;  // all 64 bits resolved (equal keys)
+  if (tid == 0) s_n = 0u;
+  __syncthreads();
 #pragma unroll
-      for (int j = 0; j < J; ++j) {
-        const int64_t i = base_i + j * stride;
-        const bool valid = i < n;
-        const unsigned long long lo = valid ? keys_lo[i] : DAL_KEY_NONE;
-        const unsigned long long hi = valid ? keys_hi[i] : DAL_KEY_NONE;
-        cw += static_cast<unsigned>(__popcll(__ballot(valid && hi <= tau && hi != DAL_KEY_NONE)));
-        below_w += static_cast<unsigned>(__popcll(__ballot(valid && lo <= tau)));
+  for (int j = 0; j < PER; ++j)
+    if (live(j) && (key[j] & mask) == prefix) s_bucket[atomicAdd(&s_n, 1u)] = key[j];
+  __syncthreads();
+  if (tid < 64) {  // rank the bucket's keys: the krem-th smallest is tau
+    const unsigned long long mine = lane < static_cast<int>(cnt) ? s_bucket[lane] : 0ull;
+    unsigned lt = 0, le = 0;
+    for (unsigned j = 0; j < cnt; ++j) {
+      const unsigned long long o = s_bucket[j];
+      lt += o < mine;
+      le += o <= mine;
+    }
+    if (lane < static_cast<int>(cnt) && lt < krem && krem <= le) s_tau = mine;  // (equal keys: same value)
+  }
+  __syncthreads();
+  return s_tau;
+}
+
+// Group minima of the keys (the standalone selections; dal_dw_step's score
+// kernel writes them itself on pools of >= 2k blocks): groups of >= 64 rows
+// take one wave each (8 x 64 keys in flight), smaller groups one lane each.
+// Block 0 also zeroes the fast-path header words.
+__global__ __launch_bounds__(256) void group_min_kernel(const uint64_t* __restrict__ keys_lo,
+                                                        const uint64_t* __restrict__ keys_hi, int64_t n,
+                                                        int64_t group_rows, int64_t ng, uint64_t* __restrict__ ginv,
+                                                        uint32_t* __restrict__ zero, int64_t zero_words) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  if (blockIdx.x == 0 && zero)
+    for (int64_t w = tid; w < zero_words; w += 256) zero[w] = 0u;
+  unsigned long long lo = DAL_KEY_NONE, hi = DAL_KEY_NONE;
+  if (group_rows < 64) {  // a lane per group
+    const int64_t g = static_cast<int64_t>(blockIdx.x) * 256 + tid;
+    if (g >= ng) return;
+    const int64_t r0 = g * group_rows, r1 = r0 + group_rows < n ? r0 + group_rows : n;
+    for (int64_t i = r0; i < r1; ++i) {
+      const unsigned long long a = keys_lo[i], c = keys_hi[i];
+      lo = a < lo ? a : lo;
+      hi = c < hi ? c : hi;
+    }
+    ginv[g] = ~lo;
+    ginv[ng + g] = ~hi;
+    return;
+  }
+  const int64_t g = static_cast<int64_t>(blockIdx.x) * 4 + (tid >> 6);  // a wave per group
+  if (g >= ng) return;
+  const int64_t r0 = g * group_rows;
+  const int64_t r1 = r0 + group_rows < n ? r0 + group_rows : n;
+  constexpr int kIlp = 8;
+  for (int64_t b = r0; b < r1; b += kIlp * 64) {
+    unsigned long long a[kIlp], c[kIlp];
+#pragma unroll
+    for (int j = 0; j < kIlp; ++j) {
+      const int64_t i = b + j * 64 + lane;
+      a[j] = i < r1 ? keys_lo[i] : DAL_KEY_NONE;
+      c[j] = i < r1 ? keys_hi[i] : DAL_KEY_NONE;
+    }
+#pragma unroll
+    for (int j = 0; j < kIlp; ++j) {
+      lo = a[j] < lo ? a[j] : lo;
+      hi = c[j] < hi ? c[j] : hi;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long a = __shfl_xor(lo, o), c = __shfl_xor(hi, o);
+    lo = a < lo ? a : lo;
+    hi = c < hi ? c : hi;
+  }
+  if (lane == 0) {
+    ginv[g] = ~lo;
+    ginv[ng + g] = ~hi;
+  }
+}
+
+// The fast level 1 over the group minima (see the top of the file).  Block b
+// owns groups [b * per, (b + 1) * per): those whose optimistic minimum is
+// <= tau are listed in LDS and scanned by the block's waves (a group's rows,
+// 8 x 64 keys in flight per wave); each 64-row slice with candidates reserves
+// its slots with one atomic.  DW: each candidate's canonical fp64 score is
+// computed in place (<= 2 per slice: the whole wave per candidate; more: one
+// lane each), and the block that arrives last sorts the candidates
+// (sort_tail_body: capacity check, selection, header clear).  !DW: indices
+// only (a separate re-rank follows).
+template <bool DW>
+__global__ __launch_bounds__(kSumThreads) void summary_select_kernel(
+    const uint64_t* __restrict__ keys_hi, int64_t n, int64_t k, int64_t idx_base, GroupSummary S,
+    TopkHdr* __restrict__ h, int64_t* __restrict__ cidx, int64_t cap, AppendRerank AR, int n_lut,
+    uint64_t* __restrict__ out_keys, int64_t* __restrict__ out_idx, double* __restrict__ out_scores, SortTail tail) {
+  constexpr int W = kSumThreads / 64;
+  __shared__ int s_hits[kMaxGroups / 32];  // per <= 128 groups (summary_grid)
+  __shared__ unsigned s_nh, s_last;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const unsigned long long tau = group_threshold(S, k);
+  if (blockIdx.x == 0 && tid == 0) h->kstar = tau;
+  const int64_t per = ceil_div(S.ng, static_cast<int64_t>(gridDim.x));
+  const int64_t g0 = static_cast<int64_t>(blockIdx.x) * per;
+  const int64_t g1 = g0 + per < S.ng ? g0 + per : S.ng;
+  if (tid == 0) s_nh = 0u;
+  __syncthreads();
+  for (int64_t g = g0 + tid; g < g1; g += kSumThreads) {
+    const unsigned long long m = ~S.ginv[S.ng + g];
+    if (m <= tau && m != DAL_KEY_NONE) s_hits[atomicAdd(&s_nh, 1u)] = static_cast<int>(g);
+  }
+  __syncthreads();
+  const int nh = static_cast<int>(s_nh);
+  const double lut_lane = DW && lane < n_lut ? AR.R.lut[lane] : 0.0;
+  const unsigned long long lt_mask = (1ull << lane) - 1ull;
+  constexpr int kIlp = 8;
+  for (int q = w; q < nh; q += W) {
+    const int64_t r0 = static_cast<int64_t>(s_hits[q]) * S.group_rows;
+    const int64_t r1 = r0 + S.group_rows < n ? r0 + S.group_rows : n;
+    for (int64_t b = r0; b < r1; b += kIlp * 64) {
+      unsigned long long hk[kIlp];
+#pragma unroll
+      for (int j = 0; j < kIlp; ++j) {
+        const int64_t i = b + j * 64 + lane;
+        hk[j] = i < r1 ? keys_hi[i] : DAL_KEY_NONE;
       }
-      if (lane == 0) s_cnt[sw * W + w] = cw;
-    }
-    if (lane == 0) s_wsum[w] = below_w;
-    __syncthreads();
-    // exclusive scan of the (super-sweep, wave) counts, row-major: thread e
-    const int ne = n_sw * W;
-    unsigned cnt_e = tid < ne ? s_cnt[tid] : 0u;
-    unsigned x = cnt_e;
-    for (int o = 1; o < 64; o <<= 1) {
-      const unsigned y = __shfl_up(x, o);
-      if (lane >= o) x += y;
-    }
-    __shared__ unsigned s_wtot[W];
-    if (lane == 63) s_wtot[w] = x;
-    __syncthreads();
-    unsigned excl = x - cnt_e;
-    for (int q = 0; q < w; ++q) excl += s_wtot[q];
-    if (tid == 0) {
-      unsigned tot_c = 0, tot_b = 0;
-      for (int q = 0; q < W; ++q) {
-        tot_c += s_wtot[q];
-        tot_b += s_wsum[q];
-      }
-      s_base = (tot_c | tot_b) ? atomicAdd(&h->packed, (static_cast<unsigned long long>(tot_b) << 32) | tot_c) : 0ull;
-    }
-    __syncthreads();
-    if (tid < ne) s_cnt[tid] = excl;  // (every thread read its count above)
-    __syncthreads();
-    const int64_t base = static_cast<int64_t>(static_cast<unsigned>(s_base & 0xFFFFFFFFull));
-    // write pass: the same rows in the same order
-    for (int sw = 0; sw < n_sw; ++sw) {
-      const int64_t base_i = r0 + sw * sw_rows + tid;
-      int64_t pos = base + s_cnt[sw * W + w];
+      unsigned cbits = 0;  // bit j: this lane's row of slice j is a candidate
+#pragma unroll
+      for (int j = 0; j < kIlp; ++j) cbits |= (hk[j] <= tau && hk[j] != DAL_KEY_NONE ? 1u : 0u) << j;
+      if (!__ballot(cbits != 0)) continue;
 #pragma unroll 1
-      for (int j = 0; j < J; ++j) {
-        const int64_t i = base_i + j * stride;
-        const bool valid = i < n;
-        const unsigned long long hi = valid ? keys_hi[i] : DAL_KEY_NONE;
-        const bool cand = valid && hi <= tau && hi != DAL_KEY_NONE;
+      for (int j = 0; j < kIlp; ++j) {
+        const int64_t i = b + j * 64 + lane;
+        const bool cand = (cbits >> j) & 1u;
         const unsigned long long cm = __ballot(cand);
         if (!cm) continue;
-        double my_s = 0.0;
-        bool my_ok = false;
-        if (__popcll(cm) > 2) {
-          const int v = cand ? AR.R.votes[i] : 0;
-          const double e = n_lut ? __shfl(lut_lane, v) : 0.0;
-          if (cand) my_ok = dw_canonical_score_lane<8>(AR.R, i, my_s, e, n_lut);
-        } else {
-          for (unsigned long long t = cm; t;) {
-            const int l = __ffsll(static_cast<long long>(t)) - 1;
-            t &= t - 1;
-            double sc;
-            const bool okl = dw_canonical_score_wave(AR.R, i - lane + l, sc, lut_lane, n_lut);
-            if (lane == l) {
-              my_s = sc;
-              my_ok = okl;
+        unsigned base = 0;
+        if (lane == 0) base = atomicAdd(&h->cand_count, static_cast<unsigned>(__popcll(cm)));
+        const int64_t p = static_cast<int64_t>(__shfl(base, 0)) + __popcll(cm & lt_mask);
+        if constexpr (DW) {
+          double my_s = 0.0;
+          bool my_ok = false;
+          if (__popcll(cm) > 2) {
+            const int v = cand ? AR.R.votes[i] : 0;
+            const double e = n_lut ? __shfl(lut_lane, v) : 0.0;
+            if (cand) my_ok = dw_canonical_score_lane<8>(AR.R, i, my_s, e, n_lut);
+          } else {
+            for (unsigned long long t = cm; t;) {
+              const int l = __ffsll(static_cast<long long>(t)) - 1;
+              t &= t - 1;
+              double sc;
+              const bool okl = dw_canonical_score_wave(AR.R, i - lane + l, sc, lut_lane, n_lut);
+              if (lane == l) {
+                my_s = sc;
+                my_ok = okl;
+              }
             }
           }
-        }
-        if (cand) {
-          const int64_t p = pos + __popcll(cm & lt_mask);
-          if (p < cap) {
+          if (cand && p < cap) {
             st_sc1(cidx + p, static_cast<int64_t>(idx_base + i));
             st_sc1(AR.cpay + p, my_s);
             st_sc1(AR.ckey + p, static_cast<uint64_t>(my_ok ? score_key(my_s, DAL_DESCENDING) : DAL_KEY_NONE));
           }
+        } else {
+          if (cand && p < cap) cidx[p] = idx_base + i;
         }
-        pos += __popcll(cm);
       }
     }
-    __syncthreads();  // s_cnt / s_base are rewritten by the next round
   }
-  // ---- the last block to arrive sorts the candidates
+  if constexpr (!DW) return;
+  // the last block to arrive sorts the candidates
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    const unsigned old = __hip_atomic_fetch_add(&h->bar[kPasses + 1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = old == G - 1;  // the returned value: every other block's stores are complete
+    const unsigned old = __hip_atomic_fetch_add(&h->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old == gridDim.x - 1;  // the returned value: every other block's stores are complete
   }
   __syncthreads();
   if (!s_last) return;
@@ -1360,34 +1301,41 @@ __global__ __launch_bounds__(256) void zero_words_kernel(uint32_t* __restrict__ 
 
 constexpr int64_t kHdrWords = sizeof(TopkHdr) / 4;
 static_assert(sizeof(TopkHdr) % 4 == 0, "header is whole words");
+constexpr int64_t kFastHdrWords = offsetof(TopkHdr, kfinal) / 4;  // cand_count, arrive, kstar
 
-void zero_header(TopkHdr* h, hipStream_t st) {
-  hipLaunchKernelGGL(zero_words_kernel, dim3(static_cast<unsigned>(ceil_div(kHdrWords, 256 * 4))), dim3(256), 0, st,
-                     reinterpret_cast<uint32_t*>(h), kHdrWords);
+void zero_words(uint32_t* p, int64_t words, hipStream_t st) {
+  hipLaunchKernelGGL(zero_words_kernel, dim3(static_cast<unsigned>(ceil_div(words, 256 * 4))), dim3(256), 0, st, p,
+                     words);
 }
 
-// dw_level1_fused_kernel's grid: ~4 keys per thread per sweep, at most half
-// the CUs (one block per CU: every block resident even beside a second
-// process on the GPU -- the grid barriers need the whole grid running).
-int fused_grid(int64_t n) {
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 2)
-    cus = 2;
-  const int64_t g = ceil_div(n, static_cast<int64_t>(kFuseThreads) * 4);
-  const int64_t gmax = cus / 2;
-  return static_cast<int>(g < 1 ? 1 : (g > gmax ? gmax : g));
+void zero_header(TopkHdr* h, hipStream_t st) { zero_words(reinterpret_cast<uint32_t*>(h), kHdrWords, st); }
+
+// Row groups of the fast level 1: whole blocks of `unit` rows, at most
+// kMaxGroups groups.
+GroupSummary make_groups(const uint64_t* ginv, int64_t n, int64_t unit) {
+  const int64_t units = ceil_div(n, unit);
+  const int64_t per = ceil_div(units, kMaxGroups);
+  return GroupSummary{ginv, ceil_div(units, per), per * unit};
 }
 
-int launch_fused_level1(const uint64_t* keys_lo, const uint64_t* keys_hi, int64_t n, int64_t k, int64_t idx_base,
-                        int passes, TopkHdr* h, int64_t* cidx, int64_t cap, const AppendRerank& AR, int n_lut,
-                        int32_t* status, uint64_t* out_keys, int64_t* out_idx, double* out_scores,
-                        const SortTail& tail, hipStream_t st) {
-  hipLaunchKernelGGL(dw_level1_fused_kernel, dim3(static_cast<unsigned>(fused_grid(n))), dim3(kFuseThreads), 0, st,
-                     keys_lo, keys_hi, n, k, idx_base, passes, h, cidx, cap, AR, n_lut, status, out_keys, out_idx,
-                     out_scores, tail);
-  DAL_RETURN_IF_LAUNCH_FAILED();
-  return DAL_OK;
+// The minima of both keys over kMaxGroups (or n) groups, by group_min_kernel
+// (which also zeroes `zero_words` words at `zero`).
+GroupSummary launch_group_min(const uint64_t* keys_lo, const uint64_t* keys_hi, int64_t n, uint64_t* ginv,
+                              uint32_t* zero, int64_t zero_words, hipStream_t st) {
+  const GroupSummary S = make_groups(ginv, n, 1);
+  const int64_t blocks = S.group_rows < 64 ? ceil_div(S.ng, 256) : ceil_div(S.ng, 4);
+  hipLaunchKernelGGL(group_min_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, keys_lo, keys_hi, n,
+                     S.group_rows, S.ng, ginv, zero, zero_words);
+  return S;
+}
+
+// summary_select_kernel's grid: <= 128 groups per block (each block derives
+// tau itself; 32 blocks x 128 = kMaxGroups), so a block's hits fit its list.
+int summary_grid(int64_t ng) {
+  int64_t g = ceil_div(ng, 128);
+  if (g > 32) g = 32;
+  if (g < 1) g = 1;
+  return static_cast<int>(g);
 }
 
 // Radix passes 0 .. passes-1 (zero: clear the header first).
@@ -1457,49 +1405,95 @@ extern "C" int dal_topk(const uint64_t* keys, int64_t n, int64_t k, int64_t idx_
 }
 
 // Two-level workspace: level 1 selects candidates from n rows (capacity cap),
-// level 2 is an exact top-k over the cap canonical candidate keys.
-static size_t rerank_ws_bytes(int64_t n, int64_t k, int64_t cap) {
-  return topk_layout(n, cap).total + topk_layout(cap, k).total + round_up(k * 8, 256);
+// level 2 is an exact top-k over the cap canonical candidate keys; then the
+// selected positions and the fast level 1's group minima ([2][kMaxGroups]).
+struct RerankWs {
+  TopkLayout L1, L2;
+  size_t l2, pos, gmin, total;
+};
+
+static RerankWs rerank_ws(int64_t n, int64_t k, int64_t cap) {
+  RerankWs W;
+  W.L1 = topk_layout(n, cap);
+  W.L2 = topk_layout(cap, k);
+  W.l2 = W.L1.total;
+  W.pos = W.l2 + W.L2.total;
+  W.gmin = W.pos + round_up(k * 8, 256);
+  W.total = W.gmin + round_up(2 * kMaxGroups * 8, 256);
+  return W;
 }
 
+static size_t rerank_ws_bytes(int64_t n, int64_t k, int64_t cap) { return rerank_ws(n, k, cap).total; }
+
+// Candidate arguments shared by the level-1 checks of the three selections.
+static int check_rerank_args(int64_t n, int64_t k, int64_t cap, int passes, void* ws, size_t ws_bytes) {
+  if (n < 1 || k < 1 || k > n || cap < k) return DAL_ERR_SHAPE;
+  if (passes < 0 || passes >= kPasses || (passes > 0 && cap > DAL_SORT_CAP_PAYLOAD)) return DAL_ERR_ARG;
+  if (k > DAL_SORT_CAP) return DAL_ERR_CAPACITY;
+  if (ws_bytes < rerank_ws_bytes(n, k, cap) || (reinterpret_cast<uintptr_t>(ws) & 255)) return DAL_ERR_SHAPE;
+  return DAL_OK;
+}
+
+// The standalone fast level 1: group minima (one pass over both keys; block 0
+// zeroes the level-1 counters) and the summary select.
+template <bool DW>
+static int launch_fast_level1(const uint64_t* keys_lo, const uint64_t* keys_hi, int64_t n, int64_t k,
+                              int64_t idx_base, int64_t cap, void* ws, const AppendRerank& AR, int32_t* status,
+                              int64_t* out_idx, double* out_scores, uint64_t* out_keys, hipStream_t st) {
+  const RerankWs W = rerank_ws(n, k, cap);
+  char* base = static_cast<char*>(ws);
+  TopkHdr* h1 = reinterpret_cast<TopkHdr*>(base + W.L1.hdr);
+  uint64_t* gmin = reinterpret_cast<uint64_t*>(base + W.gmin);
+  const GroupSummary S = launch_group_min(keys_lo, keys_hi, n, gmin, reinterpret_cast<uint32_t*>(h1),
+                                         kFastHdrWords, st);
+  SortTail tail;
+  tail.cap = cap;
+  tail.cap_miss = true;
+  tail.status = status;
+  tail.clear = reinterpret_cast<uint32_t*>(h1);
+  tail.clear_words = kFastHdrWords;
+  hipLaunchKernelGGL(summary_select_kernel<DW>, dim3(static_cast<unsigned>(summary_grid(S.ng))), dim3(kSumThreads),
+                     0, st, keys_hi, n, k, idx_base, S, h1, reinterpret_cast<int64_t*>(base + W.L1.cidx), cap, AR,
+                     0, out_keys, out_idx, out_scores, tail);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}
+
+// Exact level 1 (radix select of K + interval compaction) or the fast level 1
+// (group minima, indices only), then `rerank` (canonical keys of every slot),
+// then the exact top-k of the candidates.
 template <class Rerank>
 static int select_with_rerank(const uint64_t* keys_lo, const uint64_t* keys_hi, int64_t n, int64_t k,
                               int64_t idx_base, int64_t cap, int passes, void* ws, size_t ws_bytes,
                               Rerank rerank, int64_t* out_idx, double* out_scores, uint64_t* out_keys,
                               int32_t* dev_status, hipStream_t st) {
-  if (n < 1 || k < 1 || k > n || cap < k) return DAL_ERR_SHAPE;
-  if (passes < 0 || passes >= kPasses || (passes > 0 && cap > DAL_SORT_CAP_PAYLOAD)) return DAL_ERR_ARG;
-  if (k > DAL_SORT_CAP) return DAL_ERR_CAPACITY;
-  const TopkLayout L1 = topk_layout(n, cap), L2 = topk_layout(cap, k);
-  if (ws_bytes < rerank_ws_bytes(n, k, cap) || (reinterpret_cast<uintptr_t>(ws) & 255)) return DAL_ERR_SHAPE;
+  int rc = check_rerank_args(n, k, cap, passes, ws, ws_bytes);
+  if (rc) return rc;
+  const RerankWs W = rerank_ws(n, k, cap);
   char* base = static_cast<char*>(ws);
-  char* base2 = base + L1.total;
-  int64_t* pos = reinterpret_cast<int64_t*>(base2 + L2.total);
-  TopkHdr* h1 = reinterpret_cast<TopkHdr*>(base + L1.hdr);
-  TopkHdr* h2 = reinterpret_cast<TopkHdr*>(base2 + L2.hdr);
-  uint64_t* ckey = reinterpret_cast<uint64_t*>(base + L1.ckey);
-  int64_t* cidx = reinterpret_cast<int64_t*>(base + L1.cidx);
-  double* cpay = reinterpret_cast<double*>(base + L1.cpay);
-  int rc = DAL_OK;
+  char* base2 = base + W.l2;
+  int64_t* pos = reinterpret_cast<int64_t*>(base + W.pos);
+  TopkHdr* h1 = reinterpret_cast<TopkHdr*>(base + W.L1.hdr);
+  TopkHdr* h2 = reinterpret_cast<TopkHdr*>(base2 + W.L2.hdr);
+  uint64_t* ckey = reinterpret_cast<uint64_t*>(base + W.L1.ckey);
+  int64_t* cidx = reinterpret_cast<int64_t*>(base + W.L1.cidx);
+  double* cpay = reinterpret_cast<double*>(base + W.L1.cpay);
   if (passes > 0) {
-    rc = run_radix(keys_lo, n, k, h1, st, passes);
+    rc = launch_fast_level1<false>(keys_lo, keys_hi, n, k, idx_base, cap, ws, AppendRerank{}, dev_status, nullptr,
+                                   nullptr, nullptr, st);
     if (rc) return rc;
-    const int64_t blocks = std::min<int64_t>(ceil_div(n, kRadixThreads * 4), 1024);
-    hipLaunchKernelGGL(threshold_append_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kRadixThreads), 0, st,
-                       keys_lo, keys_hi, n, idx_base, passes, h1, cidx, cap);
-    DAL_RETURN_IF_LAUNCH_FAILED();
   } else {
     rc = run_radix(keys_lo, n, k, h1, st);
     if (rc) return rc;
-    rc = run_compact<true>(keys_lo, IntervalArgs{keys_hi}, n, idx_base, k, ws, L1, dev_status, st);
+    rc = run_compact<true>(keys_lo, IntervalArgs{keys_hi}, n, idx_base, k, ws, W.L1, dev_status, st);
     if (rc) return rc;
   }
-  // canonical keys for every slot (NONE past the count); with a truncated
-  // level 1 the re-rank also checks the candidate capacity (need_k = k)
-  rerank(h1, ckey, cidx, cpay, cap, passes > 0 ? k : 0);
+  // canonical keys for every slot (NONE past the count); with the fast level
+  // 1 the re-rank also checks the candidate capacity
+  rerank(h1, ckey, cidx, cpay, cap, passes > 0);
   if (cap <= DAL_SORT_CAP_PAYLOAD) {
-    // level 2 fits one block: sort the cand_count candidates (row order, so
-    // ties resolve by index) by canonical key with their scores, take k
+    // level 2 fits one block: sort the cand_count candidates by canonical key
+    // (then row) with their scores, take k
     hipLaunchKernelGGL(sort_kernel<true>, dim3(1), dim3(kSortThreads), 0, st, ckey, cidx, cpay, h1, int64_t{0},
                        k, out_keys, out_idx, out_scores, SortTail{});
     DAL_RETURN_IF_LAUNCH_FAILED();
@@ -1507,11 +1501,11 @@ static int select_with_rerank(const uint64_t* keys_lo, const uint64_t* keys_hi, 
   }
   rc = run_radix(ckey, cap, k, h2, st);
   if (rc) return rc;
-  rc = run_compact<false>(ckey, IntervalArgs{nullptr}, cap, 0, k, base2, L2, nullptr, st);
+  rc = run_compact<false>(ckey, IntervalArgs{nullptr}, cap, 0, k, base2, W.L2, nullptr, st);
   if (rc) return rc;
-  uint64_t* pkeys = reinterpret_cast<uint64_t*>(base2 + L2.ckey);
+  uint64_t* pkeys = reinterpret_cast<uint64_t*>(base2 + W.L2.ckey);
   hipLaunchKernelGGL(sort_kernel<false>, dim3(1), dim3(kSortThreads), 0, st, pkeys,
-                     reinterpret_cast<const int64_t*>(base2 + L2.cidx), nullptr, h2, int64_t{0}, k, pkeys,
+                     reinterpret_cast<const int64_t*>(base2 + W.L2.cidx), nullptr, h2, int64_t{0}, k, pkeys,
                      pos, nullptr, SortTail{});
   hipLaunchKernelGGL(gather_selected_kernel, dim3(static_cast<unsigned>(ceil_div(k, 256))), dim3(256), 0, st,
                      pos, pkeys, k, cidx, cpay, out_idx, out_scores, out_keys);
@@ -1535,44 +1529,31 @@ extern "C" int dal_dw_select(const uint64_t* keys_lo, const uint64_t* keys_hi, c
     return DAL_ERR_ARG;
   if (d < 1 || ldx < d) return DAL_ERR_SHAPE;
   hipStream_t st = as_stream(stream);
+  const DwRerank R{x, static_cast<int>(d), ldx, norm64, colsum, lut, votes, row_flags, beta};
   if (level1_passes > 0) {
-    // truncated level 1: header zero + ONE fused launch (radix passes with grid
-    // barriers, append with the in-place canonical re-rank, last-block sort)
-    if (n < 1 || k < 1 || k > n || cap < k) return DAL_ERR_SHAPE;
-    if (level1_passes >= kPasses || cap > DAL_SORT_CAP_PAYLOAD) return DAL_ERR_ARG;
-    if (k > DAL_SORT_CAP) return DAL_ERR_CAPACITY;
-    if (ws_bytes < rerank_ws_bytes(n, k, cap) || (reinterpret_cast<uintptr_t>(ws) & 255)) return DAL_ERR_SHAPE;
-    const TopkLayout L1 = topk_layout(n, cap);
-    char* base = static_cast<char*>(ws);
-    TopkHdr* h1 = reinterpret_cast<TopkHdr*>(base + L1.hdr);
-    zero_header(h1, st);
+    // fast level 1: group minima + ONE launch (tau, append with the in-place
+    // canonical re-rank, last-block sort)
+    const int rc = check_rerank_args(n, k, cap, level1_passes, ws, ws_bytes);
+    if (rc) return rc;
     if (colsum_ready && hipStreamWaitEvent(st, reinterpret_cast<hipEvent_t>(colsum_ready), 0) != hipSuccess)
       return DAL_ERR_HIP;
-    const DwRerank R{x, static_cast<int>(d), ldx, norm64, colsum, lut, votes, row_flags, beta};
-    SortTail tail;
-    tail.cap = cap;
-    tail.need_k = k;
-    tail.status = dev_status;
-    tail.clear = reinterpret_cast<uint32_t*>(h1);
-    tail.clear_words = kHdrWords;
-    tail.packed = true;
+    const RerankWs W = rerank_ws(n, k, cap);
+    char* base = static_cast<char*>(ws);
     // (the LUT size is not an argument of dal_dw_select: no lane-held LUT)
-    return launch_fused_level1(keys_lo, keys_hi, n, k, idx_base, level1_passes, h1,
-                               reinterpret_cast<int64_t*>(base + L1.cidx), cap,
-                               AppendRerank{R, reinterpret_cast<uint64_t*>(base + L1.ckey),
-                                            reinterpret_cast<double*>(base + L1.cpay)},
-                               0, dev_status, out_keys, out_idx, out_scores, tail, st);
+    return launch_fast_level1<true>(keys_lo, keys_hi, n, k, idx_base, cap, ws,
+                                    AppendRerank{R, reinterpret_cast<uint64_t*>(base + W.L1.ckey),
+                                                 reinterpret_cast<double*>(base + W.L1.cpay)},
+                                    dev_status, out_idx, out_scores, out_keys, st);
   }
   bool wait_failed = false;
-  auto rerank = [&](TopkHdr* h, uint64_t* ckey, int64_t* cidx, double* cpay, int64_t cp, int64_t need_k) {
+  auto rerank = [&](TopkHdr* h, uint64_t* ckey, int64_t* cidx, double* cpay, int64_t cp, bool cap_miss) {
     // the only consumer of colsum: join its producer stream here, not before the call
     if (colsum_ready && hipStreamWaitEvent(st, reinterpret_cast<hipEvent_t>(colsum_ready), 0) != hipSuccess)
       wait_failed = true;
     hipLaunchKernelGGL(rerank_kernel, dim3(static_cast<unsigned>(ceil_div(cp, 4))), dim3(256), 0, st, h,
-                       idx_base, DwRerank{x, static_cast<int>(d), ldx, norm64, colsum, lut, votes, row_flags, beta},
-                       ckey, cidx, cpay, cp, need_k, dev_status);
+                       idx_base, R, ckey, cidx, cpay, cp, cap_miss, dev_status);
   };
-  const int rc = select_with_rerank(keys_lo, keys_hi, n, k, idx_base, cap, level1_passes, ws, ws_bytes, rerank,
+  const int rc = select_with_rerank(keys_lo, keys_hi, n, k, idx_base, cap, 0, ws, ws_bytes, rerank,
                                     out_idx, out_scores, out_keys, dev_status, st);
   return rc ? rc : (wait_failed ? DAL_ERR_HIP : DAL_OK);
 }
@@ -1582,13 +1563,13 @@ extern "C" size_t dal_dw_step_workspace_bytes(int64_t n, int64_t k, int64_t cap)
 }
 
 // One density-weighted iteration: dal_forest_score (DAL_DENSITY_FIXED,
-// DAL_DESCENDING, interval keys) + dal_dw_select in one call.  With a
-// truncated level 1 (level1_passes > 0, cap <= DAL_SORT_CAP_PAYLOAD) the
-// launches are fused: the threshold append re-ranks the candidates it appends
-// (a wave per candidate), and the one-block sort checks the capacity and
-// clears the level-1 header -- 5 launches instead of 7 (no header zero with
-// DAL_STEP_WS_CLEAN, no status memset with DAL_STEP_RESET_STATUS).  Same bits
-// as the two calls.
+// DAL_DESCENDING, interval keys) + dal_dw_select in one call.  With the fast
+// level 1 (level1_passes > 0, cap <= DAL_SORT_CAP_PAYLOAD) the score kernel
+// also folds each block's minimum keys into the row groups, so the selection
+// is ONE more launch (summary_select_kernel: tau, the append with the
+// in-place canonical re-rank, the last-block sort with the capacity check and
+// the clears) -- no zeroing launch with DAL_STEP_WS_CLEAN, no status memset
+// with DAL_STEP_RESET_STATUS.  Same bits as the two calls.
 namespace dal {
 
 int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner, const uint8_t* leaf,
@@ -1603,23 +1584,21 @@ int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_
       !keys_lo || !keys_hi || !out_idx || !out_scores || !dev_status)
     return DAL_ERR_ARG;
   if (step_flags & ~static_cast<uint32_t>(DAL_STEP_RESET_STATUS | DAL_STEP_WS_CLEAN)) return DAL_ERR_ARG;
-  if (n < 1 || d < 1 || ldx < d || k < 1 || k > n || cap < k) return DAL_ERR_SHAPE;
-  if (level1_passes < 0 || level1_passes >= kPasses || (level1_passes > 0 && cap > DAL_SORT_CAP_PAYLOAD))
-    return DAL_ERR_ARG;
-  if (k > DAL_SORT_CAP) return DAL_ERR_CAPACITY;
-  if (ws_bytes < rerank_ws_bytes(n, k, cap) || (reinterpret_cast<uintptr_t>(ws) & 255)) return DAL_ERR_SHAPE;
+  if (d < 1 || ldx < d) return DAL_ERR_SHAPE;
+  int rc = check_rerank_args(n, k, cap, level1_passes, ws, ws_bytes);
+  if (rc) return rc;
   hipStream_t st = as_stream(stream);
   const bool clean = step_flags & DAL_STEP_WS_CLEAN;
   ForestStepHooks hooks;
   if (plan_hooks) hooks = *plan_hooks;
   if (step_flags & DAL_STEP_RESET_STATUS) hooks.status_reset = dev_status;
-  const TopkLayout L1 = topk_layout(n, cap);
+  const RerankWs W = rerank_ws(n, k, cap);
   char* base = static_cast<char*>(ws);
-  TopkHdr* h1 = reinterpret_cast<TopkHdr*>(base + L1.hdr);
+  TopkHdr* h1 = reinterpret_cast<TopkHdr*>(base + W.L1.hdr);
   if (level1_passes == 0) {  // exact level 1: the two calls as they are
-    int rc = forest_score_launch(x, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, DAL_DENSITY_FIXED,
-                                 density_err, row_flags, beta, DAL_DESCENDING, votes, scores, keys_lo, keys_hi,
-                                 hooks, st);
+    rc = forest_score_launch(x, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, DAL_DENSITY_FIXED,
+                             density_err, row_flags, beta, DAL_DESCENDING, votes, scores, keys_lo, keys_hi, hooks,
+                             st);
     if (rc) return rc;
     rc = dal_dw_select(keys_lo, keys_hi, votes, row_flags, n, k, idx_base, lut, beta, x, d, ldx, norm64, colsum,
                        cap, 0, ws, ws_bytes, out_idx, out_scores, out_keys, dev_status, colsum_ready, stream);
@@ -1631,31 +1610,51 @@ int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_
     DAL_RETURN_IF_LAUNCH_FAILED();
     return DAL_OK;
   }
-  if (!clean) zero_header(h1, st);
-  int rc = forest_score_launch(x, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, DAL_DENSITY_FIXED,
-                               density_err, row_flags, beta, DAL_DESCENDING, votes, scores, keys_lo, keys_hi, hooks,
-                               st);
+  // the score kernel's blocks are the row groups when there are >= 2k of them
+  // (tau then lies within a few ranks of K); smaller pools take one
+  // group_min_kernel pass over finer groups after the score kernel
+  uint64_t* gmin = reinterpret_cast<uint64_t*>(base + W.gmin);
+  const int rows_per_block = forest_rows_per_block(x, d, ldx, n_trees);
+  GroupSummary S = make_groups(gmin, n, rows_per_block);
+  const bool in_score = S.ng >= 2 * k;
+  if (in_score) {
+    hooks.gmin = gmin;
+    hooks.group_blocks = static_cast<int>(S.group_rows / rows_per_block);
+    hooks.n_groups = S.ng;
+  }
+  const bool folded = in_score && hooks.group_blocks > 1;  // atomic max: the buffer starts (and is left) zero
+  if (!clean) {
+    zero_words(reinterpret_cast<uint32_t*>(h1), kFastHdrWords, st);
+    if (folded) zero_words(reinterpret_cast<uint32_t*>(gmin), 2 * S.ng * 2, st);
+  }
+  rc = forest_score_launch(x, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, DAL_DENSITY_FIXED,
+                           density_err, row_flags, beta, DAL_DESCENDING, votes, scores, keys_lo, keys_hi, hooks, st);
   if (rc) return rc;
+  if (!in_score) S = launch_group_min(keys_lo, keys_hi, n, gmin, nullptr, 0, st);
   if (colsum_ready && hipStreamWaitEvent(st, reinterpret_cast<hipEvent_t>(colsum_ready), 0) != hipSuccess)
     return DAL_ERR_HIP;
-  uint64_t* ckey = reinterpret_cast<uint64_t*>(base + L1.ckey);
-  int64_t* cidx = reinterpret_cast<int64_t*>(base + L1.cidx);
-  double* cpay = reinterpret_cast<double*>(base + L1.cpay);
   const DwRerank R{x, static_cast<int>(d), ldx, norm64, colsum, lut, votes, row_flags, beta};
   const int n_lut = n_trees < 64 ? n_trees + 1 : 0;  // LUT held in lanes when it fits a wave
   SortTail tail;
   tail.cap = cap;
-  tail.need_k = k;
+  tail.cap_miss = true;
   tail.status = dev_status;
   tail.clear = reinterpret_cast<uint32_t*>(h1);
-  tail.clear_words = kHdrWords;
+  tail.clear_words = kFastHdrWords;
+  if (folded) {
+    tail.clear2 = reinterpret_cast<uint32_t*>(gmin);
+    tail.clear2_words = 2 * S.ng * 2;
+  }
   tail.out_slot = out_slot;
   tail.status_mirror = status_mirror;
-  tail.packed = true;
-  // the level-1 radix passes, the append with the in-place canonical re-rank
-  // and the final sort: ONE launch after the forest score
-  return launch_fused_level1(keys_lo, keys_hi, n, k, idx_base, static_cast<int>(level1_passes), h1, cidx, cap,
-                             AppendRerank{R, ckey, cpay}, n_lut, dev_status, out_keys, out_idx, out_scores, tail, st);
+  hipLaunchKernelGGL(summary_select_kernel<true>, dim3(static_cast<unsigned>(summary_grid(S.ng))),
+                     dim3(kSumThreads), 0, st, keys_hi, n, k, idx_base, S, h1,
+                     reinterpret_cast<int64_t*>(base + W.L1.cidx), cap,
+                     AppendRerank{R, reinterpret_cast<uint64_t*>(base + W.L1.ckey),
+                                  reinterpret_cast<double*>(base + W.L1.cpay)},
+                     n_lut, out_keys, out_idx, out_scores, tail);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
 }
 
 }  // namespace dal
@@ -1688,9 +1687,9 @@ extern "C" int dal_maxcos_select(const uint64_t* keys_lo, const uint64_t* keys_h
     return DAL_ERR_ARG;
   if (d < 1 || d > 256 || ld < d || m < 1) return DAL_ERR_SHAPE;
   hipStream_t st = as_stream(stream);
-  auto rerank = [&](TopkHdr* h, uint64_t* ckey, int64_t* cidx, double* cpay, int64_t cp, int64_t need_k) {
+  auto rerank = [&](TopkHdr* h, uint64_t* ckey, int64_t* cidx, double* cpay, int64_t cp, bool cap_miss) {
     hipLaunchKernelGGL(rerank_maxcos_kernel, dim3(static_cast<unsigned>(ceil_div(cp, kRrC))), dim3(256), 0, st,
-                       h, idx_base, pool, static_cast<int>(d), ld, ulab, m, ckey, cidx, cpay, cp, need_k,
+                       h, idx_base, pool, static_cast<int>(d), ld, ulab, m, ckey, cidx, cpay, cp, cap_miss,
                        dev_status);
   };
   return select_with_rerank(keys_lo, keys_hi, n, k, idx_base, cap, level1_passes, ws, ws_bytes, rerank, out_idx,

@@ -164,7 +164,7 @@ class PoolState:
         self.select_events = None  # list -> (start, end) HIP events around each dal_dw_select call
         self.cap_scale = 1  # re-rank candidate capacity multiplier, kept after an overflow
         self.cap_base = None  # initial re-rank capacity override (tests: force the overflow path)
-        self.level1_fast = True  # truncated top-k level 1 allowed (cleared after an overflow on this pool)
+        self.level1_fast = True  # fast top-k level 1 allowed (cleared after an overflow on this pool)
         self.use_graphs = os.environ.get("DAL_GRAPHS", "1") != "0"  # hipGraph replay of warm steps
         self._graphs = {}  # warm-step graphs by (T, depth, k, beta, cap, level-1 passes)
         self.last_status = 0     # status word read by the last synchronising select
@@ -442,7 +442,7 @@ class PoolState:
         if st & DAL_FLAG_CAND_OVERFLOW:
             raise _lib.DalError("density re-rank candidate set exceeded DAL_SORT_CAP_PAYLOAD")
         if st & DAL_FLAG_SAMPLE_MISS:
-            raise _lib.DalError("truncated top-k level 1 overflowed and was not re-run")
+            raise _lib.DalError("fast top-k level 1 overflowed and was not re-run")
 
 
 GRAM_KINDS = ("sym", "f32")
@@ -572,10 +572,11 @@ def candidate_cap(n: int, k: int) -> int:
     return int(min(n, max(4 * k, _lib.DAL_SORT_CAP_PAYLOAD)))
 
 
-# Truncated level 1 of dal_dw_select: 2 radix digits resolve the k-th
-# pessimistic key's bucket, whose upper edge bounds the candidate search
-# (3 launches instead of 9).  DAL_LEVEL1_PASSES overrides (0 = exact radix).
-LEVEL1_PASSES = int(os.environ.get("DAL_LEVEL1_PASSES", "2"))
+# Fast level 1 of the interval selections (ABI v6): tau = the k-th smallest
+# of <= 4096 row groups' minimum keys bounds the candidate search (group
+# minima + one launch instead of 6 radix passes + 3 compaction launches).
+# DAL_LEVEL1_PASSES overrides (0 = the exact radix level 1).
+LEVEL1_PASSES = int(os.environ.get("DAL_LEVEL1_PASSES", "1"))
 
 
 def level1_passes(state, n: int, k: int, cap: int) -> int:
@@ -631,7 +632,7 @@ def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k
         # the step's one host sync: status word (zero-norm rows, candidate overflow)
         st = int(state.status.item())
         state.last_status = st
-        if st & DAL_FLAG_SAMPLE_MISS:  # truncated level 1 over capacity: exact level 1 from now on
+        if st & DAL_FLAG_SAMPLE_MISS:  # fast level 1 over capacity: exact level 1 from now on
             state.status.bitwise_and_(~(DAL_FLAG_SAMPLE_MISS | DAL_FLAG_CAND_OVERFLOW))
             state.level1_fast = False
             continue
@@ -646,7 +647,7 @@ def dw_step_local(state: PoolState, forest: Forest, flags, dens, lut_dev, k: int
                   colsum_ready=None, cap_scale: int = None, sync: bool = True):
     """dal_dw_step on this pool or shard: votes, scores and interval keys
     of every row, then the exact canonical top-k -- one C call with fused
-    launches (the truncated level 1).  Same retries as dw_select_local.
+    launches (the fast level 1).  Same retries as dw_select_local.
     Returns (votes, scores, indices, selected scores); sync=False (the
     multi-GPU path: the caller reads the status word after the merge and
     re-runs with a larger ``cap_scale``) also returns the selected keys."""
@@ -693,7 +694,7 @@ def dw_step_local(state: PoolState, forest: Forest, flags, dens, lut_dev, k: int
             return votes, scores, out_idx, out_scores, out_keys
         st = int(state.status.item())  # the step's one host sync
         state.last_status = st
-        if st & DAL_FLAG_SAMPLE_MISS:  # truncated level 1 over capacity: exact level 1 from now on
+        if st & DAL_FLAG_SAMPLE_MISS:  # fast level 1 over capacity: exact level 1 from now on
             state.status.bitwise_and_(~(DAL_FLAG_SAMPLE_MISS | DAL_FLAG_CAND_OVERFLOW))
             state.level1_fast = False
             continue

@@ -115,7 +115,7 @@ class ShardedSelector:
         return self.state.status
 
     def prepare_retry(self, sample_miss: bool = False):
-        """After a re-rank capacity overflow (or a truncated level-1
+        """After a re-rank capacity overflow (or a fast level-1
         overflow) anywhere: grow the capacity (or fall back to the exact radix
         level 1) and go again.  The density, operand and column-sum caches stay valid,
         so the retry does not redo the Gram."""

@@ -181,7 +181,7 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
             passes = LEVEL1_PASSES if cap <= _lib.DAL_SORT_CAP_PAYLOAD else 0
             status.zero_()
             continue
-        if st & DAL_FLAG_SAMPLE_MISS:  # the truncated level 1 overflowed: exact level 1
+        if st & DAL_FLAG_SAMPLE_MISS:  # the fast level 1 overflowed: exact level 1
             passes = 0
             status.zero_()
             continue

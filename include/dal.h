@@ -55,7 +55,7 @@ enum dal_status {
 #define DAL_FLAG_ZERO_NORM 1      /* a pool row has ||x|| == 0 (cosine undefined) */
 #define DAL_FLAG_CAND_OVERFLOW 2  /* re-rank candidate set exceeded capacity */
 #define DAL_FLAG_RF_SPLITS 4      /* a feature produced more than num_splits + 1 thresholds */
-#define DAL_FLAG_SAMPLE_MISS 8    /* truncated top-k level 1 over capacity: re-run with level1_passes = 0 */
+#define DAL_FLAG_SAMPLE_MISS 8    /* fast top-k level 1 over capacity: re-run with level1_passes = 0 */
 
 /* per-row flags (uint8 per pool row) */
 #define DAL_ROW_CANDIDATE 1 /* row is in the unlabeled set and may be selected */
@@ -253,12 +253,14 @@ int dal_topk(const uint64_t* keys, int64_t n, int64_t k, int64_t idx_base, void*
  * another stream; the call makes ``stream`` wait for it just before the
  * re-rank (the radix select and compaction run without it), so a cold step's
  * canonical column sum overlaps the candidate search.
- * level1_passes = p in 1..5 (cap <= DAL_SORT_CAP_PAYLOAD): level 1 resolves
- * only the first p radix digits of K; tau = the upper edge of K's bucket
- * (tau >= K) and the candidates are every row whose optimistic key is <= tau
- * -- a superset of the exact candidates, found in p + 1 launches instead of 9
- * (the engine uses p = 2: ~2^-11 relative, about a density interval's width).
- * More than cap candidates sets DAL_FLAG_SAMPLE_MISS: re-run with
+ * level1_passes > 0 (1..5; cap <= DAL_SORT_CAP_PAYLOAD): the fast level 1
+ * (ABI v6) -- the pool is cut into <= 4096 row groups, tau = the k-th smallest
+ * group-minimum pessimistic key (k keys of the pool, so tau >= K), and the
+ * candidates are every row whose optimistic key is <= tau, found by scanning
+ * only the groups whose minimum optimistic key is <= tau: a superset of the
+ * exact candidates in two launches (group minima; tau + append with the
+ * in-place canonical re-rank + the final sort by the block that finishes
+ * last).  More than cap candidates sets DAL_FLAG_SAMPLE_MISS: re-run with
  * level1_passes = 0.  The selection is the same either way. */
 size_t dal_dw_select_workspace_bytes(int64_t n, int64_t k, int64_t cap);
 int dal_dw_select(const uint64_t* keys_lo, const uint64_t* keys_hi, const int32_t* votes,
@@ -274,11 +276,12 @@ int dal_dw_select(const uint64_t* keys_lo, const uint64_t* keys_hi, const int32_
  * row_flags, beta, DAL_DESCENDING, votes, scores, keys_lo, keys_hi) followed by
  * dal_dw_select(keys_lo, keys_hi, votes, row_flags, n, k, idx_base, lut, beta,
  * x, d, ldx, norm64, colsum, cap, level1_passes, ...) -- same outputs, same
- * bits -- with the launches fused when level1_passes > 0 (and cap <=
- * DAL_SORT_CAP_PAYLOAD): the score kernel counts the first radix digit
- * itself, the threshold append computes each candidate's canonical score, and
- * the final sort checks the capacity (DAL_FLAG_SAMPLE_MISS) and clears the
- * level-1 header.  step_flags:
+ * bits -- with the fast level 1 fused when level1_passes > 0 (and cap <=
+ * DAL_SORT_CAP_PAYLOAD): the score kernel folds each block's minimum keys
+ * into the row groups itself, and ONE more launch derives tau, appends the
+ * candidates with their canonical scores and sorts them (capacity check:
+ * DAL_FLAG_SAMPLE_MISS; the level-1 words are cleared for the next call).
+ * step_flags:
  *   DAL_STEP_RESET_STATUS  *dev_status is zeroed at the start of the step (on
  *                          the device: a replayed hipGraph needs no memset node);
  *   DAL_STEP_WS_CLEAN      the workspace header is zero on entry (a previous
@@ -374,7 +377,8 @@ int dal_interval_keys_f32(const float* values, int64_t n, double err, const uint
  * ulab = canonical fp64 unit rows of the m labeled rows, feature-major
  * [d][m] (dal_canon_unit_rows_bf16 with feature_major = 1); d <= 256.  Same candidate/re-rank contract
  * as dal_dw_select, including level1_passes (0 = exact radix level 1; 1-5 =
- * truncated, DAL_FLAG_SAMPLE_MISS when its candidates overflow cap <= 4096). */
+ * the fast group-minimum level 1, DAL_FLAG_SAMPLE_MISS when its candidates
+ * overflow cap <= 4096). */
 size_t dal_maxcos_select_workspace_bytes(int64_t n, int64_t k, int64_t cap);
 int dal_maxcos_select(const uint64_t* keys_lo, const uint64_t* keys_hi, int64_t n, int64_t k,
                       int64_t idx_base, const uint16_t* pool, int64_t d, int64_t ld,

@@ -1,10 +1,11 @@
-"""Truncated level 1 of dal_dw_select (density_weighting.py:168,172 sortBy +
-take): two radix digits bound the k-th pessimistic key and every row whose
-optimistic key is under the bound becomes a candidate, instead of the 6-pass
-radix select + ordered compaction.  The selection must be the oracle's,
-whether the bound keeps the candidates under the capacity (the fast path
-stays enabled) or not (a forced small capacity: DAL_FLAG_SAMPLE_MISS, exact
-re-run, the fast level 1 disabled for the pool), on one GPU and across
+"""Fast level 1 of dal_dw_select (density_weighting.py:168,172 sortBy +
+take): tau = the k-th smallest of the row groups' minimum pessimistic keys
+bounds the k-th pessimistic key, and every row whose optimistic key is under
+it becomes a candidate, instead of the 6-pass radix select + ordered
+compaction.  The selection must be the oracle's, whether the bound keeps the
+candidates under the capacity (the fast path stays enabled) or not (a forced
+small capacity, or the top rows packed into a few groups: DAL_FLAG_SAMPLE_MISS,
+exact re-run, the fast level 1 disabled for the pool), on one GPU and across
 emulated shards; and the warm-step hipGraph must replay it exactly."""
 import numpy as np
 import pytest
@@ -24,31 +25,31 @@ def _case(n, d, seed=0):
 
 @pytest.mark.parametrize("n,d,k", [(100_000, 64, 100), (20_000, 32, 10), (5_000, 48, 100), (1_500, 16, 1),
                                    (250_000, 30, 1000)])
-def test_truncated_level1_select_bit_exact(cuda, n, d, k):
+def test_fast_level1_select_bit_exact(cuda, n, d, k):
     from dal import density_weighting as dw
     from dal.engine import PoolState, level1_passes
     from dal.forest import Forest
 
     X, of, E, unl = _case(n, d)
     st = PoolState(X, excluded=E, device=cuda)
-    assert level1_passes(st, n, k, 4096) > 0  # the truncated level 1 is the path under test
+    assert level1_passes(st, n, k, 4096) > 0  # the fast level 1 is the path under test
     F = Forest.synthetic(10, 4, d, seed=1)
     ref_sc, ref_idx, ref_ss = O.density_select(X, unl, of, k, 1.0, E)
     for _ in range(2):  # cold, then warm
         sel = dw.select(st, unl, F, k)
         assert np.array_equal(sel.indices.cpu().numpy(), ref_idx)
         assert np.array_equal(sel.selected_scores.cpu().numpy(), ref_ss)
-    assert st.level1_fast  # no overflow: every step took the truncated level 1
+    assert st.level1_fast  # no overflow: every step took the fast level 1
 
 
-def test_truncated_level1_overflow_reruns_exactly(cuda):
+def test_fast_level1_overflow_reruns_exactly(cuda):
     from dal import density_weighting as dw
     from dal.engine import PoolState
     from dal.forest import Forest
 
     X, of, E, unl = _case(50_000, 32, seed=5)
     st = PoolState(X, excluded=E, device=cuda)
-    st.cap_base = 100  # capacity k: the bucket bound holds more candidates than that
+    st.cap_base = 100  # capacity k: the group bound holds more candidates than that
     F = Forest.synthetic(10, 4, 32, seed=1)
     sel = dw.select(st, unl, F, 100)
     _, ref_idx, ref_ss = O.density_select(X, unl, of, 100, 1.0, E)
@@ -57,7 +58,7 @@ def test_truncated_level1_overflow_reruns_exactly(cuda):
     assert not st.level1_fast  # the overflow switched the pool to the exact level 1
 
 
-def test_truncated_level1_overflow_sharded(cuda):
+def test_fast_level1_overflow_sharded(cuda):
     from dal import parallel
     from dal.forest import Forest
 
@@ -74,6 +75,30 @@ def test_truncated_level1_overflow_sharded(cuda):
     assert np.array_equal(idx.cpu().numpy(), ref_idx)
     assert np.array_equal(sc.cpu().numpy(), ref_ss)
     assert not all(s.state.level1_fast for s in sels)
+
+
+def test_fast_level1_top_rows_in_few_groups(cuda):
+    """The best rows packed at the front of the pool (a sorted pool): the k-th
+    group minimum then lies far above the k-th key, the candidates overflow
+    and the step re-runs exactly -- same selection as the oracle."""
+    from dal import density_weighting as dw
+    from dal.engine import PoolState
+    from dal.forest import Forest
+
+    n, d, k = 60_000, 32, 100
+    X0, of, E, unl = _case(n, d, seed=23)
+    ref_sc0, _, _ = O.density_select(X0, unl, of, k, 1.0, E)
+    s_full = np.full(n, -np.inf)
+    s_full[unl] = np.nan_to_num(ref_sc0, nan=-np.inf)
+    order = np.argsort(-s_full, kind="stable")  # best rows first
+    X = np.ascontiguousarray(X0[order])
+    F = Forest.synthetic(10, 4, d, seed=1)
+    _, ref_idx, ref_ss = O.density_select(X, unl, of, k, 1.0, E)
+    st = PoolState(X, excluded=E, device=cuda)
+    for _ in range(2):
+        sel = dw.select(st, unl, F, k)
+        assert np.array_equal(sel.indices.cpu().numpy(), ref_idx)
+        assert np.array_equal(sel.selected_scores.cpu().numpy().view(np.int64), ref_ss.view(np.int64))
 
 
 @pytest.mark.parametrize("n,d,k", [(30_000, 32, 10), (8_000, 64, 100)])
@@ -130,16 +155,17 @@ def test_warm_graph_outputs_survive_later_steps(cuda):
         assert np.array_equal(a.indices.cpu().numpy(), b.indices.cpu().numpy())
 
 
-@pytest.mark.parametrize("n,d,trees,passes", [(100_000, 64, 10, 2), (284_807 // 4, 30, 100, 2),
-                                              (100_000, 256, 10, 2), (20_000, 32, 10, 0),
-                                              (3_000, 16, 7, 1)])
+@pytest.mark.parametrize("n,d,trees,passes", [(100_000, 64, 10, 1), (284_807 // 4, 30, 100, 1),
+                                              (100_000, 256, 10, 1), (20_000, 32, 10, 0),
+                                              (3_000, 16, 7, 1), (300_000, 64, 10, 1)])
 def test_dw_step_matches_separate_calls(cuda, n, d, trees, passes):
-    """dal_dw_step (fused launches: pass-0 histogram in the score kernel --
-    or a separate pass 0 when the grid is large, as at d = 256 here -- the
-    re-rank inside the threshold append, capacity check + header clear in the
-    sort) gives the same bits as dal_forest_score + dal_dw_select, call after
-    call on one workspace with DAL_STEP_WS_CLEAN, and DAL_STEP_RESET_STATUS
-    clears a stale status word."""
+    """dal_dw_step (the score kernel writes the row-group minima -- one group
+    per block, or several blocks folded by atomic max at 300,000 x 64 -- then
+    ONE launch: tau, the append with the in-place re-rank, the last-block sort
+    with the capacity check and the clears) gives the same bits as
+    dal_forest_score + dal_dw_select, call after call on one workspace with
+    DAL_STEP_WS_CLEAN (the folded minima must be left zero for the next call),
+    and DAL_STEP_RESET_STATUS clears a stale status word."""
     import torch
 
     from dal import _lib, engine
@@ -196,13 +222,13 @@ def test_dw_step_matches_separate_calls(cuda, n, d, trees, passes):
         assert torch.equal(klo, klo0) and torch.equal(khi, khi0)
         assert torch.equal(i1, i0)
         assert torch.equal(c1.view(torch.int64), c0.view(torch.int64))
-        hdr = ws[(wsp - ws.data_ptr()):(wsp - ws.data_ptr()) + 49328]  # sizeof(TopkHdr)
+        hdr = ws[(wsp - ws.data_ptr()):(wsp - ws.data_ptr()) + 49312]  # sizeof(TopkHdr)
         assert int(hdr.count_nonzero()) == 0  # the header is left zero for the next call
 
 
 def test_dw_step_sample_miss_flag(cuda):
-    """A truncated level 1 over capacity raises DAL_FLAG_SAMPLE_MISS from the
-    fused sort (the engine then re-runs with the exact level 1)."""
+    """A fast level 1 over capacity raises DAL_FLAG_SAMPLE_MISS from the
+    last-block sort (the engine then re-runs with the exact level 1)."""
     import torch
 
     from dal import _lib, engine
@@ -218,7 +244,7 @@ def test_dw_step_sample_miss_flag(cuda):
     inner, leaf = F.device(cuda)
     lut = engine.device_lut("entropy", 10, cuda)
     lib = _lib.load()
-    cap = k  # the bucket bound holds more candidates than k
+    cap = k  # the group bound holds more candidates than k
     wsb = int(lib.dal_dw_step_workspace_bytes(n, k, cap))
     ws, wsp = engine.workspace(wsb, cuda)
     P = lambda t: t.data_ptr()  # noqa: E731
@@ -227,7 +253,7 @@ def test_dw_step_sample_miss_flag(cuda):
     c1 = torch.empty(k, dtype=torch.float64, device=cuda)
     st.status.zero_()
     call("dal_dw_step", P(st.x), n, d, d, P(inner), P(leaf), 10, 4, P(lut), P(dens), float(engine.density_error(st)),
-         P(flags), 1.0, 0, P(norm64), P(colsum), k, cap, 2, 0, wsp, wsb, *[P(t) for t in outs], P(i1), P(c1), 0,
+         P(flags), 1.0, 0, P(norm64), P(colsum), k, cap, 1, 0, wsp, wsb, *[P(t) for t in outs], P(i1), P(c1), 0,
          P(st.status), 0, torch.cuda.current_stream(cuda).cuda_stream)
     assert int(st.status.item()) & _lib.DAL_FLAG_SAMPLE_MISS
 
@@ -259,7 +285,7 @@ def test_many_candidates_and_ties(cuda, n_distinct):
 
 
 def test_warm_plan_exact_level1_and_capacity_growth(cuda):
-    """Warm steps through dal_dw_plan when the truncated level 1 overflows
+    """Warm steps through dal_dw_plan when the fast level 1 overflows
     (the plan is rebuilt with the exact level 1: dal_dw_select inside the
     graph + the publishing kernel) and when the re-rank capacity must grow:
     every step equals the oracle, and the pool keeps the modes it fell back to."""
@@ -268,7 +294,7 @@ def test_warm_plan_exact_level1_and_capacity_growth(cuda):
 
     X, _, E, unl = _case(40_000, 32, seed=13)
     st = engine.PoolState(X, excluded=E, device=cuda)
-    st.cap_base = 100  # capacity k: the bucket bound overflows the truncated level 1
+    st.cap_base = 100  # capacity k: the group bound overflows the fast level 1
     k = 100
     for it in range(3):
         F = Forest.synthetic(10, 4, 32, seed=200 + it)

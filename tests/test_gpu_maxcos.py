@@ -90,7 +90,7 @@ def test_diversity_select_scale(cuda):
 
 @pytest.mark.parametrize("case", ["bucket_overflow", "foreign_candidates"])
 def test_diversity_select_fallbacks(cuda, case):
-    """The truncated level 1 overflowing its 4,096 slots (5,000 identical
+    """The fast level 1 overflowing its 4,096 slots (5,000 identical
     least-similar rows: DAL_FLAG_SAMPLE_MISS, exact re-run), and candidate
     lists holding indices outside the pool (filtered after the status read,
     then re-selected with the true count)."""
