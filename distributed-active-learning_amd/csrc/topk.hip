@@ -895,7 +895,10 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
     // short lists (the common case: ~100-300 candidates): rank selection.  The
     // (key, index) pairs are distinct, so every element's rank -- the count of
     // smaller pairs, read as LDS broadcasts -- is its output position: two
-    // barriers instead of the bitonic network's log^2 m stages.
+    // barriers instead of the bitonic network's log^2 m stages.  tpe lanes of
+    // one wave share an element (each counts every tpe-th pair, a butterfly
+    // adds them): m / tpe dependent LDS reads per lane instead of m (one
+    // lane per element: ~10 us at m = 110).
     for (int i = tid; i < m; i += kSortThreads) {
       sk[i] = ld_sc1(keys + i);
       si[i] = ld_sc1(idx + i);
@@ -909,16 +912,24 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
     int64_t* const di = s_dest[0];
     double* const ds = reinterpret_cast<double*>(s_dest[1]);
     const int64_t kk = k < m ? k : m;
-    for (int e = tid; e < m; e += kSortThreads) {
-      const unsigned long long ke = sk[e];
-      const long long ie = si[e];
+    int tpe = 1;  // lanes per element: a power of two <= 64, tpe * m <= kSortThreads
+    while (tpe < 64 && 2 * tpe * m <= kSortThreads) tpe <<= 1;
+    const int part = tid & (tpe - 1);
+    for (int e0 = 0; e0 < m; e0 += kSortThreads / tpe) {  // block-uniform
+      const int e = e0 + tid / tpe;
+      const bool live = e < m;
+      const unsigned long long ke = live ? sk[e] : 0ull;
+      const long long ie = live ? si[e] : 0ll;
       int r = 0;
+      if (live) {
 #pragma unroll 4
-      for (int j = 0; j < m; ++j) {
-        const unsigned long long kj = sk[j];
-        r += kj < ke || (kj == ke && si[j] < ie);
+        for (int j = part; j < m; j += tpe) {
+          const unsigned long long kj = sk[j];
+          r += kj < ke || (kj == ke && si[j] < ie);
+        }
       }
-      if (r < kk) {
+      for (int o = 1; o < tpe; o <<= 1) r += __shfl_xor(r, o);
+      if (live && part == 0 && r < kk) {
         if (out_keys) out_keys[r] = ke;
         out_idx[r] = ie;
         if (PAY && out_pay) out_pay[r] = sp[e];
@@ -1044,35 +1055,71 @@ struct GroupSummary {
 };
 
 // tau = the k-th smallest of the groups' minimum pessimistic keys (NONE when
-// k > ng): k group minima are k keys of the pool, so at least k keys are
-// <= tau, i.e. tau >= K.  Block radix select (8-bit digits MSB first, up to
-// 4 keys per thread in registers) until the k-th key's bucket holds <= 64
-// keys, which one wave then ranks.  Every block computes it (no grid sync).
+// fewer than k groups hold a key): k group minima are k keys of the pool, so
+// at least k keys are <= tau, i.e. tau >= K.  Block radix select over the
+// keys' differing low bits (the common high bits of the minimum and maximum
+// -- for DW keys the sign and most of the exponent -- are skipped; up to 4
+// keys per thread in registers, 8-bit digits) until the k-th key's bucket
+// holds <= 64 keys, which one wave then ranks.  Every block computes it (no
+// grid sync).
 __device__ unsigned long long group_threshold(const GroupSummary& S, int64_t k) {
   constexpr int PER = kMaxGroups / kSumThreads;
+  constexpr int W = kSumThreads / 64;
   __shared__ unsigned int hist[256];
-  __shared__ unsigned long long s_prefix, s_tau;
-  __shared__ unsigned int s_krem, s_cnt, s_n;
+  __shared__ unsigned long long s_prefix, s_tau, s_mn[W], s_mx[W];
+  __shared__ unsigned int s_krem, s_cnt, s_n, s_nv[W];
   __shared__ unsigned long long s_bucket[64];
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (k > S.ng) return DAL_KEY_NONE;
   unsigned long long key[PER];
+  bool val[PER];
+  unsigned long long mn = DAL_KEY_NONE, mx = 0;
+  unsigned nv = 0;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int64_t g = tid + static_cast<int64_t>(j) * kSumThreads;
-    key[j] = g < S.ng ? ~S.ginv[g] : 0ull;
+    key[j] = g < S.ng ? ~S.ginv[g] : DAL_KEY_NONE;
+    val[j] = key[j] != DAL_KEY_NONE;
+    if (val[j]) {
+      mn = key[j] < mn ? key[j] : mn;
+      mx = key[j] > mx ? key[j] : mx;
+      ++nv;
+    }
   }
-  auto live = [&](int j) { return tid + static_cast<int64_t>(j) * kSumThreads < S.ng; };
-  unsigned long long prefix = 0, mask = 0;
-  unsigned int krem = static_cast<unsigned int>(k), cnt = static_cast<unsigned int>(S.ng);
-  for (int pass = 0; pass < 8 && cnt > 64; ++pass) {
-    const int shift = 56 - 8 * pass;
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+    nv += __shfl_xor(nv, o);
+  }
+  if (lane == 0) {
+    s_mn[w] = mn;
+    s_mx[w] = mx;
+    s_nv[w] = nv;
+  }
+  __syncthreads();
+  nv = 0;
+#pragma unroll
+  for (int q = 0; q < W; ++q) {
+    mn = s_mn[q] < mn ? s_mn[q] : mn;
+    mx = s_mx[q] > mx ? s_mx[q] : mx;
+    nv += s_nv[q];
+  }
+  if (nv < k) return DAL_KEY_NONE;  // (block-uniform)
+  if (mn == mx) return mn;
+  int top = 64 - __clzll(static_cast<long long>(mn ^ mx));  // bits [0, top) still to resolve
+  unsigned long long mask = top == 64 ? 0ull : ~((1ull << top) - 1ull);
+  unsigned long long prefix = mn & mask;
+  unsigned int krem = static_cast<unsigned int>(k), cnt = nv;
+  while (cnt > 64 && top > 0) {
+    const int width = top < 8 ? top : 8, shift = top - width;
+    const unsigned dmask = (1u << width) - 1u;
     if (tid < 256) hist[tid] = 0u;
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      const bool valid = live(j) && (key[j] & mask) == prefix;
-      const unsigned bin = static_cast<unsigned>((key[j] >> shift) & 255ull);
+      const bool valid = val[j] && (key[j] & mask) == prefix;
+      const unsigned bin = static_cast<unsigned>(key[j] >> shift) & dmask;
       const unsigned long long vm = __ballot(valid);
       if (vm) {  // the wave's most common bin (the first valid lane's) with one atomic
         const int first = __ffsll(static_cast<long long>(vm)) - 1;
@@ -1112,14 +1159,15 @@ __device__ unsigned long long group_threshold(const GroupSummary& S, int64_t k) 
     prefix = s_prefix;
     krem = s_krem;
     cnt = s_cnt;
-    mask |= 255ull << shift;
+    mask |= static_cast<unsigned long long>(dmask) << shift;
+    top = shift;
   }
-  if (mask == ~0ull) return prefix;  // all 64 bits resolved (equal keys)
+  if (top == 0) return prefix;  // every bit resolved (equal keys)
   if (tid == 0) s_n = 0u;
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < PER; ++j)
-    if (live(j) && (key[j] & mask) == prefix) s_bucket[atomicAdd(&s_n, 1u)] = key[j];
+    if (val[j] && (key[j] & mask) == prefix) s_bucket[atomicAdd(&s_n, 1u)] = key[j];
   __syncthreads();
   if (tid < 64) {  // rank the bucket's keys: the krem-th smallest is tau
     const unsigned long long mine = lane < static_cast<int>(cnt) ? s_bucket[lane] : 0ull;
@@ -1137,8 +1185,9 @@ __device__ unsigned long long group_threshold(const GroupSummary& S, int64_t k) 
 
 // Group minima of the keys (the standalone selections; dal_dw_step's score
 // kernel writes them itself on pools of >= 2k blocks): groups of >= 64 rows
-// take one wave each (8 x 64 keys in flight), smaller groups one lane each.
-// Block 0 also zeroes the fast-path header words.
+// take one wave each (8 x 64 keys in flight); smaller groups (a power of two
+// of rows) are lane segments of a wave: one coalesced key per lane and a
+// butterfly over each segment.  Block 0 also zeroes the fast-path header words.
 __global__ __launch_bounds__(256) void group_min_kernel(const uint64_t* __restrict__ keys_lo,
                                                         const uint64_t* __restrict__ keys_hi, int64_t n,
                                                         int64_t group_rows, int64_t ng, uint64_t* __restrict__ ginv,
@@ -1147,17 +1196,22 @@ __global__ __launch_bounds__(256) void group_min_kernel(const uint64_t* __restri
   if (blockIdx.x == 0 && zero)
     for (int64_t w = tid; w < zero_words; w += 256) zero[w] = 0u;
   unsigned long long lo = DAL_KEY_NONE, hi = DAL_KEY_NONE;
-  if (group_rows < 64) {  // a lane per group
-    const int64_t g = static_cast<int64_t>(blockIdx.x) * 256 + tid;
-    if (g >= ng) return;
-    const int64_t r0 = g * group_rows, r1 = r0 + group_rows < n ? r0 + group_rows : n;
-    for (int64_t i = r0; i < r1; ++i) {
-      const unsigned long long a = keys_lo[i], c = keys_hi[i];
+  if (group_rows < 64) {  // segments of group_rows lanes
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + tid;
+    if (i < n) {
+      lo = keys_lo[i];
+      hi = keys_hi[i];
+    }
+    for (int o = 1; o < group_rows; o <<= 1) {
+      const unsigned long long a = __shfl_xor(lo, o), c = __shfl_xor(hi, o);
       lo = a < lo ? a : lo;
       hi = c < hi ? c : hi;
     }
-    ginv[g] = ~lo;
-    ginv[ng + g] = ~hi;
+    const int64_t g = i / group_rows;
+    if ((lane & (group_rows - 1)) == 0 && g < ng) {
+      ginv[g] = ~lo;
+      ginv[ng + g] = ~hi;
+    }
     return;
   }
   const int64_t g = static_cast<int64_t>(blockIdx.x) * 4 + (tid >> 6);  // a wave per group
@@ -1244,9 +1298,10 @@ __global__ __launch_bounds__(kSumThreads) void summary_select_kernel(
         const bool cand = (cbits >> j) & 1u;
         const unsigned long long cm = __ballot(cand);
         if (!cm) continue;
+        // the slot reservation goes out first: its round trip overlaps the
+        // re-rank's loads (the value is read after the score)
         unsigned base = 0;
         if (lane == 0) base = atomicAdd(&h->cand_count, static_cast<unsigned>(__popcll(cm)));
-        const int64_t p = static_cast<int64_t>(__shfl(base, 0)) + __popcll(cm & lt_mask);
         if constexpr (DW) {
           double my_s = 0.0;
           bool my_ok = false;
@@ -1266,12 +1321,14 @@ __global__ __launch_bounds__(kSumThreads) void summary_select_kernel(
               }
             }
           }
+          const int64_t p = static_cast<int64_t>(__shfl(base, 0)) + __popcll(cm & lt_mask);
           if (cand && p < cap) {
             st_sc1(cidx + p, static_cast<int64_t>(idx_base + i));
             st_sc1(AR.cpay + p, my_s);
             st_sc1(AR.ckey + p, static_cast<uint64_t>(my_ok ? score_key(my_s, DAL_DESCENDING) : DAL_KEY_NONE));
           }
         } else {
+          const int64_t p = static_cast<int64_t>(__shfl(base, 0)) + __popcll(cm & lt_mask);
           if (cand && p < cap) cidx[p] = idx_base + i;
         }
       }
@@ -1322,8 +1379,11 @@ GroupSummary make_groups(const uint64_t* ginv, int64_t n, int64_t unit) {
 // (which also zeroes `zero_words` words at `zero`).
 GroupSummary launch_group_min(const uint64_t* keys_lo, const uint64_t* keys_hi, int64_t n, uint64_t* ginv,
                               uint32_t* zero, int64_t zero_words, hipStream_t st) {
-  const GroupSummary S = make_groups(ginv, n, 1);
-  const int64_t blocks = S.group_rows < 64 ? ceil_div(S.ng, 256) : ceil_div(S.ng, 4);
+  // groups below a wave are a power of two of rows (lane segments)
+  int64_t rows = ceil_div(n, kMaxGroups), unit = 1;
+  while (unit < rows && unit < 64) unit <<= 1;
+  const GroupSummary S = make_groups(ginv, n, unit);
+  const int64_t blocks = S.group_rows < 64 ? ceil_div(n, 256) : ceil_div(S.ng, 4);
   hipLaunchKernelGGL(group_min_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, keys_lo, keys_hi, n,
                      S.group_rows, S.ng, ginv, zero, zero_words);
   return S;

@@ -25,6 +25,7 @@ trees = int(sys.argv[3]) if len(sys.argv) > 3 else 10
 k = int(sys.argv[4]) if len(sys.argv) > 4 else 100
 lib = _lib.load()
 lib.dal_k3_trace.argtypes = [ctypes.c_void_p]
+lib.dal_k3_trace_reset.argtypes = []
 x = bench.upload(bench.host_pool(0, n, d, "normal" if d == 30 else "uniform"), dev)
 st = engine.PoolState(x, excluded=np.arange(10), device=dev)
 forest = Forest.synthetic(trees, 4, d, seed=1)
@@ -34,6 +35,7 @@ dens, cs = st.density_fixed(), st.colsum()
 buf = (ctypes.c_ulonglong * 256)()
 rows = []
 for it in range(30):
+    zero = (ctypes.c_ulonglong * 256)()
     engine.dw_step_local(st, forest, flags, dens, lut, k, 1.0, cs)
     torch.cuda.synchronize()
     lib.dal_k3_trace(ctypes.addressof(buf))
@@ -41,9 +43,12 @@ for it in range(30):
     G = t[5]
     arr = [t[64 + b] for b in range(G)]
     t0 = t[0]
-    rows.append(((t[1] - t0) / 100, (t[2] - t0) / 100, (min(arr) - t0) / 100, (max(arr) - t0) / 100,
-                 (t[3] - t0) / 100, (t[6] - t0) / 100, t[4], G, sum(t[128 + b] for b in range(G))))
+    rows.append(((t[10] - t0) / 100, (t[11] - t0) / 100, t[13], (t[1] - t0) / 100, (t[2] - t0) / 100, (min(arr) - t0) / 100, (max(arr) - t0) / 100,
+                 (t[3] - t0) / 100, (t[7] - t0) / 100, (t[8] - t0) / 100, (t[9] - t0) / 100, (t[6] - t0) / 100,
+                 t[4], G, sum(t[128 + b] for b in range(G)), t[20] / 100, t[21] / 100, t[22] / 100))
+    lib.dal_k3_trace_reset()
 print(f"{n}x{d} T={trees} k={k} level1_fast={st.level1_fast} (us from block 0's start; medians of 30)")
-names = ["tau", "hits", "first_arrive", "last_arrive", "sort_start", "end", "cands", "grid", "hit_groups"]
+names = ["minmax", "passes_done", "bucket", "tau", "hits", "first_arrive", "last_arrive", "sort_start", "sort_read_hdr", "sort_loaded", "sort_ranked",
+         "end", "cands", "grid", "hit_groups", "max_scan_load", "max_score", "max_store_drain"]
 for j, nm in enumerate(names):
     print(f"  {nm:13s} {statistics.median(r[j] for r in rows[5:]):9.2f}")

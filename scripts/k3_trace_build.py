@@ -1,0 +1,101 @@
+"""Build a timing-only variant of libdal.so whose summary_select_kernel (the
+fast level 1 of the top-k) stamps s_memrealtime at its phase boundaries into a
+device array (dal_k3_trace copies it out; read by scripts/k3_trace.py).  The
+product source is not modified: the instrumented copy is compiled from /tmp.
+usage: python scripts/k3_trace_build.py OUT_DIR"""
+import glob
+import os
+import subprocess
+import sys
+
+REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+CSRC = os.path.join(REPO, "distributed-active-learning_amd", "csrc")
+out = os.path.abspath(sys.argv[1])
+os.makedirs(out, exist_ok=True)
+s = open(os.path.join(CSRC, "topk.hip")).read()
+
+
+def sub(old, new):
+    global s
+    assert old in s, old[:60]
+    s = s.replace(old, new, 1)
+
+
+sub("struct TopkHdr {", """__device__ unsigned long long g_k3[256];
+#define K3T(slot) do { if (threadIdx.x == 0) g_k3[slot] = __builtin_amdgcn_s_memrealtime(); } while (0)
+struct TopkHdr {""")
+sub("""  const unsigned long long tau = group_threshold(S, k);
+  if (blockIdx.x == 0 && tid == 0) h->kstar = tau;""", """  if (blockIdx.x == 0) K3T(0);
+  const unsigned long long tau = group_threshold(S, k);
+  if (blockIdx.x == 0) K3T(1);
+  if (blockIdx.x == 0 && tid == 0) h->kstar = tau;""")
+sub("""  const int nh = static_cast<int>(s_nh);""", """  const int nh = static_cast<int>(s_nh);
+  if (blockIdx.x == 0) K3T(2);
+  if (tid == 0) g_k3[128 + blockIdx.x] = nh;""")
+sub("""  if (!s_last) return;
+  sort_tail_body<true>(AR.ckey, cidx, AR.cpay, h, int64_t{0}, k, out_keys, out_idx, out_scores, tail);
+}""", """  K3T(64 + blockIdx.x);
+  if (!s_last) return;
+  K3T(3);
+  if (tid == 0) { g_k3[4] = ld_sc1(&h->cand_count); g_k3[5] = gridDim.x; }
+  sort_tail_body<true>(AR.ckey, cidx, AR.cpay, h, int64_t{0}, k, out_keys, out_idx, out_scores, tail);
+  __syncthreads();
+  K3T(6);
+}""")
+sub("""  if (nv < k) return DAL_KEY_NONE;  // (block-uniform)""", """  if (blockIdx.x == 0) K3T(10);
+  if (nv < k) return DAL_KEY_NONE;  // (block-uniform)""")
+sub("""  if (top == 0) return prefix;  // every bit resolved (equal keys)""", """  if (blockIdx.x == 0) K3T(11);
+  if (blockIdx.x == 0 && threadIdx.x == 0) g_k3[13] = cnt;
+  if (top == 0) return prefix;  // every bit resolved (equal keys)""")
+sub("""  if (m <= kRankMax) {""", """  K3T(7);
+  if (m <= kRankMax) {""")
+sub("""      if (PAY) sp[i] = ld_sc1(pay + i);
+    }
+    __syncthreads();
+    if (tail.clear) {  // every thread read the header above""", """      if (PAY) sp[i] = ld_sc1(pay + i);
+    }
+    __syncthreads();
+    K3T(8);
+    if (tail.clear) {  // every thread read the header above""")
+sub("""    if (PAY && h) {
+      for (int64_t i = kk + tid; i < k; i += kSortThreads) {""", """    __syncthreads();
+    K3T(9);
+    if (PAY && h) {
+      for (int64_t i = kk + tid; i < k; i += kSortThreads) {""")
+sub("""    const int64_t r0 = static_cast<int64_t>(s_hits[q]) * S.group_rows;""", """    const unsigned long long ta = __builtin_amdgcn_s_memrealtime();
+    const int64_t r0 = static_cast<int64_t>(s_hits[q]) * S.group_rows;""")
+sub("""      if (!__ballot(cbits != 0)) continue;""", """      const unsigned long long tb = __builtin_amdgcn_s_memrealtime();
+      if (lane == 0) atomicMax(&g_k3[20], tb - ta);
+      if (!__ballot(cbits != 0)) continue;""")
+sub("""          const int64_t p = static_cast<int64_t>(__shfl(base, 0)) + __popcll(cm & lt_mask);
+          if (cand && p < cap) {
+            st_sc1(cidx + p, static_cast<int64_t>(idx_base + i));""", """          const int64_t p = static_cast<int64_t>(__shfl(base, 0)) + __popcll(cm & lt_mask);
+          const unsigned long long tc = __builtin_amdgcn_s_memrealtime();
+          if (lane == 0) atomicMax(&g_k3[21], tc - tb);
+          if (cand && p < cap) {
+            st_sc1(cidx + p, static_cast<int64_t>(idx_base + i));""")
+sub("""  // the last block to arrive sorts the candidates
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();""", """  // the last block to arrive sorts the candidates
+  const unsigned long long te = __builtin_amdgcn_s_memrealtime();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(&g_k3[22], __builtin_amdgcn_s_memrealtime() - te);""")
+s += """
+extern "C" int dal_k3_trace(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dal::g_k3), sizeof(unsigned long long) * 256) == hipSuccess ? 0 : 1;
+}
+extern "C" int dal_k3_trace_reset() {
+  unsigned long long z[256] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(dal::g_k3), z, sizeof(z)) == hipSuccess ? 0 : 1;
+}
+"""
+src = "/tmp/topk_k3trace.hip"
+open(src, "w").write(s)
+hipcc = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+         "-I" + os.path.join(REPO, "include"), "-I" + CSRC]
+subprocess.run(hipcc + ["-c", src, "-o", os.path.join(out, "topk.o")], check=True)
+objs = [o for o in glob.glob(os.path.join(REPO, "build", "csrc", "*.o")) if not o.endswith("topk.o")]
+subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
+                os.path.join(out, "libdal.so")] + objs + [os.path.join(out, "topk.o")], check=True)
+print("built", os.path.join(out, "libdal.so"))
