@@ -98,6 +98,8 @@ struct TopkHdr {
   unsigned long long prefix[kPasses + 1];
   unsigned long long krem[kPasses + 1];
   uint32_t hist[kPasses][kBins];
+  // fast level 1: candidates found by each summary_select block (its region)
+  unsigned int reg_count[32];
 };
 
 struct TopkLayout {
@@ -465,10 +467,12 @@ struct DwRerank {
 
 // The canonical score of local row i, computed by a whole wave (every lane
 // calls it with the same row): lane f forms the rounded product
-// (x_f / norm) * s_f -- the divisions and loads run in parallel -- and the
-// sequential sum over f takes the products from the lanes in order (the
-// oracle's operations in the oracle's order).  false (NONE key, NaN payload)
-// when the row is not an unlabeled candidate (a shard with < k candidates).
+// (x_f / norm) * s_f -- the loads and divisions of 256 features in flight
+// together (one memory round trip per 256 features: a round trip per
+// 64-feature chunk made a d = 256 row cost ~13 us) -- and the sequential sum
+// over f takes the products from the lanes in order (the oracle's operations
+// in the oracle's order).  false (NONE key, NaN payload) when the row is not
+// an unlabeled candidate (a shard with < k candidates).
 __device__ __forceinline__ double readlane_f64(double v, int l) {  // l wave-uniform
   const long long b = __double_as_longlong(v);
   const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(b), l));
@@ -478,21 +482,31 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {  // l wave-uni
 
 __device__ __forceinline__ bool dw_canonical_score_wave(const DwRerank& R, int64_t i, double& s,
                                                         double lut_lane = 0.0, int n_lut = 0) {
+  constexpr int kC = 4;  // 64-feature chunks per round: every chunk's loads and divisions in flight together
   const int lane = threadIdx.x & 63;
   const uint8_t fl = R.flags ? R.flags[i] : DAL_ROW_CANDIDATE;
   const double nr = R.norm64[i];
   const int v = R.votes[i];
   const float* xr = R.x + i * R.ldx;
   double acc = 0.0;
-  for (int f0 = 0; f0 < R.d; f0 += 64) {
-    const int f = f0 + lane;
-    double p = 0.0;
-    if (f < R.d) {
-      const double u = static_cast<double>(xr[f]) / nr;
-      p = u * R.colsum[f];
+  for (int f0 = 0; f0 < R.d; f0 += 64 * kC) {
+    double p[kC];
+#pragma unroll
+    for (int c = 0; c < kC; ++c) {
+      const int f = f0 + 64 * c + lane;
+      p[c] = f < R.d ? (static_cast<double>(xr[f]) / nr) * R.colsum[f] : 0.0;
     }
-    const int m = R.d - f0 < 64 ? R.d - f0 : 64;
-    for (int q = 0; q < m; ++q) acc = acc + readlane_f64(p, q);  // v_readlane: no LDS round trip
+#pragma unroll
+    for (int c = 0; c < kC; ++c) {
+      const int rest = __builtin_amdgcn_readfirstlane(R.d - f0 - 64 * c);
+      if (rest <= 0) break;
+      if (rest >= 64) {
+#pragma unroll
+        for (int q = 0; q < 64; ++q) acc = acc + readlane_f64(p[c], q);  // v_readlane: no LDS round trip
+      } else {
+        for (int q = 0; q < rest; ++q) acc = acc + readlane_f64(p[c], q);
+      }
+    }
   }
   if (!(fl & DAL_ROW_CANDIDATE)) {
     s = __builtin_nan("");
@@ -728,6 +742,11 @@ __global__ __launch_bounds__(256) void gather_selected_kernel(const int64_t* __r
 struct SortTail {
   int64_t cap = 0;
   bool cap_miss = false;
+  // candidates in n_reg regions of reg_stride entries (summary_select_kernel:
+  // one per block, reg_count[r] each) instead of one list of cand_count
+  int n_reg = 0;
+  int64_t reg_stride = 0;
+  const unsigned int* reg_count = nullptr;
   int32_t* status = nullptr;
   uint32_t* clear = nullptr;
   int64_t clear_words = 0;
@@ -771,14 +790,33 @@ __global__ __launch_bounds__(256) void publish_kernel(const int64_t* __restrict_
 // the bucket are compacted (any order) into sk/si/sp[0..m_out).  Returns
 // false (nothing written) when the bucket never shrinks that far (many equal
 // keys): the caller sorts everything.  Block-uniform.
+// Logical candidate e -> its slot: identity for one list, else region r with
+// pre[r] <= e < pre[r + 1] (pre: LDS prefix sums of the region counts; empty
+// regions repeat a value, the last such r is the one holding e).
+struct RegionMap {
+  int n = 0;
+  int64_t stride = 0;
+  const unsigned int* pre = nullptr;
+  __device__ int64_t operator()(int64_t e) const {
+    if (n == 0) return e;
+    int lo = 0, hi = n - 1;  // the last r with pre[r] <= e (binary search: <= 5 LDS reads)
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pre[mid] <= e) lo = mid;
+      else hi = mid - 1;
+    }
+    return lo * stride + (e - pre[lo]);
+  }
+};
+
 constexpr int64_t kSelMin = 1024;    // below this the full bitonic is cheap
 constexpr int64_t kRankMax = 512;    // at most this many: rank selection, no sorting network
 constexpr int64_t kSelMaxK = 1536;   // k + kSelSmall must fit the sort arrays
 constexpr int kSelSmall = 512;
 
 __device__ bool select_compact(const uint64_t* __restrict__ keys, const int64_t* __restrict__ idx,
-                               const double* __restrict__ pay, int64_t m, int64_t k, unsigned long long* sk,
-                               long long* si, double* sp, int64_t& m_out) {
+                               const double* __restrict__ pay, const RegionMap& M, int64_t m, int64_t k,
+                               unsigned long long* sk, long long* si, double* sp, int64_t& m_out) {
   __shared__ unsigned int hist[256];
   __shared__ unsigned long long s_prefix;
   __shared__ unsigned int s_krem, s_neq, s_count;
@@ -788,7 +826,7 @@ __device__ bool select_compact(const uint64_t* __restrict__ keys, const int64_t*
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     const int64_t e = tid + static_cast<int64_t>(j) * kSortThreads;
-    key[j] = e < m ? ld_sc1(keys + e) : 0ull;
+    key[j] = e < m ? ld_sc1(keys + M(e)) : 0ull;
   }
   unsigned long long prefix = 0, mask = 0;
   unsigned int krem = static_cast<unsigned int>(k), neq = static_cast<unsigned int>(m);
@@ -859,8 +897,8 @@ __device__ bool select_compact(const uint64_t* __restrict__ keys, const int64_t*
     if (take) {
       const unsigned p = base + static_cast<unsigned>(__popcll(tm & ((1ull << lane) - 1ull)));
       sk[p] = key[j];
-      si[p] = ld_sc1(idx + e);
-      sp[p] = ld_sc1(pay + e);
+      si[p] = ld_sc1(idx + M(e));
+      sp[p] = ld_sc1(pay + M(e));
     }
   }
   __syncthreads();
@@ -882,7 +920,28 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
   __shared__ int64_t* s_dest[2];
   const int tid = threadIdx.x;
   if (tid < 2) s_dest[tid] = load_out_slot(tail.out_slot, tid);  // host round trips, overlapping the sort
-  int64_t m = !h ? n_static : static_cast<int64_t>(ld_sc1(&h->cand_count));
+  __shared__ unsigned int s_pre[33];
+  RegionMap M;
+  int64_t m;
+  if (tail.n_reg) {
+    if (tid < tail.n_reg) s_pre[tid] = ld_sc1(tail.reg_count + tid);  // the counts' loads in parallel
+    __syncthreads();
+    if (tid == 0) {
+      unsigned long long tot = 0;
+      for (int r = 0; r < tail.n_reg; ++r) {
+        const unsigned c = s_pre[r];
+        s_pre[r] = static_cast<unsigned>(tot);
+        tot += c < tail.reg_stride ? c : static_cast<unsigned>(tail.reg_stride);
+        if (c > tail.reg_stride) tot = ~0ull >> 1;  // a region over capacity: miss
+      }
+      s_pre[tail.n_reg] = tot > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<unsigned>(tot);
+    }
+    __syncthreads();
+    M = RegionMap{tail.n_reg, tail.reg_stride, s_pre};
+    m = s_pre[tail.n_reg];
+  } else {
+    m = !h ? n_static : static_cast<int64_t>(ld_sc1(&h->cand_count));
+  }
   if (tail.cap_miss && tid == 0 && m > tail.cap) atomicOr(tail.status, DAL_FLAG_SAMPLE_MISS);
   if (tail.cap && m > tail.cap) m = tail.cap;
   if (m > CAP) m = CAP;
@@ -900,9 +959,10 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
     // adds them): m / tpe dependent LDS reads per lane instead of m (one
     // lane per element: ~10 us at m = 110).
     for (int i = tid; i < m; i += kSortThreads) {
-      sk[i] = ld_sc1(keys + i);
-      si[i] = ld_sc1(idx + i);
-      if (PAY) sp[i] = ld_sc1(pay + i);
+      const int64_t q = M(i);
+      sk[i] = ld_sc1(keys + q);
+      si[i] = ld_sc1(idx + q);
+      if (PAY) sp[i] = ld_sc1(pay + q);
     }
     __syncthreads();
     if (tail.clear) {  // every thread read the header above
@@ -953,7 +1013,8 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
     return;
   }
   bool loaded = false;
-  if (PAY && h && m > kSelMin && k <= kSelMaxK && k < m) loaded = select_compact(keys, idx, pay, m, k, sk, si, sp, m);
+  if (PAY && h && m > kSelMin && k <= kSelMaxK && k < m)
+    loaded = select_compact(keys, idx, pay, M, m, k, sk, si, sp, m);
   int mp = 2;
   while (mp < m) mp <<= 1;
   for (int i = tid; i < mp; i += kSortThreads) {
@@ -964,9 +1025,10 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
         if (PAY) sp[i] = 0.0;
       }
     } else if (i < m) {
-      sk[i] = ld_sc1(keys + i);
-      si[i] = ld_sc1(idx + i);
-      if (PAY) sp[i] = ld_sc1(pay + i);
+      const int64_t q = M(i);
+      sk[i] = ld_sc1(keys + q);
+      si[i] = ld_sc1(idx + q);
+      if (PAY) sp[i] = ld_sc1(pay + q);
     } else {
       sk[i] = ~0ull;
       si[i] = 0x7FFFFFFFFFFFFFFFll;
@@ -1060,15 +1122,14 @@ struct GroupSummary {
 // keys' differing low bits (the common high bits of the minimum and maximum
 // -- for DW keys the sign and most of the exponent -- are skipped; up to 4
 // keys per thread in registers, 8-bit digits) until the k-th key's bucket
-// holds <= 64 keys, which one wave then ranks.  Every block computes it (no
-// grid sync).
+// holds <= 64 keys; tau is that bucket's upper edge.  Every block computes it
+// (no grid sync).
 __device__ unsigned long long group_threshold(const GroupSummary& S, int64_t k) {
   constexpr int PER = kMaxGroups / kSumThreads;
   constexpr int W = kSumThreads / 64;
   __shared__ unsigned int hist[256];
-  __shared__ unsigned long long s_prefix, s_tau, s_mn[W], s_mx[W];
-  __shared__ unsigned int s_krem, s_cnt, s_n, s_nv[W];
-  __shared__ unsigned long long s_bucket[64];
+  __shared__ unsigned long long s_prefix, s_mn[W], s_mx[W];
+  __shared__ unsigned int s_krem, s_cnt, s_nv[W];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (k > S.ng) return DAL_KEY_NONE;
   unsigned long long key[PER];
@@ -1162,25 +1223,10 @@ __device__ unsigned long long group_threshold(const GroupSummary& S, int64_t k) 
     mask |= static_cast<unsigned long long>(dmask) << shift;
     top = shift;
   }
-  if (top == 0) return prefix;  // every bit resolved (equal keys)
-  if (tid == 0) s_n = 0u;
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < PER; ++j)
-    if (val[j] && (key[j] & mask) == prefix) s_bucket[atomicAdd(&s_n, 1u)] = key[j];
-  __syncthreads();
-  if (tid < 64) {  // rank the bucket's keys: the krem-th smallest is tau
-    const unsigned long long mine = lane < static_cast<int>(cnt) ? s_bucket[lane] : 0ull;
-    unsigned lt = 0, le = 0;
-    for (unsigned j = 0; j < cnt; ++j) {
-      const unsigned long long o = s_bucket[j];
-      lt += o < mine;
-      le += o <= mine;
-    }
-    if (lane < static_cast<int>(cnt) && lt < krem && krem <= le) s_tau = mine;  // (equal keys: same value)
-  }
-  __syncthreads();
-  return s_tau;
+  // the upper edge of the k-th key's bucket: >= the k-th group minimum, and at
+  // most the bucket's <= 64 keys above it (ranking them exactly -- a gather
+  // and two more barriers -- cost more than the few extra candidates)
+  return prefix | (top >= 64 ? ~0ull : ((1ull << top) - 1ull));
 }
 
 // Group minima of the keys (the standalone selections; dal_dw_step's score
@@ -1260,14 +1306,17 @@ __global__ __launch_bounds__(kSumThreads) void summary_select_kernel(
     uint64_t* __restrict__ out_keys, int64_t* __restrict__ out_idx, double* __restrict__ out_scores, SortTail tail) {
   constexpr int W = kSumThreads / 64;
   __shared__ int s_hits[kMaxGroups / 32];  // per <= 128 groups (summary_grid)
-  __shared__ unsigned s_nh, s_last;
+  __shared__ unsigned s_nh, s_nc, s_last;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const unsigned long long tau = group_threshold(S, k);
   if (blockIdx.x == 0 && tid == 0) h->kstar = tau;
   const int64_t per = ceil_div(S.ng, static_cast<int64_t>(gridDim.x));
   const int64_t g0 = static_cast<int64_t>(blockIdx.x) * per;
   const int64_t g1 = g0 + per < S.ng ? g0 + per : S.ng;
-  if (tid == 0) s_nh = 0u;
+  if (tid == 0) {
+    s_nh = 0u;
+    s_nc = 0u;
+  }
   __syncthreads();
   for (int64_t g = g0 + tid; g < g1; g += kSumThreads) {
     const unsigned long long m = ~S.ginv[S.ng + g];
@@ -1298,10 +1347,6 @@ __global__ __launch_bounds__(kSumThreads) void summary_select_kernel(
         const bool cand = (cbits >> j) & 1u;
         const unsigned long long cm = __ballot(cand);
         if (!cm) continue;
-        // the slot reservation goes out first: its round trip overlaps the
-        // re-rank's loads (the value is read after the score)
-        unsigned base = 0;
-        if (lane == 0) base = atomicAdd(&h->cand_count, static_cast<unsigned>(__popcll(cm)));
         if constexpr (DW) {
           double my_s = 0.0;
           bool my_ok = false;
@@ -1321,13 +1366,20 @@ __global__ __launch_bounds__(kSumThreads) void summary_select_kernel(
               }
             }
           }
+          // slots in this block's region (an LDS counter: same-address device
+          // atomics from ~100 waves serialised at ~0.1 us each)
+          unsigned base = 0;
+          if (lane == 0) base = atomicAdd(&s_nc, static_cast<unsigned>(__popcll(cm)));
           const int64_t p = static_cast<int64_t>(__shfl(base, 0)) + __popcll(cm & lt_mask);
           if (cand && p < cap) {
-            st_sc1(cidx + p, static_cast<int64_t>(idx_base + i));
-            st_sc1(AR.cpay + p, my_s);
-            st_sc1(AR.ckey + p, static_cast<uint64_t>(my_ok ? score_key(my_s, DAL_DESCENDING) : DAL_KEY_NONE));
+            const int64_t q = static_cast<int64_t>(blockIdx.x) * cap + p;
+            st_sc1(cidx + q, static_cast<int64_t>(idx_base + i));
+            st_sc1(AR.cpay + q, my_s);
+            st_sc1(AR.ckey + q, static_cast<uint64_t>(my_ok ? score_key(my_s, DAL_DESCENDING) : DAL_KEY_NONE));
           }
         } else {
+          unsigned base = 0;
+          if (lane == 0) base = atomicAdd(&h->cand_count, static_cast<unsigned>(__popcll(cm)));
           const int64_t p = static_cast<int64_t>(__shfl(base, 0)) + __popcll(cm & lt_mask);
           if (cand && p < cap) cidx[p] = idx_base + i;
         }
@@ -1335,7 +1387,9 @@ __global__ __launch_bounds__(kSumThreads) void summary_select_kernel(
     }
   }
   if constexpr (!DW) return;
-  // the last block to arrive sorts the candidates
+  // this block's count, then the last block to arrive sorts the candidates
+  __syncthreads();
+  if (tid == 0) st_sc1(&h->reg_count[blockIdx.x], s_nc);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
@@ -1469,8 +1523,9 @@ extern "C" int dal_topk(const uint64_t* keys, int64_t n, int64_t k, int64_t idx_
 // selected positions and the fast level 1's group minima ([2][kMaxGroups]).
 struct RerankWs {
   TopkLayout L1, L2;
-  size_t l2, pos, gmin, total;
+  size_t l2, pos, gmin, reg, total;
 };
+constexpr int kMaxSumBlocks = 32;  // summary_select_kernel blocks (candidate regions)
 
 static RerankWs rerank_ws(int64_t n, int64_t k, int64_t cap) {
   RerankWs W;
@@ -1479,7 +1534,9 @@ static RerankWs rerank_ws(int64_t n, int64_t k, int64_t cap) {
   W.l2 = W.L1.total;
   W.pos = W.l2 + W.L2.total;
   W.gmin = W.pos + round_up(k * 8, 256);
-  W.total = W.gmin + round_up(2 * kMaxGroups * 8, 256);
+  // per-block candidate regions of the fast level 1: keys | indices | scores
+  W.reg = W.gmin + round_up(2 * kMaxGroups * 8, 256);
+  W.total = W.reg + 3 * round_up(kMaxSumBlocks * cap * 8, 256);
   return W;
 }
 
@@ -1492,6 +1549,27 @@ static int check_rerank_args(int64_t n, int64_t k, int64_t cap, int passes, void
   if (k > DAL_SORT_CAP) return DAL_ERR_CAPACITY;
   if (ws_bytes < rerank_ws_bytes(n, k, cap) || (reinterpret_cast<uintptr_t>(ws) & 255)) return DAL_ERR_SHAPE;
   return DAL_OK;
+}
+
+// The density-weighted fast level 1 writes its candidates into per-block
+// regions of the workspace (keys | indices | scores, cap each).
+struct DwRegions {
+  uint64_t* keys;
+  int64_t* idx;
+  double* pay;
+};
+
+static DwRegions dw_regions(void* ws, const RerankWs& W, int64_t cap) {
+  char* r = static_cast<char*>(ws) + W.reg;
+  const size_t part = round_up(kMaxSumBlocks * cap * 8, 256);
+  return DwRegions{reinterpret_cast<uint64_t*>(r), reinterpret_cast<int64_t*>(r + part),
+                   reinterpret_cast<double*>(r + 2 * part)};
+}
+
+static void set_regions(SortTail& tail, TopkHdr* h, int64_t cap, int blocks) {
+  tail.n_reg = blocks;
+  tail.reg_stride = cap;
+  tail.reg_count = h->reg_count;
 }
 
 // The standalone fast level 1: group minima (one pass over both keys; block 0
@@ -1512,9 +1590,18 @@ static int launch_fast_level1(const uint64_t* keys_lo, const uint64_t* keys_hi, 
   tail.status = status;
   tail.clear = reinterpret_cast<uint32_t*>(h1);
   tail.clear_words = kFastHdrWords;
-  hipLaunchKernelGGL(summary_select_kernel<DW>, dim3(static_cast<unsigned>(summary_grid(S.ng))), dim3(kSumThreads),
-                     0, st, keys_hi, n, k, idx_base, S, h1, reinterpret_cast<int64_t*>(base + W.L1.cidx), cap, AR,
-                     0, out_keys, out_idx, out_scores, tail);
+  const int G = summary_grid(S.ng);
+  AppendRerank A = AR;
+  int64_t* cidx = reinterpret_cast<int64_t*>(base + W.L1.cidx);
+  if (DW) {  // candidates in per-block regions, gathered by the last block
+    const DwRegions Rg = dw_regions(ws, W, cap);
+    A.ckey = Rg.keys;
+    A.cpay = Rg.pay;
+    cidx = Rg.idx;
+    set_regions(tail, h1, cap, G);
+  }
+  hipLaunchKernelGGL(summary_select_kernel<DW>, dim3(static_cast<unsigned>(G)), dim3(kSumThreads), 0, st, keys_hi, n,
+                     k, idx_base, S, h1, cidx, cap, A, 0, out_keys, out_idx, out_scores, tail);
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
 }
@@ -1707,11 +1794,11 @@ int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_
   }
   tail.out_slot = out_slot;
   tail.status_mirror = status_mirror;
-  hipLaunchKernelGGL(summary_select_kernel<true>, dim3(static_cast<unsigned>(summary_grid(S.ng))),
-                     dim3(kSumThreads), 0, st, keys_hi, n, k, idx_base, S, h1,
-                     reinterpret_cast<int64_t*>(base + W.L1.cidx), cap,
-                     AppendRerank{R, reinterpret_cast<uint64_t*>(base + W.L1.ckey),
-                                  reinterpret_cast<double*>(base + W.L1.cpay)},
+  const int G = summary_grid(S.ng);
+  const DwRegions Rg = dw_regions(ws, W, cap);
+  set_regions(tail, h1, cap, G);
+  hipLaunchKernelGGL(summary_select_kernel<true>, dim3(static_cast<unsigned>(G)), dim3(kSumThreads), 0, st, keys_hi,
+                     n, k, idx_base, S, h1, Rg.idx, cap, AppendRerank{R, Rg.keys, Rg.pay},
                      n_lut, out_keys, out_idx, out_scores, tail);
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;

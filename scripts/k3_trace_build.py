@@ -37,22 +37,23 @@ sub("""  if (!s_last) return;
 }""", """  K3T(64 + blockIdx.x);
   if (!s_last) return;
   K3T(3);
-  if (tid == 0) { g_k3[4] = ld_sc1(&h->cand_count); g_k3[5] = gridDim.x; }
+  if (tid == 0) g_k3[5] = gridDim.x;
   sort_tail_body<true>(AR.ckey, cidx, AR.cpay, h, int64_t{0}, k, out_keys, out_idx, out_scores, tail);
   __syncthreads();
   K3T(6);
 }""")
 sub("""  if (nv < k) return DAL_KEY_NONE;  // (block-uniform)""", """  if (blockIdx.x == 0) K3T(10);
   if (nv < k) return DAL_KEY_NONE;  // (block-uniform)""")
-sub("""  if (top == 0) return prefix;  // every bit resolved (equal keys)""", """  if (blockIdx.x == 0) K3T(11);
+sub("""  // the upper edge of the k-th key's bucket: >= the k-th group minimum, and at""", """  if (blockIdx.x == 0) K3T(11);
   if (blockIdx.x == 0 && threadIdx.x == 0) g_k3[13] = cnt;
-  if (top == 0) return prefix;  // every bit resolved (equal keys)""")
-sub("""  if (m <= kRankMax) {""", """  K3T(7);
+  // the upper edge of the k-th key's bucket: >= the k-th group minimum, and at""")
+sub("""  if (m <= kRankMax) {""", """  if (threadIdx.x == 0) g_k3[4] = m;
+  K3T(7);
   if (m <= kRankMax) {""")
-sub("""      if (PAY) sp[i] = ld_sc1(pay + i);
+sub("""      if (PAY) sp[i] = ld_sc1(pay + q);
     }
     __syncthreads();
-    if (tail.clear) {  // every thread read the header above""", """      if (PAY) sp[i] = ld_sc1(pay + i);
+    if (tail.clear) {  // every thread read the header above""", """      if (PAY) sp[i] = ld_sc1(pay + q);
     }
     __syncthreads();
     K3T(8);
@@ -69,14 +70,14 @@ sub("""      if (!__ballot(cbits != 0)) continue;""", """      const unsigned lo
       if (!__ballot(cbits != 0)) continue;""")
 sub("""          const int64_t p = static_cast<int64_t>(__shfl(base, 0)) + __popcll(cm & lt_mask);
           if (cand && p < cap) {
-            st_sc1(cidx + p, static_cast<int64_t>(idx_base + i));""", """          const int64_t p = static_cast<int64_t>(__shfl(base, 0)) + __popcll(cm & lt_mask);
+            const int64_t q = static_cast<int64_t>(blockIdx.x) * cap + p;""", """          const int64_t p = static_cast<int64_t>(__shfl(base, 0)) + __popcll(cm & lt_mask);
           const unsigned long long tc = __builtin_amdgcn_s_memrealtime();
           if (lane == 0) atomicMax(&g_k3[21], tc - tb);
           if (cand && p < cap) {
-            st_sc1(cidx + p, static_cast<int64_t>(idx_base + i));""")
-sub("""  // the last block to arrive sorts the candidates
+            const int64_t q = static_cast<int64_t>(blockIdx.x) * cap + p;""")
+sub("""  if (tid == 0) st_sc1(&h->reg_count[blockIdx.x], s_nc);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();""", """  // the last block to arrive sorts the candidates
+  __syncthreads();""", """  if (tid == 0) st_sc1(&h->reg_count[blockIdx.x], s_nc);
   const unsigned long long te = __builtin_amdgcn_s_memrealtime();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
