@@ -747,6 +747,7 @@ struct SortTail {
   int n_reg = 0;
   int64_t reg_stride = 0;
   const unsigned int* reg_count = nullptr;
+  int64_t reg_uniform = 0;  // > 0: every region holds this many (no reg_count)
   int32_t* status = nullptr;
   uint32_t* clear = nullptr;
   int64_t clear_words = 0;
@@ -924,7 +925,8 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
   RegionMap M;
   int64_t m;
   if (tail.n_reg) {
-    if (tid < tail.n_reg) s_pre[tid] = ld_sc1(tail.reg_count + tid);  // the counts' loads in parallel
+    if (tid < tail.n_reg)  // the counts' loads in parallel
+      s_pre[tid] = tail.reg_uniform ? static_cast<unsigned>(tail.reg_uniform) : ld_sc1(tail.reg_count + tid);
     __syncthreads();
     if (tid == 0) {
       unsigned long long tot = 0;
@@ -951,9 +953,9 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
   // full bitonic over 4,096 keys is LDS-bound (~95 us).  Same result: every
   // key of the top k lies in the sorted subset.
   if (m <= kRankMax) {
-    // short lists (the common case: ~100-300 candidates): rank selection.  The
-    // (key, index) pairs are distinct, so every element's rank -- the count of
-    // smaller pairs, read as LDS broadcasts -- is its output position: two
+    // short lists (the common case: ~100-300 candidates): rank selection.
+    // Every element's rank -- the count of smaller (key, index, position)
+    // triples, read as LDS broadcasts -- is its output position: two
     // barriers instead of the bitonic network's log^2 m stages.  tpe lanes of
     // one wave share an element (each counts every tpe-th pair, a butterfly
     // adds them): m / tpe dependent LDS reads per lane instead of m (one
@@ -985,7 +987,9 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
 #pragma unroll 4
         for (int j = part; j < m; j += tpe) {
           const unsigned long long kj = sk[j];
-          r += kj < ke || (kj == ke && si[j] < ie);
+          const long long ij = si[j];
+          // equal pairs (the merge's padding: NONE key, index -1) rank by position
+          r += kj < ke || (kj == ke && (ij < ie || (ij == ie && j < e)));
         }
       }
       for (int o = 1; o < tpe; o <<= 1) r += __shfl_xor(r, o);
@@ -1013,7 +1017,7 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
     return;
   }
   bool loaded = false;
-  if (PAY && h && m > kSelMin && k <= kSelMaxK && k < m)
+  if (PAY && (h || tail.n_reg) && m > kSelMin && k <= kSelMaxK && k < m)
     loaded = select_compact(keys, idx, pay, M, m, k, sk, si, sp, m);
   int mp = 2;
   while (mp < m) mp <<= 1;
@@ -1902,20 +1906,58 @@ __global__ __launch_bounds__(256) void merge_gather_kernel(const int64_t* __rest
 }  // namespace
 }  // namespace dal
 
+namespace dal {
+namespace {
+// The merge in ONE launch when the P x k candidates fit the payload sort:
+// the packed rows are P regions of the sort tail (keys | indices | score
+// bits at offsets 0, k, 2k of a row), ordered by (key, global index) --
+// the same order as (key, rank-major position): ranks hold ascending row
+// ranges and each rank's list is sorted by (key, index); padding keys sort
+// last -- and the status words are OR-ed by thread 0.
+__global__ __launch_bounds__(kSortThreads) void merge_rows_kernel(const int64_t* __restrict__ packed, int64_t n_ranks,
+                                                                  int64_t width, int64_t k,
+                                                                  int64_t* __restrict__ out_idx,
+                                                                  double* __restrict__ out_scores,
+                                                                  uint64_t* __restrict__ out_keys,
+                                                                  int32_t* __restrict__ status_or) {
+  if (status_or && threadIdx.x == 0) {
+    int32_t s = 0;
+    for (int64_t r = 0; r < n_ranks; ++r) s |= static_cast<int32_t>(packed[r * width + 3 * k]);
+    *status_or = s;
+  }
+  SortTail tail;
+  tail.n_reg = static_cast<int>(n_ranks);
+  tail.reg_stride = width;
+  tail.reg_uniform = k;
+  sort_tail_body<true>(reinterpret_cast<const uint64_t*>(packed), packed + k,
+                       reinterpret_cast<const double*>(packed + 2 * k), nullptr, int64_t{0}, k, out_keys, out_idx,
+                       out_scores, tail);
+}
+}  // namespace
+}  // namespace dal
+
 extern "C" size_t dal_topk_merge_workspace_bytes(int64_t n_ranks, int64_t k) {
   if (n_ranks < 1 || k < 1) return 0;
+  if (n_ranks * k <= DAL_SORT_CAP_PAYLOAD && n_ranks <= 32) return 0;  // the one-launch merge
   return static_cast<size_t>(n_ranks * k) * 16 + static_cast<size_t>(k) * 16;
 }
 
 extern "C" int dal_topk_merge(const int64_t* packed, int64_t n_ranks, int64_t width, int64_t k, void* ws,
                               size_t ws_bytes, int64_t* out_idx, double* out_scores, uint64_t* out_keys,
                               int32_t* status_or, dal_stream_t stream) {
-  if (!packed || !ws || !out_idx || !out_scores) return DAL_ERR_ARG;
+  if (!packed || !out_idx || !out_scores) return DAL_ERR_ARG;
   if (n_ranks < 1 || k < 1 || width < 3 * k + (status_or ? 1 : 0)) return DAL_ERR_SHAPE;
   const int64_t n = n_ranks * k;
   if (n > DAL_SORT_CAP) return DAL_ERR_CAPACITY;
-  if (ws_bytes < dal_topk_merge_workspace_bytes(n_ranks, k)) return DAL_ERR_CAPACITY;
   hipStream_t st = as_stream(stream);
+  if (n <= DAL_SORT_CAP_PAYLOAD && n_ranks <= 32) {  // one launch, no workspace
+    hipLaunchKernelGGL(merge_rows_kernel, dim3(1), dim3(kSortThreads), 0, st, packed, n_ranks, width, k, out_idx,
+                       out_scores, out_keys, status_or);
+    DAL_RETURN_IF_LAUNCH_FAILED();
+    return DAL_OK;
+  }
+  if (!ws) return DAL_ERR_ARG;
+  if (ws_bytes < dal_topk_merge_workspace_bytes(n_ranks, k)) return DAL_ERR_CAPACITY;
   uint64_t* keys = static_cast<uint64_t*>(ws);
   int64_t* pos = reinterpret_cast<int64_t*>(keys + n);
   uint64_t* ws_keys = reinterpret_cast<uint64_t*>(pos + n);

@@ -517,13 +517,14 @@ def merge_row(comm, packed, k: int, all_valid: bool = False):
     n_ranks = int(g.shape[0])
     lib = _lib.load()
     wsb = int(lib.dal_topk_merge_workspace_bytes(n_ranks, k))
-    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
-    out_idx = torch.empty(k, dtype=torch.int64, device=dev)
-    out_sc = torch.empty(k, dtype=torch.float64, device=dev)
-    out_keys = None if all_valid else torch.empty(k, dtype=torch.int64, device=dev)
-    st_or = torch.empty(1, dtype=torch.int32, device=dev)
-    call("dal_topk_merge", _ptr(g), n_ranks, w, k, _ptr(ws), wsb, _ptr(out_idx), _ptr(out_sc),
-         0 if out_keys is None else _ptr(out_keys), _ptr(st_or), _stream(dev))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev) if wsb else None  # (the one-launch merge needs none)
+    # the outputs in one allocation: indices | score bits | (keys) | status
+    buf = torch.empty((2 if all_valid else 3) * k + 1, dtype=torch.int64, device=dev)
+    out_idx, out_sc = buf[:k], buf[k:2 * k].view(torch.float64)
+    out_keys = None if all_valid else buf[2 * k:3 * k]
+    st_or = buf[-1:].view(torch.int32)[:1]
+    call("dal_topk_merge", _ptr(g), n_ranks, w, k, 0 if ws is None else _ptr(ws), wsb, _ptr(out_idx),
+         _ptr(out_sc), 0 if out_keys is None else _ptr(out_keys), _ptr(st_or), _stream(dev))
     st = int(st_or.item())
     if out_keys is not None:
         valid = out_keys != _as_i64(DAL_KEY_NONE)

@@ -402,7 +402,11 @@ int dal_sort_pairs(const uint64_t* keys, const int64_t* idx, const double* paylo
  * by global row index -- to out_idx / out_scores, and the OR of the status
  * words to *status_or (nullable), the winners' keys to out_keys (nullable;
  * DAL_KEY_NONE marks padding that won only because fewer than k candidates
- * exist).  Three launches; n_ranks * k <= DAL_SORT_CAP.
+ * exist).  n_ranks * k <= DAL_SORT_CAP.  One launch and no workspace (ws may
+ * be NULL; dal_topk_merge_workspace_bytes returns 0) when n_ranks * k <=
+ * DAL_SORT_CAP_PAYLOAD and n_ranks <= 32: the rows are read in place by the
+ * one-block sort, ordered by (key, global index) -- the same order, as ranks
+ * hold ascending row ranges; otherwise three launches (unpack, sort, gather).
  * Replaces the sortBy(...).take(k) of density_weighting.py:168,172 across
  * shards (the Spark range-partition sort over all executors). */
 size_t dal_topk_merge_workspace_bytes(int64_t n_ranks, int64_t k);

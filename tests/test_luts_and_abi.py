@@ -81,13 +81,15 @@ def test_merge_and_mark_count_validation_without_gpu():
     """ABI v4 entry points reject bad arguments before any HIP call."""
     lib = _lib.load()
     p = ctypes.c_void_p(256)
-    assert lib.dal_topk_merge_workspace_bytes(8, 100) == 8 * 100 * 16 + 100 * 16
+    assert lib.dal_topk_merge_workspace_bytes(8, 1000) == 8 * 1000 * 16 + 1000 * 16
+    assert lib.dal_topk_merge_workspace_bytes(8, 100) == 0  # one launch, no workspace
     assert lib.dal_topk_merge_workspace_bytes(0, 100) == 0
     assert lib.dal_topk_merge(None, 2, 301, 100, p, 1 << 20, p, p, None, p, None) == -1
     assert lib.dal_topk_merge(p, 2, 300, 100, p, 1 << 20, p, p, None, p, None) == -2  # no room for status
     assert lib.dal_topk_merge(p, 0, 301, 100, p, 1 << 20, p, p, None, p, None) == -2
     assert lib.dal_topk_merge(p, 9, 3001, 1000, p, 1 << 20, p, p, None, p, None) == -5  # > DAL_SORT_CAP
-    assert lib.dal_topk_merge(p, 2, 301, 100, p, 16, p, p, None, p, None) == -5  # workspace too small
+    assert lib.dal_topk_merge(p, 5, 3001, 1000, p, 16, p, p, None, p, None) == -5  # workspace too small
+    assert lib.dal_topk_merge(p, 5, 3001, 1000, None, 1 << 30, p, p, None, p, None) == -1  # needs one
     assert lib.dal_mark_rows_count(None, 10, 0, 10, 1, p, p, None) == -1
     assert lib.dal_mark_rows_count(p, 10, 0, 10, 1, p, None, None) == -1
     assert lib.dal_mark_rows_count(p, -1, 0, 10, 1, p, p, None) == -2
