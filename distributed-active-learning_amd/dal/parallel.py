@@ -369,9 +369,28 @@ class TorchComm:
         self.dist = dist
         self.group = group
         self.world = dist.get_world_size(group)
+        self.backend = dist.get_backend(group)
         # RCCL collectives are asynchronous on their own stream: they can run
         # beside a Gram launch (gloo stages through the host synchronously)
-        self.overlaps = dist.get_backend(group) == "nccl"
+        self.overlaps = self.backend == "nccl"
+        self._rows = {}  # (width, device) -> the merge's gathered-rows buffer
+
+    def all_gather_rows(self, row):
+        """All-gather one int64 row per rank into a buffer kept for the next
+        step ([P, w]; its previous contents were consumed by the previous
+        merge, which the step's status read waited for).  The warm multi-GPU
+        step's collective, with the fewest host calls (RCCL: enqueued on the
+        communicator's stream, ordered before the current stream's next work)."""
+        torch = __import__("torch")
+        if not row.is_cuda or self.backend == "gloo":
+            return self.all_gather(row.reshape(1, -1))
+        w = int(row.shape[0])
+        key = (w, row.device)
+        out = self._rows.get(key)
+        if out is None:
+            out = self._rows[key] = torch.empty((self.world, w), dtype=row.dtype, device=row.device)
+        self.dist.all_gather_into_tensor(out, row, group=self.group)
+        return out
 
     def all_gather(self, t):
         out, work = self.all_gather_start(t)
@@ -385,7 +404,7 @@ class TorchComm:
         if t.dim() and _needs_bytes(t.dtype):
             out, work = self.all_gather_start(t.contiguous().view(torch.uint8))
             return out.view(t.dtype), work
-        if t.is_cuda and self.dist.get_backend(self.group) == "gloo":
+        if t.is_cuda and self.backend == "gloo":
             # rehearsal path (several ranks sharing one GPU): stage through the host
             return self.all_gather(t.cpu()).to(t.device), None
         out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
@@ -400,7 +419,7 @@ class TorchComm:
         torch = __import__("torch")
         m = t.shape[0] // self.world
         rank = self.dist.get_rank(self.group)
-        if self.dist.get_backend(self.group) == "gloo":
+        if self.backend == "gloo":
             h = t.cpu()
             self.dist.all_reduce(h, op=self.dist.ReduceOp.SUM, group=self.group)
             return h[rank * m:(rank + 1) * m].to(t.device)
@@ -513,19 +532,21 @@ def merge_row(comm, packed, k: int, all_valid: bool = False):
 
     dev = packed.device
     w = int(packed.shape[0])
-    g = comm.all_gather(packed.reshape(1, w))  # [P, 3k + 1]
+    g = comm.all_gather_rows(packed) if hasattr(comm, "all_gather_rows") else comm.all_gather(packed.reshape(1, w))
     n_ranks = int(g.shape[0])
     lib = _lib.load()
     wsb = int(lib.dal_topk_merge_workspace_bytes(n_ranks, k))
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev) if wsb else None  # (the one-launch merge needs none)
     # the outputs in one allocation: indices | score bits | (keys) | status
-    buf = torch.empty((2 if all_valid else 3) * k + 1, dtype=torch.int64, device=dev)
+    nk = 2 if all_valid else 3
+    buf = torch.empty(nk * k + 1, dtype=torch.int64, device=dev)
+    b0 = buf.data_ptr()
+    call("dal_topk_merge", _ptr(g), n_ranks, w, k, 0 if ws is None else _ptr(ws), wsb, b0, b0 + 8 * k,
+         0 if all_valid else b0 + 16 * k, b0 + 8 * nk * k, _stream(dev))
+    st = int(buf[nk * k].item()) & 0xFFFFFFFF  # the int32 status in the low half (little endian)
+    st = st - (1 << 32) if st >= (1 << 31) else st
     out_idx, out_sc = buf[:k], buf[k:2 * k].view(torch.float64)
     out_keys = None if all_valid else buf[2 * k:3 * k]
-    st_or = buf[-1:].view(torch.int32)[:1]
-    call("dal_topk_merge", _ptr(g), n_ranks, w, k, 0 if ws is None else _ptr(ws), wsb, _ptr(out_idx),
-         _ptr(out_sc), 0 if out_keys is None else _ptr(out_keys), _ptr(st_or), _stream(dev))
-    st = int(st_or.item())
     if out_keys is not None:
         valid = out_keys != _as_i64(DAL_KEY_NONE)
         out_idx, out_sc = out_idx[valid], out_sc[valid]
