@@ -307,15 +307,10 @@ extern "C" int dal_canon_colsum_partials(const float* x, int64_t n, int64_t d, i
   // features per block: 8 (scripts/colsum_ab.py: 100k x 64 33.3 -> 27.8 us, 284,807 x 30
   // 48.4 -> 36.6, 2M x 256 2.31 -> 1.58 ms against 16; 4 and 32 slower): more, smaller
   // blocks keep more of the sequential 256-add chains in flight
-  int cf = 8;
-  if (const char* e = getenv("DAL_COLSUM_FEAT")) cf = atoi(e);  // timing knob (A/B runs): 8, 16
-#define DAL_COLSUM_LAUNCH(CF)                                                                             \
-  hipLaunchKernelGGL(canon_colsum_partials_kernel<CF>,                                                   \
-                     dim3(static_cast<unsigned>(chunks), static_cast<unsigned>(ceil_div(d, CF))), dim3(256), \
-                     0, as_stream(stream), x, n, static_cast<int>(d), ldx, norm64, row_flags, partials)
-  if (cf == 16) DAL_COLSUM_LAUNCH(16);
-  else DAL_COLSUM_LAUNCH(8);
-#undef DAL_COLSUM_LAUNCH
+  constexpr int kCf = 8;
+  hipLaunchKernelGGL(canon_colsum_partials_kernel<kCf>,
+                     dim3(static_cast<unsigned>(chunks), static_cast<unsigned>(ceil_div(d, kCf))), dim3(256), 0,
+                     as_stream(stream), x, n, static_cast<int>(d), ldx, norm64, row_flags, partials);
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
 }
