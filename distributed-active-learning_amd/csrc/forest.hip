@@ -74,111 +74,19 @@ __device__ __forceinline__ uint8_t row_flag(const ForestArgs& A, int64_t row) {
   return static_cast<uint8_t>(A.hooks.base_flags[row] | (cand ? DAL_ROW_CANDIDATE : 0));
 }
 
-template <bool X_LDS, bool F_LDS>
-__global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs A, int R, int tpr,
-                                                                      int x_floats, bool vec4, bool pad4,
-                                                                      bool pre, bool dma) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* xs = reinterpret_cast<float*>(smem);
-  if (A.hooks.status_reset && blockIdx.x == 0 && threadIdx.x == 0) *A.hooks.status_reset = 0;
+// Votes, score and keys of tile `tile` (R rows from LDS or global memory),
+// and the tile's minimum keys folded into its row group (hooks.gmin).
+template <bool X_LDS>
+__device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs, int xstride, int64_t tile, int R,
+                                           int tpr, const int2* inner, const uint8_t* leaf, bool pre,
+                                           uint8_t fl_pre, long long dens_pre) {
   const int n_inner = (1 << A.depth) - 1;
   const int n_leaf = 1 << A.depth;
-  const int2* inner = A.inner;
-  const uint8_t* leaf = A.leaf;
   const int tid = threadIdx.x;
-  if (F_LDS) {
-    int2* fs = reinterpret_cast<int2*>(smem + static_cast<size_t>(x_floats) * 4);
-    uint8_t* ls = reinterpret_cast<uint8_t*>(fs + A.n_trees * n_inner);
-    for (int e = tid; e < A.n_trees * n_inner; e += kForestThreads) fs[e] = A.inner[e];
-    for (int e = tid; e < A.n_trees * n_leaf; e += kForestThreads) ls[e] = A.leaf[e];
-    inner = fs;
-    leaf = ls;
-  }
-  // row stride in LDS: d + 1 words for scalar staging; with 16-B staging
-  // d + 4 (rows stay 16-B aligned, one ds_write_b128 per load, consecutive
-  // lanes on consecutive banks; rows of a wave start 4 banks apart)
-  const int xstride = A.d + (pad4 ? 4 : 1);
-  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * R;
+  const int64_t row0 = tile * R;
   const int r = tid / tpr, sub = tid - r * tpr;
   const int64_t row = row0 + r;
   const bool live = r < R && row < A.n;
-  // the row leader's epilogue inputs are loaded with the tile (one HBM
-  // latency per block instead of two)
-  uint8_t fl_pre = DAL_ROW_CANDIDATE;
-  long long dens_pre = 0;
-  if (pre && live && sub == 0) {
-    if (A.flags) fl_pre = row_flag(A, row);
-    if (A.dkind) dens_pre = static_cast<const long long*>(A.density)[row];
-  }
-  if (X_LDS) {
-    const int rows_here = static_cast<int>(min(static_cast<int64_t>(R), A.n - row0));
-    if (dma) {
-      // LDS-DMA staging (d % 4 == 0, 16-B-aligned padded rows): one
-      // global_load_lds_dwordx4 per 1 KiB of a row (the last piece with only
-      // the lanes it needs), lane l's 16 B landing at M0 + 16 l; no VGPRs and
-      // no LDS write instructions (2M x 256: 535 -> 433 us)
-      const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-      const int row_bytes = A.d * 4;
-      for (int rr = wave; rr < rows_here; rr += kForestThreads / 64) {
-        const float* src = A.x + (row0 + rr) * A.ldx;
-        for (int p = 0; p * 1024 < row_bytes; ++p) {
-          typedef __attribute__((address_space(3))) float lds_float;
-          const unsigned dst = __builtin_amdgcn_readfirstlane(
-              static_cast<unsigned>(reinterpret_cast<uintptr_t>((lds_float*)(xs + rr * xstride + p * 256))));
-          const unsigned voff = static_cast<unsigned>(p * 1024 + lane * 16);
-          if (static_cast<int>(voff) < row_bytes) {
-            unsigned keep;
-            asm volatile(
-                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                "global_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %0"
-                : "=&s"(keep)
-                : "v"(voff), "s"(dst), "s"(src)
-                : "memory");
-          }
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if (vec4) {
-      // 16-B loads, kStageBatch per thread issued before any LDS write (the
-      // block's whole tile in flight: this kernel is an HBM stream)
-      constexpr int kStageBatch = 8;
-      const int q = A.d >> 2, total = rows_here * q;
-      for (int e0 = 0; e0 < total; e0 += kForestThreads * kStageBatch) {
-        typedef float v4f __attribute__((ext_vector_type(4)));
-        v4f v[kStageBatch];
-#pragma unroll
-        for (int j = 0; j < kStageBatch; ++j) {
-          const int e = e0 + j * kForestThreads + tid;
-          if (e < total) {
-            const int r = e / q, c = e - r * q;
-            v[j] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(A.x + (row0 + r) * A.ldx) + c);
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < kStageBatch; ++j) {
-          const int e = e0 + j * kForestThreads + tid;
-          if (e < total) {
-            const int r = e / q, c = e - r * q;
-            float* dst = xs + r * xstride + 4 * c;
-            if (pad4) {
-              *reinterpret_cast<v4f*>(dst) = v[j];
-            } else {
-              dst[0] = v[j].x;
-              dst[1] = v[j].y;
-              dst[2] = v[j].z;
-              dst[3] = v[j].w;
-            }
-          }
-        }
-      }
-    } else {
-      for (int e = tid; e < rows_here * A.d; e += kForestThreads) {
-        const int r = e / A.d, c = e - r * A.d;
-        xs[r * xstride + c] = A.x[(row0 + r) * A.ldx + c];
-      }
-    }
-  }
-  __syncthreads();
 
   const float* xrow = X_LDS ? xs + r * xstride : A.x + (live ? row : 0) * A.ldx;
 
@@ -258,7 +166,7 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
       klo = s_min[0][w] < klo ? s_min[0][w] : klo;
       khi = s_min[1][w] < khi ? s_min[1][w] : khi;
     }
-    const int64_t g = blockIdx.x / A.hooks.group_blocks;
+    const int64_t g = tile / A.hooks.group_blocks;
     unsigned long long* lo_g = reinterpret_cast<unsigned long long*>(A.hooks.gmin) + g;
     unsigned long long* hi_g = lo_g + A.hooks.n_groups;
     if (A.hooks.group_blocks == 1) {
@@ -268,6 +176,131 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
       if (klo != DAL_KEY_NONE) atomicMax(lo_g, ~klo);
       if (khi != DAL_KEY_NONE) atomicMax(hi_g, ~khi);
     }
+  }
+}
+
+// One block per tile (grid = tiles), or PERSIST (LDS-DMA staging only; grid
+// = the blocks resident at once, walking tiles blockIdx.x, + gridDim.x, ...):
+// the forest is copied into LDS once per block instead of once per tile
+// (T = 100: 13.6 KB per 32-row tile).  PERSIST is its own instantiation: the
+// vec4 staging path's registers would cost it occupancy (147 VGPRs, 3 waves
+// per SIMD, against 65 / 7 without the loop).  Each tile: the leaders'
+// epilogue inputs and the rows are loaded together, then scored (score_tile).
+template <bool X_LDS, bool F_LDS, bool PERSIST>
+__global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs A, int R, int tpr,
+                                                                      int x_floats, bool vec4, bool pad4,
+                                                                      bool pre, bool dma, int64_t n_tiles) {
+  static_assert(!PERSIST || X_LDS, "the persistent form stages rows by LDS-DMA");
+  if (PERSIST) {
+    dma = true;
+    vec4 = false;
+    pad4 = true;
+  }
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* xs = reinterpret_cast<float*>(smem);
+  if (A.hooks.status_reset && blockIdx.x == 0 && threadIdx.x == 0) *A.hooks.status_reset = 0;
+  const int n_inner = (1 << A.depth) - 1;
+  const int n_leaf = 1 << A.depth;
+  const int2* inner = A.inner;
+  const uint8_t* leaf = A.leaf;
+  const int tid = threadIdx.x;
+  if (F_LDS) {
+    int2* fs = reinterpret_cast<int2*>(smem + static_cast<size_t>(x_floats) * 4);
+    uint8_t* ls = reinterpret_cast<uint8_t*>(fs + A.n_trees * n_inner);
+    for (int e = tid; e < A.n_trees * n_inner; e += kForestThreads) fs[e] = A.inner[e];
+    for (int e = tid; e < A.n_trees * n_leaf; e += kForestThreads) ls[e] = A.leaf[e];
+    inner = fs;
+    leaf = ls;
+  }
+  // row stride in LDS: d + 1 words for scalar staging; with 16-B staging
+  // d + 4 (rows stay 16-B aligned, one ds_write_b128 per load, consecutive
+  // lanes on consecutive banks; rows of a wave start 4 banks apart)
+  const int xstride = A.d + (pad4 ? 4 : 1);
+  const int r = tid / tpr, sub = tid - r * tpr;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {  // block-uniform
+    const int64_t row0 = tile * R;
+    const int64_t row = row0 + r;
+    const bool live = r < R && row < A.n;
+    // the row leader's epilogue inputs are loaded with the tile (one HBM
+    // latency per tile instead of two)
+    uint8_t fl_pre = DAL_ROW_CANDIDATE;
+    long long dens_pre = 0;
+    if (pre && live && sub == 0) {
+      if (A.flags) fl_pre = row_flag(A, row);
+      if (A.dkind) dens_pre = static_cast<const long long*>(A.density)[row];
+    }
+    if (X_LDS) {
+      const int rows_here = static_cast<int>(min(static_cast<int64_t>(R), A.n - row0));
+      if (dma) {
+        // LDS-DMA staging (d % 4 == 0, 16-B-aligned padded rows): one
+        // global_load_lds_dwordx4 per 1 KiB of a row (the last piece with only
+        // the lanes it needs), lane l's 16 B landing at M0 + 16 l; no VGPRs and
+        // no LDS write instructions (2M x 256: 535 -> 433 us)
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+        const int row_bytes = A.d * 4;
+        for (int rr = wave; rr < rows_here; rr += kForestThreads / 64) {
+          const float* src = A.x + (row0 + rr) * A.ldx;
+          for (int p = 0; p * 1024 < row_bytes; ++p) {
+            typedef __attribute__((address_space(3))) float lds_float;
+            const unsigned dst = __builtin_amdgcn_readfirstlane(
+                static_cast<unsigned>(reinterpret_cast<uintptr_t>((lds_float*)(xs + rr * xstride + p * 256))));
+            const unsigned voff = static_cast<unsigned>(p * 1024 + lane * 16);
+            if (static_cast<int>(voff) < row_bytes) {
+              unsigned keep;
+              asm volatile(
+                  "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                  "global_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %0"
+                  : "=&s"(keep)
+                  : "v"(voff), "s"(dst), "s"(src)
+                  : "memory");
+            }
+          }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if (vec4) {
+        // 16-B loads, kStageBatch per thread issued before any LDS write (the
+        // block's whole tile in flight: this kernel is an HBM stream)
+        constexpr int kStageBatch = 8;
+        const int q = A.d >> 2, total = rows_here * q;
+        for (int e0 = 0; e0 < total; e0 += kForestThreads * kStageBatch) {
+          typedef float v4f __attribute__((ext_vector_type(4)));
+          v4f v[kStageBatch];
+  #pragma unroll
+          for (int j = 0; j < kStageBatch; ++j) {
+            const int e = e0 + j * kForestThreads + tid;
+            if (e < total) {
+              const int r = e / q, c = e - r * q;
+              v[j] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(A.x + (row0 + r) * A.ldx) + c);
+            }
+          }
+  #pragma unroll
+          for (int j = 0; j < kStageBatch; ++j) {
+            const int e = e0 + j * kForestThreads + tid;
+            if (e < total) {
+              const int r = e / q, c = e - r * q;
+              float* dst = xs + r * xstride + 4 * c;
+              if (pad4) {
+                *reinterpret_cast<v4f*>(dst) = v[j];
+              } else {
+                dst[0] = v[j].x;
+                dst[1] = v[j].y;
+                dst[2] = v[j].z;
+                dst[3] = v[j].w;
+              }
+            }
+          }
+        }
+      } else {
+        for (int e = tid; e < rows_here * A.d; e += kForestThreads) {
+          const int r = e / A.d, c = e - r * A.d;
+          xs[r * xstride + c] = A.x[(row0 + r) * A.ldx + c];
+        }
+      }
+    }
+    __syncthreads();
+    score_tile<X_LDS>(A, xs, xstride, tile, R, tpr, inner, leaf, pre, fl_pre, dens_pre);
+    if (!PERSIST) break;
+    __syncthreads();  // every wave done with the tile before the next one is staged
   }
 }
 
@@ -349,20 +382,39 @@ int forest_score_launch(const float* x, int64_t n, int64_t d, int64_t ldx, const
   const int xf = static_cast<int>(round_up(x_floats, 4));  // forest region 16-B aligned
   size_t smem = static_cast<size_t>(xf) * 4 + (f_lds ? static_cast<size_t>(f_bytes) : 0);
   if (smem == 0) smem = 16;
-  const dim3 grid(static_cast<unsigned>(blocks));
-#define DAL_FOREST_LAUNCH(XL, FL)                                                                   \
-  do {                                                                                              \
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(forest_score_kernel<XL, FL>),             \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(smem)) !=  \
-        hipSuccess)                                                                                 \
-      return DAL_ERR_HIP;                                                                           \
-    hipLaunchKernelGGL((forest_score_kernel<XL, FL>), grid, dim3(kForestThreads), smem, st, A, R,  \
-                       tpr, xf, vec4, pad4, pre, T.dma);                                            \
+  // LDS-DMA tiles: a persistent grid of exactly the blocks resident at once
+  // (registers, LDS, waves: the occupancy query -- a grid past it would start
+  // its extra blocks only when others END) (2M x 256: 430 -> 404 us at
+  // T = 10, 677 -> 486 us at T = 100: the forest is copied once per block,
+  // not once per 32-row tile)
+  int64_t persist_grid = 0;
+  if (T.dma) {
+    int dev = 0, cus = 0, per_cu = 0;
+    const void* fn = f_lds ? reinterpret_cast<const void*>(forest_score_kernel<true, true, true>)
+                           : reinterpret_cast<const void*>(forest_score_kernel<true, false, true>);
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1 ||
+        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(smem)) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kForestThreads, smem) != hipSuccess)
+      return DAL_ERR_HIP;
+    if (per_cu < 1) per_cu = 1;
+    persist_grid = blocks < static_cast<int64_t>(cus) * per_cu ? blocks : static_cast<int64_t>(cus) * per_cu;
+  }
+#define DAL_FOREST_LAUNCH(XL, FL, PS, G)                                                                  \
+  do {                                                                                                    \
+    if (!(PS) && hipFuncSetAttribute(reinterpret_cast<const void*>(forest_score_kernel<XL, FL, PS>),      \
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,                          \
+                                     static_cast<int>(smem)) != hipSuccess)                               \
+      return DAL_ERR_HIP;                                                                                 \
+    hipLaunchKernelGGL((forest_score_kernel<XL, FL, PS>), dim3(static_cast<unsigned>(G)),                 \
+                       dim3(kForestThreads), smem, st, A, R, tpr, xf, vec4, pad4, pre, T.dma, blocks);    \
   } while (0)
-  if (T.x_lds && f_lds) DAL_FOREST_LAUNCH(true, true);
-  else if (T.x_lds) DAL_FOREST_LAUNCH(true, false);
-  else if (f_lds) DAL_FOREST_LAUNCH(false, true);
-  else DAL_FOREST_LAUNCH(false, false);
+  if (T.dma && f_lds) DAL_FOREST_LAUNCH(true, true, true, persist_grid);
+  else if (T.dma) DAL_FOREST_LAUNCH(true, false, true, persist_grid);
+  else if (T.x_lds && f_lds) DAL_FOREST_LAUNCH(true, true, false, blocks);
+  else if (T.x_lds) DAL_FOREST_LAUNCH(true, false, false, blocks);
+  else if (f_lds) DAL_FOREST_LAUNCH(false, true, false, blocks);
+  else DAL_FOREST_LAUNCH(false, false, false, blocks);
 #undef DAL_FOREST_LAUNCH
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;

@@ -480,6 +480,11 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {  // l wave-uni
   return __longlong_as_double(static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
 }
 
+// d^beta for beta != 1 (the reference declares beta, density_weighting.py:33;
+// 1 in every call): out of line, so its constants do not crowd the callers'
+// scalar registers.
+__device__ __attribute__((noinline)) double density_pow_canon(double d, double beta) { return pow(d, beta); }
+
 __device__ __forceinline__ bool dw_canonical_score_wave(const DwRerank& R, int64_t i, double& s,
                                                         double lut_lane = 0.0, int n_lut = 0) {
   constexpr int kC = 4;  // 64-feature chunks per round: every chunk's loads and divisions in flight together
@@ -515,7 +520,7 @@ __device__ __forceinline__ bool dw_canonical_score_wave(const DwRerank& R, int64
   if (fl & DAL_ROW_EXCLUDED) acc = __builtin_nan("");
   // n_lut > 0: lane l holds lut[l] (T < 64), no dependent load on the vote
   const double e = v < n_lut ? readlane_f64(lut_lane, v) : R.lut[v];
-  s = e * (R.beta == 1.0 ? acc : pow(acc, R.beta));
+  s = e * (R.beta == 1.0 ? acc : density_pow_canon(acc, R.beta));
   return true;
 }
 
@@ -551,7 +556,7 @@ __device__ __forceinline__ bool dw_canonical_score_lane(const DwRerank& R, int64
   }
   if (fl & DAL_ROW_EXCLUDED) acc = __builtin_nan("");
   const double e = n_lut ? e_in : R.lut[R.votes[i]];
-  s = e * (R.beta == 1.0 ? acc : pow(acc, R.beta));
+  s = e * (R.beta == 1.0 ? acc : density_pow_canon(acc, R.beta));
   return true;
 }
 

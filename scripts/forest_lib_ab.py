@@ -3,7 +3,7 @@ between two builds of libdal.so: ab/libdal_base.so (the committed kernel) and
 the current in-tree library.  Per shape: both libraries' outputs (votes,
 scores, both keys) must be bit-identical; then 20 back-to-back launches
 between two HIP events, interleaved A/B/A/B, median of the rounds.
-usage: python scripts/forest_lib_ab.py [NxDxT[:normal] ...]"""
+usage: python scripts/forest_lib_ab.py [NxDxT[:normal] ...]   (AB_BASE / AB_NEW: other library paths)"""
 import ctypes
 import os
 import statistics
@@ -36,7 +36,8 @@ def main():
     shapes = [a for a in sys.argv[1:]] or ["100000x64x10", "284807x30x100:normal", "2000000x256x10",
                                            "2000000x32x100", "2000000x256x100"]
     dev = torch.device("cuda:0")
-    libs = {"base": bind(os.path.join(REPO, "ab", "libdal_base.so")), "new": bind(_lib.LIB_PATH)}
+    base = os.environ.get("AB_BASE", os.path.join(REPO, "ab", "libdal_base.so"))
+    libs = {"base": bind(base), "new": bind(os.environ.get("AB_NEW", _lib.LIB_PATH))}
     for spec in shapes:
         dims, _, dist = spec.partition(":")
         n, d, T = (int(v) for v in dims.split("x"))
