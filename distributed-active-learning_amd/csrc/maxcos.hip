@@ -34,6 +34,9 @@ namespace dal {
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 #define AS3 __attribute__((address_space(3)))
 
@@ -72,7 +75,25 @@ struct McCfg {
   static_assert(NCT % 2 == 0, "column tiles go in pairs");
 };
 
-template <int DK, bool ARG, int OCC>
+// UNIT (dal_max_cosine_unit, no arg-max): the labeled operand is the fp16
+// table 2^15 x_l / ||x_l|| (dal_unit_rows_f16) and every pool row is scaled by
+// the power of two 2^s that puts its largest |x_if| in [2^15, 2^16) and
+// converted to fp16 in registers (exact for the bf16 significand; only
+// entries below 2^-29 of the row maximum lose bits).  The per-column scaling
+// leaves the epilogue -- one v_max3 per two products -- which is what held
+// this kernel's clock down; the operand rounding widens the bound to
+// dal_maxcos_unit_error_bound (about 2^-11 on the cosine).
+template <bool UNIT>
+__device__ __forceinline__ f32x4 mc_mfma(const uint4& a, const uint4& b, const f32x4& c) {
+  if constexpr (UNIT)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
+                                                  0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+}
+
+template <int DK, bool ARG, int OCC, bool UNIT = false>
 __global__ __launch_bounds__(256, OCC) void maxcos_kernel(
     const uint16_t* __restrict__ pool, int64_t n, const uint16_t* __restrict__ lab, int64_t m_pad,
     const float* __restrict__ inv_lab, const float* __restrict__ inv_pool, float* __restrict__ out,
@@ -86,7 +107,8 @@ __global__ __launch_bounds__(256, OCC) void maxcos_kernel(
   const int64_t row0 = static_cast<int64_t>(blockIdx.x) * 256 + wave * 64;
   const int n_stages = static_cast<int>(m_pad / C::SR);
 
-  for (int i = tid; i < m_pad; i += 256) invl[i] = inv_lab[i];
+  if constexpr (!UNIT)
+    for (int i = tid; i < m_pad; i += 256) invl[i] = inv_lab[i];
 
   unsigned voff[C::PIECES];
 #pragma unroll
@@ -114,14 +136,46 @@ __global__ __launch_bounds__(256, OCC) void maxcos_kernel(
   };
   issue(0, 0);
 
-  bf16x8 a[C::RT][C::NKS];
+  uint4 a[C::RT][C::NKS];
 #pragma unroll
   for (int rt = 0; rt < C::RT; ++rt) {
     int64_t row = row0 + rt * 16 + li;
     row = row < n ? row : n - 1;
 #pragma unroll
-    for (int s = 0; s < C::NKS; ++s)
-      a[rt][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pool + row * DK + 32 * s + 8 * lq));
+    for (int s = 0; s < C::NKS; ++s) a[rt][s] = *reinterpret_cast<const uint4*>(pool + row * DK + 32 * s + 8 * lq);
+  }
+  if constexpr (UNIT) {
+    // row r of tile rt lives on lanes li = r of the four lane groups: the
+    // largest |bits| of the row (bf16 magnitudes order as their bit patterns)
+#pragma unroll
+    for (int rt = 0; rt < C::RT; ++rt) {
+      u16x2 mm = {0, 0};
+#pragma unroll
+      for (int s = 0; s < C::NKS; ++s) {
+        const unsigned w[4] = {a[rt][s].x, a[rt][s].y, a[rt][s].z, a[rt][s].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          mm = __builtin_elementwise_max(mm, __builtin_bit_cast(u16x2, w[e] & 0x7FFF7FFFu));
+      }
+      unsigned mr = mm.x > mm.y ? mm.x : mm.y;
+      mr = max(mr, static_cast<unsigned>(__shfl_xor(static_cast<int>(mr), 16)));
+      mr = max(mr, static_cast<unsigned>(__shfl_xor(static_cast<int>(mr), 32)));
+      // 2^s puts the row maximum in [2^15, 2^16); exponent-0 rows (zero or
+      // bf16-subnormal) stay unscaled and end as zero-norm rows
+      const int ex = static_cast<int>(mr >> 7);
+      const int sc = ex ? 142 - ex : 0;
+#pragma unroll
+      for (int s = 0; s < C::NKS; ++s) {
+        unsigned w[4] = {a[rt][s].x, a[rt][s].y, a[rt][s].z, a[rt][s].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float lo = __builtin_ldexpf(__uint_as_float(w[e] << 16), sc);
+          const float hi = __builtin_ldexpf(__uint_as_float(w[e] & 0xFFFF0000u), sc);
+          w[e] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(lo, hi));
+        }
+        a[rt][s] = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+    }
   }
 
   // 1/||x_i|| from the resident fragments: ||x_i||^2 is the diagonal of the
@@ -137,7 +191,7 @@ __global__ __launch_bounds__(256, OCC) void maxcos_kernel(
     for (int rt = 0; rt < C::RT; ++rt) {
       f32x4 g = {};
 #pragma unroll
-      for (int s = 0; s < C::NKS; ++s) g = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rt][s], a[rt][s], g, 0, 0, 0);
+      for (int s = 0; s < C::NKS; ++s) g = mc_mfma<UNIT>(a[rt][s], a[rt][s], g);
       const int j = li & 3;
       const float mine = j == 0 ? g[0] : j == 1 ? g[1] : j == 2 ? g[2] : g[3];
       const float n2 = __shfl(mine, src);
@@ -185,14 +239,20 @@ __global__ __launch_bounds__(256, OCC) void maxcos_kernel(
     for (int h = 0; h < 2; ++h) {
 #pragma unroll
       for (int s = 0; s < C::NKS; ++s) {
-        const bf16x8 b = __builtin_bit_cast(bf16x8, B[(ct + h) * 16 * C::SLOTS + boff[s]]);
+        const uint4 b = __builtin_bit_cast(uint4, B[(ct + h) * 16 * C::SLOTS + boff[s]]);
 #pragma unroll
-        for (int rt = 0; rt < C::RT; ++rt)
-          c[h][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rt][s], b, s == 0 ? zero : c[h][rt], 0, 0, 0);
+        for (int rt = 0; rt < C::RT; ++rt) c[h][rt] = mc_mfma<UNIT>(a[rt][s], b, s == 0 ? zero : c[h][rt]);
       }
     }
   };
   auto epi_pair = [&](int col, const f32x4 (&c)[2][C::RT]) {
+    if constexpr (UNIT) {
+#pragma unroll
+      for (int rt = 0; rt < C::RT; ++rt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mx[rt][i] = fmaxf(fmaxf(mx[rt][i], c[0][rt][i]), c[1][rt][i]);
+      return;
+    }
     const float ila = invl[col + li], ilb = invl[col + 16 + li];
     if constexpr (ARG) {
 #pragma unroll
@@ -315,7 +375,8 @@ __global__ __launch_bounds__(256, OCC) void maxcos_kernel(
   if (row < n) {
     const float iv = inv_pool ? inv_pool[row] : iv_reg;
     if (!(iv < __builtin_inff())) atomicOr(status, DAL_FLAG_ZERO_NORM);
-    out[row] = v[0] * iv;
+    // UNIT: the labeled operand carries 2^15 (an exact power-of-two rescale)
+    out[row] = UNIT ? (v[0] * iv) * 0x1p-15f : v[0] * iv;
   }
 }
 
@@ -348,6 +409,21 @@ __global__ __launch_bounds__(64) void canon_unit_rows_bf16_kernel(const uint16_t
     const double v = static_cast<double>(bf16_to_f32(x[i * ld + f])) / nr;
     u[feature_major ? f * n + i : i * d + f] = v;
   }
+}
+
+// The UNIT kernel's labeled operand: fp16(2^15 x_l / ||x_l||) with the
+// canonical fp64 norm (sequential, as the re-rank's), one rounding fp64 ->
+// fp16 (round to nearest even); padding rows [m, m_pad) repeat row 0 (a
+// duplicate never changes a maximum).  Zero-norm rows flag status.
+__global__ __launch_bounds__(64) void unit_rows_f16_kernel(const uint16_t* __restrict__ x, int64_t m, int d,
+                                                            int64_t ld, _Float16* __restrict__ out,
+                                                            int32_t* __restrict__ status) {
+  const int64_t i = blockIdx.x;
+  const int64_t src = i < m ? i : 0;
+  const double nr = __builtin_sqrt(row_sq_norm_bf16(x + src * ld, d));
+  if (i < m && !(nr > 0.0) && threadIdx.x == 0) atomicOr(status, DAL_FLAG_ZERO_NORM);
+  for (int f = threadIdx.x; f < d; f += 64)
+    out[i * d + f] = static_cast<_Float16>(static_cast<double>(bf16_to_f32(x[src * ld + f])) / nr * 32768.0);
 }
 
 // Canonical fp64 arg-max of the rows dal_max_cosine marked ambiguous
@@ -417,19 +493,26 @@ __global__ __launch_bounds__(256) void maxcos_argmax_resolve_kernel(const uint16
   }
 }
 
-template <int DK, bool ARG, int OCC>
+template <int DK, bool ARG, int OCC, bool UNIT = false>
 int launch_maxcos_t(const uint16_t* pool, int64_t n, const uint16_t* lab, int64_t m_pad, const float* inv_lab,
                       const float* inv_pool, float* out, int32_t* out_arg, double gap, int32_t* status,
                       hipStream_t st) {
   const int64_t blocks = ceil_div(n, kMcRows);
-  const size_t shm = 2 * McCfg<DK, OCC == 3 ? 16384 : 32768>::STAGE + static_cast<size_t>(m_pad) * 4;
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(maxcos_kernel<DK, ARG, OCC>),
+  const size_t shm = 2 * McCfg<DK, OCC == 3 ? 16384 : 32768>::STAGE + (UNIT ? 0 : static_cast<size_t>(m_pad) * 4);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(maxcos_kernel<DK, ARG, OCC, UNIT>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(shm)) != hipSuccess)
     return DAL_ERR_HIP;
-  hipLaunchKernelGGL((maxcos_kernel<DK, ARG, OCC>), dim3(static_cast<unsigned>(blocks)), dim3(256), shm, st, pool, n,
+  hipLaunchKernelGGL((maxcos_kernel<DK, ARG, OCC, UNIT>), dim3(static_cast<unsigned>(blocks)), dim3(256), shm, st, pool, n,
                      lab, m_pad, inv_lab, inv_pool, out, out_arg, gap, status);
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
+}
+
+template <int DK>
+int launch_maxcos_unit(const uint16_t* pool, int64_t n, const uint16_t* lab, int64_t m_pad, float* out,
+                       int32_t* status, hipStream_t st) {
+  constexpr int OCC = DK <= 128 ? 3 : 2;
+  return launch_maxcos_t<DK, false, OCC, true>(pool, n, lab, m_pad, nullptr, nullptr, out, nullptr, 0.0, status, st);
 }
 
 template <int DK>
@@ -481,6 +564,48 @@ extern "C" double dal_maxcos_error_bound(int64_t d) {
   const double u = 1.0 / 16777216.0;
   const double k = 3.0 * static_cast<double>(d) + 6.0;
   return k * u / (1.0 - k * u) * 1.01 + 1e-12;
+}
+
+extern "C" int dal_unit_rows_f16(const uint16_t* x, int64_t m, int64_t m_pad, int64_t d, int64_t ld,
+                                 uint16_t* out, int32_t* dev_status, dal_stream_t stream) {
+  if (!x || !out || !dev_status) return DAL_ERR_ARG;
+  if (m < 1 || m_pad < m || d < 1 || ld < d) return DAL_ERR_SHAPE;
+  hipLaunchKernelGGL(unit_rows_f16_kernel, dim3(static_cast<unsigned>(m_pad)), dim3(64), 0, as_stream(stream), x, m,
+                     static_cast<int>(d), ld, reinterpret_cast<_Float16*>(out), dev_status);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}
+
+// dal_max_cosine_unit, relative to the cosine scale (Cauchy-Schwarz on the
+// scaled rows x~ = 2^s x, max |x~_f| in [2^15, 2^16), and y' = the fp16 table
+// 2^15 y / ||y||):
+//  * y' rounding: one fp64 -> fp16 rounding of an fp64 quotient, relative
+//    u16 + 2u per entry (u16 = 2^-11), or at most 2^-14 absolute where y'_f is
+//    fp16-subnormal or flushed: (u16 + 2u) + 2^-29 sqrt(d);
+//  * x~ conversion: exact for entries in the fp16 normal range (a bf16
+//    significand fits), at most 2^-14 absolute below it, i.e. 2^-29 of
+//    ||x~|| >= 2^15 per entry; moving both the dot and the norm,
+//    |cos(a, y) - cos(b, y)| <= 2 ||a - b|| / ||b||: 2^-28 sqrt(d);
+//  * fp32 arithmetic of exact fp16 products (the dal_maxcos_error_bound
+//    terms: d-term dot, in-kernel norm, two scalings): (3d + 6) u, times
+//    ||y'|| / 2^15 <= 1 + 2^-10.
+extern "C" double dal_maxcos_unit_error_bound(int64_t d) {
+  const double u = 1.0 / 16777216.0, u16 = 1.0 / 2048.0;
+  const double rd = __builtin_sqrt(static_cast<double>(d));
+  const double b = (u16 + 2.0 * u) + 3.0 * 0x1p-29 * rd + (3.0 * static_cast<double>(d) + 6.0) * u * (1.0 + 0x1p-10);
+  return b * 1.01 + 1e-12;
+}
+
+extern "C" int dal_max_cosine_unit(const uint16_t* pool, int64_t n, int64_t d, const uint16_t* lab_unit,
+                                   int64_t m_pad, float* out_max, int32_t* dev_status, dal_stream_t stream) {
+  if (!pool || !lab_unit || !out_max || !dev_status) return DAL_ERR_ARG;
+  if (n < 1 || (d != 64 && d != 128 && d != 256)) return DAL_ERR_SHAPE;
+  if (m_pad < 1 || m_pad % dal_maxcos_label_rows_granule(d) || m_pad > kMaxLab) return DAL_ERR_SHAPE;
+  if ((reinterpret_cast<uintptr_t>(pool) | reinterpret_cast<uintptr_t>(lab_unit)) & 15) return DAL_ERR_SHAPE;
+  hipStream_t st = as_stream(stream);
+  if (d == 64) return launch_maxcos_unit<64>(pool, n, lab_unit, m_pad, out_max, dev_status, st);
+  if (d == 128) return launch_maxcos_unit<128>(pool, n, lab_unit, m_pad, out_max, dev_status, st);
+  return launch_maxcos_unit<256>(pool, n, lab_unit, m_pad, out_max, dev_status, st);
 }
 
 extern "C" int dal_max_cosine(const uint16_t* pool, int64_t n, int64_t d, const uint16_t* lab, int64_t m_pad,

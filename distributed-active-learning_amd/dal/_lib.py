@@ -101,6 +101,9 @@ SIGNATURES = {
     "dal_canon_unit_rows_bf16": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p]),
     "dal_max_cosine": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p, c_void_p]),
+    "dal_unit_rows_f16": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
+    "dal_maxcos_unit_error_bound": (c_double, [c_int64]),
+    "dal_max_cosine_unit": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "dal_text_shape": (c_int, [c_void_p, c_size_t, c_int64, c_void_p, c_void_p]),
     "dal_parse_labeled_text": (c_int, [c_void_p, c_size_t, c_int64, c_int64, c_int, c_void_p, c_void_p, c_int]),
     "dal_maxcos_argmax_resolve": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64, c_void_p,

@@ -42,9 +42,11 @@ def _bf16_pool(pool, device):
 
 
 class LabeledSet:
-    """The labeled rows as the kernel's B operand: bf16 [m_pad, d] (padding
-    rows carry 1/||x|| = NaN, ignored by the max), fp32 1/||x||, and the
-    canonical fp64 unit rows (feature-major) for the exact re-rank."""
+    """The labeled rows as the kernels' B operands: bf16 [m_pad, d] (padding
+    rows carry 1/||x|| = NaN, ignored by the max) with fp32 1/||x|| for the
+    arg-max kernel, the folded fp16 table 2^15 x/||x|| for the max-only
+    kernel (``unit16``, built on first use), and the canonical fp64 unit rows
+    (feature-major) for the exact re-rank."""
 
     def __init__(self, rows_bf16, device):
         import torch
@@ -68,6 +70,24 @@ class LabeledSet:
         self.unit64_t = torch.empty((d, m), dtype=torch.float64, device=device)
         _lib.call("dal_canon_unit_rows_bf16", _ptr(self.rows), m, d, d, 1, _ptr(self.unit64_t),
                   _stream(device))
+        self.device = device
+        self._unit16 = None
+
+    @property
+    def unit16(self):
+        """fp16 [m_pad, d] = 2^15 x_l / ||x_l|| (canonical fp64 norm, one
+        rounding; padding rows repeat row 0) -- dal_max_cosine_unit's B."""
+        if self._unit16 is None:
+            import torch
+
+            from . import _lib
+            from .engine import _ptr, _stream
+
+            u = torch.empty((self.m_pad, self.d), dtype=torch.float16, device=self.device)
+            _lib.call("dal_unit_rows_f16", _ptr(self.rows), self.m, self.m_pad, self.d, self.d, _ptr(u),
+                      _ptr(self.status), _stream(self.device))
+            self._unit16 = u
+        return self._unit16
 
 
 def max_cosine(pool, labeled_idx, device=None):
@@ -103,7 +123,8 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
                      labeled_rows=None):
     """Select the k candidate rows least similar to the labeled set (smallest
     max-cosine, ties -> lower index), exact against the canonical fp64
-    max-cosine.  Returns Selection(scores = fp32 max-cos of the candidates,
+    max-cosine.  Returns Selection(scores = fp32 max-cos of the candidates
+    (within dal_maxcos_unit_error_bound of the canonical values),
     indices [k], selected_scores = canonical fp64 max-cos).
 
     For a row shard (multi-GPU) pass ``row_base`` (global index of row 0),
@@ -126,8 +147,10 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
     lab = LabeledSet(lab_rows, dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     mx = torch.empty(n, dtype=torch.float32, device=dev)
-    _lib.call("dal_max_cosine", _ptr(x), n, d, _ptr(lab.rows), lab.m_pad, _ptr(lab.inv), 0,
-              _ptr(mx), 0, _ptr(status), _stream(dev))
+    # values only (no arg-max): the folded-operand kernel; its wider bound
+    # only widens the interval keys -- the fp64 re-rank keeps the selection exact
+    _lib.call("dal_max_cosine_unit", _ptr(x), n, d, _ptr(lab.unit16), lab.m_pad, _ptr(mx), _ptr(status),
+              _stream(dev))
     in_range = None  # device count of the candidates inside this shard (read with the status)
     if candidates is None:
         flags = torch.full((n,), DAL_ROW_CANDIDATE, dtype=torch.uint8, device=dev)
@@ -150,7 +173,7 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
     kk = min(int(k), n_cand)
     lo = torch.empty(n, dtype=torch.int64, device=dev)
     hi = torch.empty(n, dtype=torch.int64, device=dev)
-    _lib.call("dal_interval_keys_f32", _ptr(mx), n, float(lib.dal_maxcos_error_bound(d)), _ptr(flags),
+    _lib.call("dal_interval_keys_f32", _ptr(mx), n, float(lib.dal_maxcos_unit_error_bound(d)), _ptr(flags),
               DAL_ASCENDING, _ptr(lo), _ptr(hi), _stream(dev))
     cap = candidate_cap(n, kk)
     passes = LEVEL1_PASSES if cap <= _lib.DAL_SORT_CAP_PAYLOAD else 0

@@ -363,6 +363,20 @@ int dal_canon_unit_rows_bf16(const uint16_t* x, int64_t n, int64_t d, int64_t ld
 int dal_max_cosine(const uint16_t* pool, int64_t n, int64_t d, const uint16_t* lab, int64_t m_pad,
                    const float* inv_lab, const float* inv_pool, float* out_max, int32_t* out_arg,
                    int32_t* dev_status, dal_stream_t stream);
+/* Max-cosine WITHOUT the arg-max on a folded labeled operand (ABI v7; the
+ * diversity selection's values): lab_unit = dal_unit_rows_f16's fp16 table
+ * 2^15 x_l / ||x_l|| [m_pad][d] (no per-column scaling left in the kernel:
+ * the epilogue is a bare running max).  Each pool row is rescaled by a power
+ * of two and converted to fp16 in registers; v_mfma_f32_16x16x32_f16.
+ * |m_gpu - m_canonical| <= dal_maxcos_unit_error_bound(d) (~2^-11: the fp16
+ * rounding of the unit rows; the selection stays exact through the fp64
+ * re-rank).  Rows whose largest |x_if| is zero or a bf16 subnormal flag
+ * DAL_FLAG_ZERO_NORM, as in dal_max_cosine. */
+int dal_unit_rows_f16(const uint16_t* x, int64_t m, int64_t m_pad, int64_t d, int64_t ld, uint16_t* out,
+                      int32_t* dev_status, dal_stream_t stream);
+double dal_maxcos_unit_error_bound(int64_t d);
+int dal_max_cosine_unit(const uint16_t* pool, int64_t n, int64_t d, const uint16_t* lab_unit, int64_t m_pad,
+                        float* out_max, int32_t* dev_status, dal_stream_t stream);
 /* Canonical fp64 arg-max (oracle max_cosine_canonical: sequential norm and
  * dot products, no FMA, first l on ties) of every row with out_arg < 0;
  * ulab = canonical fp64 unit rows of the m labeled rows, feature-major [d][m]

@@ -112,3 +112,64 @@ def test_diversity_select_fallbacks(cuda, case):
     assert np.array_equal(_np(sel.selected_scores), ref_sc)
     if case == "bucket_overflow":
         assert (ref_idx == np.arange(3000, 3100)).all()  # ties -> lower index
+
+
+def _unit_max(cuda, X, L):
+    import torch
+
+    from dal import _lib
+    from dal import similarity as sim
+
+    x, dev = sim._bf16_pool(X, cuda)
+    lab = sim.LabeledSet(x[torch.as_tensor(L, device=dev)], dev)
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    out = torch.empty(x.shape[0], dtype=torch.float32, device=dev)
+    _lib.call("dal_max_cosine_unit", x.data_ptr(), x.shape[0], x.shape[1], lab.unit16.data_ptr(), lab.m_pad,
+              out.data_ptr(), st.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    return _np(out).astype(np.float64), int(st.item()) | int(lab.status.item())
+
+
+@pytest.mark.parametrize("n,d,m,dist", [(3000, 128, 300, "uniform"), (2500, 64, 1024, "uniform"),
+                                        (1800, 256, 130, "normal"), (700, 128, 1, "normal")])
+def test_max_cosine_unit_within_bound(cuda, n, d, m, dist):
+    """The folded-operand kernel (fp16 unit labeled rows, power-of-two
+    rescaled pool rows): |m_gpu - m_canonical| <= dal_maxcos_unit_error_bound."""
+    from dal import _lib
+
+    X = O.bf16_round(O.synthetic_pool(n, d, seed=n + 3 * d, dist=dist))
+    L = np.arange(0, n, max(1, n // m))[:m]
+    got, st = _unit_max(cuda, X, L)
+    ref, _ = O.max_cosine_canonical(X, L)
+    bound = _lib.load().dal_maxcos_unit_error_bound(d)
+    assert st == 0
+    assert np.abs(got - ref).max() <= bound
+    assert np.abs(got - ref).max() > 0  # the fp16 operand is not the bf16 one
+
+
+@pytest.mark.parametrize("d", [64, 128, 256])
+def test_max_cosine_unit_dynamic_range(cuda, d):
+    """Rows spanning many binades (whole rows scaled by 2^-100 .. 2^100 and
+    entries down to 2^-40 of the row maximum, i.e. below the fp16 range after
+    the row rescale; labeled rows with entries below fp16's normal range):
+    the bound still holds (the rescale is exact, only tiny entries flush)."""
+    from dal import _lib
+
+    rng = np.random.default_rng(d)
+    n = 2048
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    X *= np.exp2(rng.integers(-40, 1, size=(n, d))).astype(np.float32)  # entry magnitudes over 40 binades
+    X *= np.exp2(rng.integers(-100, 101, size=(n, 1))).astype(np.float32)  # whole-row scales
+    X = O.bf16_round(X)
+    X[X.any(axis=1) == 0, 0] = 1.0
+    L = np.arange(0, n, 7)[:200]
+    got, st = _unit_max(cuda, X, L)
+    ref, _ = O.max_cosine_canonical(X, L)
+    assert st == 0
+    assert np.abs(got - ref).max() <= _lib.load().dal_maxcos_unit_error_bound(d)
+
+
+def test_max_cosine_unit_zero_row_flags(cuda):
+    X = O.bf16_round(O.synthetic_pool(600, 64, seed=3))
+    X[17] = 0.0
+    _, st = _unit_max(cuda, X, np.arange(0, 600, 3))
+    assert st & 1

@@ -36,7 +36,7 @@ def test_library_exports_every_header_symbol():
 
 def test_host_helpers():
     lib = _lib.load()
-    assert lib.dal_abi_version() == 6
+    assert lib.dal_abi_version() == 7
     assert lib.dal_pad_rows(1) == 512 and lib.dal_pad_rows(100000) == 100352
     assert [lib.dal_pad_features(d) for d in (1, 30, 33, 64, 65, 128, 129, 256, 500, 784)] == \
         [32, 32, 64, 64, 128, 128, 256, 256, 512, 1024]
