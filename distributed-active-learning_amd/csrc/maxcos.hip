@@ -229,11 +229,25 @@ __global__ __launch_bounds__(256, OCC) void maxcos_kernel(
 #pragma unroll
   for (int s = 0; s < C::NKS; ++s) boff[s] = li * C::SLOTS + ((4 * s + lq) ^ (li & C::SWZ));
 
-  // a pair of column tiles (ct, ct + 1): MFMAs into (c, e), then the scaled
-  // running max; a scheduling fence per pair keeps the compiler from hoisting
-  // a whole stage's B reads (registers decide the occupancy here)
-  constexpr int NP = C::NCT / 2;
+  // column tile ct: its B fragments were read during tile ct - 1's MFMAs
+  // (two register sets: the LDS latency never waits in front of a tile);
+  // accumulators alternate between (c, e) and the scaled running max takes a
+  // pair of tiles at once.  A scheduling fence per tile keeps the compiler
+  // from hoisting a whole stage's B reads (registers decide the occupancy).
   f32x4 acc[2][C::RT];
+  auto load_b = [&](const float4* B, int ct, uint4 (&bb)[C::NKS]) {
+#pragma unroll
+    for (int s = 0; s < C::NKS; ++s) bb[s] = __builtin_bit_cast(uint4, B[ct * 16 * C::SLOTS + boff[s]]);
+  };
+  auto mfma_ct = [&](const uint4 (&bb)[C::NKS], f32x4 (&c)[C::RT]) {
+#pragma unroll
+    for (int s = 0; s < C::NKS; ++s)
+#pragma unroll
+      for (int rt = 0; rt < C::RT; ++rt) c[rt] = mc_mfma<UNIT>(a[rt][s], bb[s], s == 0 ? zero : c[rt]);
+  };
+  // d = 256: two register sets of 8 k-steps' B do not fit beside the A
+  // fragments (spills); a pair of tiles reads its B as it goes
+  constexpr bool kPrefetch = DK <= 128;
   auto mfma_pair = [&](const float4* B, int ct, f32x4 (&c)[2][C::RT]) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -286,11 +300,23 @@ __global__ __launch_bounds__(256, OCC) void maxcos_kernel(
     __syncthreads();
     if (st + 1 < n_stages) issue(buf ^ 1, st + 1);
     const float4* B = lds + buf * C::F4;
+    if constexpr (kPrefetch) {
+      uint4 bb[2][C::NKS];
+      load_b(B, 0, bb[0]);
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_pair(B, 2 * p, acc);
-      epi_pair(st * C::SR + 2 * p * 16, acc);
+      for (int ct = 0; ct < C::NCT; ++ct) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (ct + 1 < C::NCT) load_b(B, ct + 1, bb[(ct + 1) & 1]);
+        mfma_ct(bb[ct & 1], acc[ct & 1]);
+        if (ct & 1) epi_pair(st * C::SR + (ct - 1) * 16, acc);
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < C::NCT / 2; ++p) {
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_pair(B, 2 * p, acc);
+        epi_pair(st * C::SR + 2 * p * 16, acc);
+      }
     }
     pin();
   };
