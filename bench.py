@@ -39,6 +39,10 @@ METRIC = "pool rows scored/sec (density-weighted uncertainty), 1–8 GPU; % MFMA
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.29 TB/s measured float4 copy)
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
+# K2 / K3 launch timing: a GPU spin of this many cycles is queued ahead of each
+# timed call, so its launches are submitted before the GPU reaches them and the
+# HIP events bracket the device span only (not the host's submission gaps)
+EVENT_LEAD_CYCLES = 400_000
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 MFMA (same cycles as bf16)
 
 CONFIGS = {
@@ -274,7 +278,7 @@ def forest_roofline(n_rows, d, trees, forest_ms, config, world):
            "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
            "traffic": _traffic(config, "forest_score_bytes_per_launch", world), "launch_ms": forest_ms,
            "algorithmic_bytes_per_launch": nbytes, "bytes_per_row": per_row,
-           "note": "timed with HIP events on the launch stream over the warm steps (density cached)"}
+           "note": "timed with HIP events on the launch stream over the warm steps (density cached), each call queued behind a GPU spin (device span, no host submission gaps)"}
     if trees > 32:
         out["counters"] = ("PMC per launch at config 3 (profiles/r02/forest_config3_pmc.csv): LDS array busy "
                            "SQ_LDS_IDX_ACTIVE, 42% of it bank-conflict cycles (lane-divergent feature gathers); "
@@ -305,7 +309,7 @@ def topk_roofline(n_rows, select_ms, config, world, level1_passes=0):
             "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
             "traffic": _traffic(config, "dw_select_bytes_per_launch", world), "launch_ms": select_ms,
             "algorithmic_bytes_per_launch": nbytes, "bytes_per_row": per_row,
-            "note": "one C-ABI call, HIP events on the launch stream, warm steps"}
+            "note": "one C-ABI call (all its launches), HIP events on the launch stream, warm steps, each call queued behind a GPU spin (device span, no host submission gaps)"}
 
 
 # ----------------------------------------------------------- workloads --
@@ -491,11 +495,13 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
         step()
         # per-kernel HIP-event timing of K2 / K3 (eager launches, events on the launch stream)
         state.forest_events, state.select_events = [], []
+        state.event_lead_cycles = EVENT_LEAD_CYCLES
         for _ in range(min(warm_steps, 20)):
             step(cold=False)
         torch.cuda.synchronize()
         fev, sev = state.forest_events, state.select_events
         state.forest_events = state.select_events = None
+        state.event_lead_cycles = 0
         if fev:
             forest_ms = sum(a.elapsed_time(b) for a, b in fev) / len(fev)
         if sev:

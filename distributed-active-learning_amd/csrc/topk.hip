@@ -506,8 +506,16 @@ __device__ __forceinline__ bool dw_canonical_score_wave(const DwRerank& R, int64
       const int rest = __builtin_amdgcn_readfirstlane(R.d - f0 - 64 * c);
       if (rest <= 0) break;
       if (rest >= 64) {
+        // v_readlane (no LDS round trip), 16 lanes' products into distinct
+        // scalar registers ahead of their adds: only the add chain is serial
 #pragma unroll
-        for (int q = 0; q < 64; ++q) acc = acc + readlane_f64(p[c], q);  // v_readlane: no LDS round trip
+        for (int q0 = 0; q0 < 64; q0 += 16) {
+          double t[16];
+#pragma unroll
+          for (int j = 0; j < 16; ++j) t[j] = readlane_f64(p[c], q0 + j);
+#pragma unroll
+          for (int j = 0; j < 16; ++j) acc = acc + t[j];
+        }
       } else {
         for (int q = 0; q < rest; ++q) acc = acc + readlane_f64(p[c], q);
       }

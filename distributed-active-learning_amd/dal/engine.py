@@ -162,6 +162,11 @@ class PoolState:
         self.residual_events = []  # (start, end) HIP events around each residual call (with gram_events)
         self.forest_events = None  # list -> (start, end) HIP events around each forest-score call
         self.select_events = None  # list -> (start, end) HIP events around each dal_dw_select call
+        # bench: a GPU spin (torch.cuda._sleep cycles) queued before each timed
+        # call's start event, so the call's launches are all submitted before
+        # the GPU reaches them -- the events then bracket the device span, not
+        # the host's submission gaps between a call's kernels
+        self.event_lead_cycles = 0
         self.cap_scale = 1  # re-rank candidate capacity multiplier, kept after an overflow
         self.cap_base = None  # initial re-rank capacity override (tests: force the overflow path)
         self.level1_fast = True  # fast top-k level 1 allowed (cleared after an overflow on this pool)
@@ -530,6 +535,8 @@ def forest_score(state: PoolState, forest: Forest, lut_dev, flags, order: int, d
     ev = None
     if state.forest_events is not None:  # bench: K2 launch timing on the launch stream
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        if state.event_lead_cycles:
+            torch.cuda._sleep(state.event_lead_cycles)
         ev[0].record()
     call("dal_forest_score", _ptr(state.x), n, state.d, state.d, _ptr(inner), _ptr(leaf),
          forest.n_trees, forest.depth, _ptr(lut_dev), 0 if density is None else _ptr(density), kind,
@@ -618,6 +625,8 @@ def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k
         ev = None
         if state.select_events is not None:  # bench: K3 timing on the launch stream
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            if state.event_lead_cycles:
+                torch.cuda._sleep(state.event_lead_cycles)
             ev[0].record()
         call("dal_dw_select", _ptr(keys_lo), _ptr(keys_hi), _ptr(votes), _ptr(flags), n, k,
              state.row_base, _ptr(lut_dev), float(beta), _ptr(state.x), state.d, state.d,
