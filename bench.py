@@ -42,7 +42,11 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
 # K2 / K3 launch timing: a GPU spin of this many cycles is queued ahead of each
 # timed call, so its launches are submitted before the GPU reaches them and the
 # HIP events bracket the device span only (not the host's submission gaps)
-EVENT_LEAD_CYCLES = 400_000
+EVENT_LEAD_CYCLES = 2_000_000
+# ... and each timed call is issued EVENT_REPEAT times between its two events
+# (an event record on this stack is a marker with a cache release: several us,
+# comparable to K3 itself); launch_ms = the bracket / EVENT_REPEAT
+EVENT_REPEAT = 10
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense f16 MFMA (same cycles as bf16)
 
 CONFIGS = {
@@ -278,7 +282,7 @@ def forest_roofline(n_rows, d, trees, forest_ms, config, world):
            "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
            "traffic": _traffic(config, "forest_score_bytes_per_launch", world), "launch_ms": forest_ms,
            "algorithmic_bytes_per_launch": nbytes, "bytes_per_row": per_row,
-           "note": "timed with HIP events on the launch stream over the warm steps (density cached), each call queued behind a GPU spin (device span, no host submission gaps)"}
+           "note": "timed with HIP events on the launch stream over the warm steps (density cached), each call queued behind a GPU spin and issued 10x back to back between the events (device time per call incl. its launch gaps; no host submission gaps, event cost amortised)"}
     if trees > 32:
         out["counters"] = ("PMC per launch at config 3 (profiles/r02/forest_config3_pmc.csv): LDS array busy "
                            "SQ_LDS_IDX_ACTIVE, 42% of it bank-conflict cycles (lane-divergent feature gathers); "
@@ -309,7 +313,7 @@ def topk_roofline(n_rows, select_ms, config, world, level1_passes=0):
             "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
             "traffic": _traffic(config, "dw_select_bytes_per_launch", world), "launch_ms": select_ms,
             "algorithmic_bytes_per_launch": nbytes, "bytes_per_row": per_row,
-            "note": "one C-ABI call (all its launches), HIP events on the launch stream, warm steps, each call queued behind a GPU spin (device span, no host submission gaps)"}
+            "note": "one C-ABI call (all its launches), HIP events on the launch stream, warm steps, each call queued behind a GPU spin and issued 10x back to back between the events (device time per call incl. its launch gaps; no host submission gaps, event cost amortised)"}
 
 
 # ----------------------------------------------------------- workloads --
@@ -495,17 +499,17 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
         step()
         # per-kernel HIP-event timing of K2 / K3 (eager launches, events on the launch stream)
         state.forest_events, state.select_events = [], []
-        state.event_lead_cycles = EVENT_LEAD_CYCLES
+        state.event_lead_cycles, state.event_repeat = EVENT_LEAD_CYCLES, EVENT_REPEAT
         for _ in range(min(warm_steps, 20)):
             step(cold=False)
         torch.cuda.synchronize()
         fev, sev = state.forest_events, state.select_events
         state.forest_events = state.select_events = None
-        state.event_lead_cycles = 0
+        state.event_lead_cycles, state.event_repeat = 0, 1
         if fev:
-            forest_ms = sum(a.elapsed_time(b) for a, b in fev) / len(fev)
+            forest_ms = sum(a.elapsed_time(b) for a, b in fev) / len(fev) / EVENT_REPEAT
         if sev:
-            select_ms = sum(a.elapsed_time(b) for a, b in sev) / len(sev)
+            select_ms = sum(a.elapsed_time(b) for a, b in sev) / len(sev) / EVENT_REPEAT
         # warm latency: the step as a user runs it (one GPU: the hipGraph replay)
         step(cold=False)
         tw, (idx_w, sc_w) = _timed(lambda: step(cold=False), warm_steps, barrier)
