@@ -93,3 +93,21 @@ def test_merge_and_mark_count_validation_without_gpu():
     assert lib.dal_mark_rows_count(None, 10, 0, 10, 1, p, p, None) == -1
     assert lib.dal_mark_rows_count(p, 10, 0, 10, 1, p, None, None) == -1
     assert lib.dal_mark_rows_count(p, -1, 0, 10, 1, p, p, None) == -2
+
+
+def test_maxcos_unit_bound_and_validation_without_gpu():
+    """ABI v7: the folded-operand max-cosine's bound (one fp16 rounding of
+    the unit labeled rows dominates: ~2^-11) and argument checks before any
+    HIP call."""
+    lib = _lib.load()
+    p = ctypes.c_void_p(256)
+    for d in (64, 128, 256):
+        b, b16 = lib.dal_maxcos_unit_error_bound(d), lib.dal_maxcos_error_bound(d)
+        assert 2.0 ** -11 < b < 2.0 ** -11 * 1.2 and b > 10 * b16
+    assert lib.dal_max_cosine_unit(None, 10, 128, p, 256, p, p, None) == -1
+    assert lib.dal_max_cosine_unit(p, 10, 96, p, 256, p, p, None) == -2      # d not 64/128/256
+    assert lib.dal_max_cosine_unit(p, 10, 128, p, 300, p, p, None) == -2     # m_pad off the granule
+    assert lib.dal_max_cosine_unit(p, 10, 128, p, 8192, p, p, None) == -2    # > 4096 labeled rows
+    assert lib.dal_max_cosine_unit(ctypes.c_void_p(264), 10, 128, p, 256, p, p, None) == -2  # unaligned
+    assert lib.dal_unit_rows_f16(None, 4, 256, 128, 128, p, p, None) == -1
+    assert lib.dal_unit_rows_f16(p, 4, 2, 128, 128, p, p, None) == -2        # m_pad < m
