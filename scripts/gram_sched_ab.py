@@ -52,6 +52,9 @@ for sh in sys.argv[1:] or ["284807x30", "100000x64"]:
         run(name)
     torch.cuda.synchronize()
     same = torch.equal(accs["base"], accs["new"])
+    # fixed point in units of 2^-32: the largest density difference, against the rigorous bound
+    diff = float((accs["base"] - accs["new"]).abs().max().item()) / 2.0 ** 32
+    bound = float(_lib._lib.dal_density_error_bound_sym(n - 10))
     reps = 5 if n * d < 5e7 else 2
     t = {"base": [], "new": []}
     for _ in range(5):
@@ -66,7 +69,8 @@ for sh in sys.argv[1:] or ["284807x30", "100000x64"]:
     fl = 2.0 * (n - 10) * (n - 10) * d
     tb, tn = statistics.median(t["base"]), statistics.median(t["new"])
     print(f"{n} x {d}: base {tb:.4f} ms ({fl / tb / 1e9 / 2500:.3f})  new {tn:.4f} ms ({fl / tn / 1e9 / 2500:.3f})  "
-          f"{'density bits identical' if same else 'DENSITY DIFFERS'}", flush=True)
+          f"{'density bits identical' if same else f'densities differ by <= {diff:.3g} (bound {bound:.3g})'}",
+          flush=True)
     _lib._lib = libs["new"]
     del st, x, op, accs
     torch.cuda.empty_cache()
