@@ -74,12 +74,30 @@ __device__ __forceinline__ uint8_t row_flag(const ForestArgs& A, int64_t row) {
   return static_cast<uint8_t>(A.hooks.base_flags[row] | (cand ? DAL_ROW_CANDIDATE : 0));
 }
 
+// A tile's minimum keys bound for its row group's atomic max (thread 0).
+struct GroupFold {
+  unsigned long long* lo_g = nullptr;  // null: nothing pending
+  unsigned long long lo = DAL_KEY_NONE, hi = DAL_KEY_NONE;
+  int64_t n_groups = 0;
+};
+
+__device__ __forceinline__ void issue_fold(GroupFold& f) {
+  if (!f.lo_g) return;
+  if (f.lo != DAL_KEY_NONE) atomicMax(f.lo_g, ~f.lo);
+  if (f.hi != DAL_KEY_NONE) atomicMax(f.lo_g + f.n_groups, ~f.hi);
+  f.lo_g = nullptr;
+}
+
 // Votes, score and keys of tile `tile` (R rows from LDS or global memory),
-// and the tile's minimum keys folded into its row group (hooks.gmin).
+// and the tile's minimum keys folded into its row group (hooks.gmin).  With
+// several blocks per group the fold is an atomic max that thread 0 returns
+// in `fold` instead of issuing (the persistent kernel issues it after the
+// next tile's DMA wait: up to 16 blocks hit a group's two words at once, and
+// a contended atomic still in flight would hold that wait).
 template <bool X_LDS>
 __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs, int xstride, int64_t tile, int R,
                                            int tpr, const int2* inner, const uint8_t* leaf, bool pre,
-                                           uint8_t fl_pre, long long dens_pre) {
+                                           uint8_t fl_pre, long long dens_pre, GroupFold& fold) {
   const int n_inner = (1 << A.depth) - 1;
   const int n_leaf = 1 << A.depth;
   const int tid = threadIdx.x;
@@ -173,8 +191,10 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
       *lo_g = ~klo;
       *hi_g = ~khi;
     } else {
-      if (klo != DAL_KEY_NONE) atomicMax(lo_g, ~klo);
-      if (khi != DAL_KEY_NONE) atomicMax(hi_g, ~khi);
+      fold.lo_g = lo_g;
+      fold.lo = klo;
+      fold.hi = khi;
+      fold.n_groups = A.hooks.n_groups;
     }
   }
 }
@@ -217,6 +237,7 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
   // lanes on consecutive banks; rows of a wave start 4 banks apart)
   const int xstride = A.d + (pad4 ? 4 : 1);
   const int r = tid / tpr, sub = tid - r * tpr;
+  GroupFold fold;  // thread 0: the previous tile's group fold, not yet issued
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {  // block-uniform
     const int64_t row0 = tile * R;
     const int64_t row = row0 + r;
@@ -298,10 +319,12 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
       }
     }
     __syncthreads();
-    score_tile<X_LDS>(A, xs, xstride, tile, R, tpr, inner, leaf, pre, fl_pre, dens_pre);
+    if (PERSIST && tid == 0) issue_fold(fold);  // after this tile's DMA wait: completes during the traversal
+    score_tile<X_LDS>(A, xs, xstride, tile, R, tpr, inner, leaf, pre, fl_pre, dens_pre, fold);
     if (!PERSIST) break;
     __syncthreads();  // every wave done with the tile before the next one is staged
   }
+  if (tid == 0) issue_fold(fold);
 }
 
 }  // namespace
