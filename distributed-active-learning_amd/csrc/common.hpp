@@ -112,6 +112,10 @@ struct ForestStepHooks {
   uint64_t* gmin = nullptr;
   int group_blocks = 1;
   int64_t n_groups = 0;
+  // base_flags set: also write the step's flags to row_flags for later
+  // kernels (the exact level 1 reads them); the fast level 1's re-rank derives
+  // its candidates' flags from the stamps itself (2M byte stores: 20 us)
+  bool write_flags = true;
 };
 
 // Rows per block of dal_forest_score's kernel for this shape (the row

@@ -140,7 +140,7 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
   unsigned long long klo = DAL_KEY_NONE, khi = DAL_KEY_NONE;
   if (live && sub == 0) {
     const uint8_t fl = pre ? fl_pre : A.flags ? row_flag(A, row) : DAL_ROW_CANDIDATE;
-    if (A.hooks.base_flags) const_cast<uint8_t*>(A.flags)[row] = fl;  // the step's flags for the later kernels
+    if (A.hooks.base_flags && A.hooks.write_flags) const_cast<uint8_t*>(A.flags)[row] = fl;  // for later kernels
     const double e = A.lut[v];
     double s, err = 0.0;
     if (A.dkind) {

@@ -463,7 +463,18 @@ struct DwRerank {
   const int32_t* votes;
   const uint8_t* flags;
   double beta;
+  // a plan step (ForestStepHooks): flags = base_flags | (stamp == step ?
+  // CANDIDATE : 0), derived here for the candidates instead of stored per row
+  const uint8_t* base_flags = nullptr;
+  const uint32_t* stamp = nullptr;
+  const uint32_t* step_id = nullptr;
 };
+
+__device__ __forceinline__ uint8_t rerank_flag(const DwRerank& R, int64_t i) {
+  if (R.base_flags)
+    return static_cast<uint8_t>(R.base_flags[i] | (R.stamp[i] == *R.step_id ? DAL_ROW_CANDIDATE : 0));
+  return R.flags ? R.flags[i] : DAL_ROW_CANDIDATE;
+}
 
 // The canonical score of local row i, computed by a whole wave (every lane
 // calls it with the same row): lane f forms the rounded product
@@ -489,7 +500,7 @@ __device__ __forceinline__ bool dw_canonical_score_wave(const DwRerank& R, int64
                                                         double lut_lane = 0.0, int n_lut = 0) {
   constexpr int kC = 4;  // 64-feature chunks per round: every chunk's loads and divisions in flight together
   const int lane = threadIdx.x & 63;
-  const uint8_t fl = R.flags ? R.flags[i] : DAL_ROW_CANDIDATE;
+  const uint8_t fl = rerank_flag(R, i);
   const double nr = R.norm64[i];
   const int v = R.votes[i];
   const float* xr = R.x + i * R.ldx;
@@ -539,7 +550,7 @@ __device__ __forceinline__ bool dw_canonical_score_wave(const DwRerank& R, int64
 template <int kChunk = 64>
 __device__ __forceinline__ bool dw_canonical_score_lane(const DwRerank& R, int64_t i, double& s, double e_in,
                                                         int n_lut) {
-  const uint8_t fl = R.flags ? R.flags[i] : DAL_ROW_CANDIDATE;
+  const uint8_t fl = rerank_flag(R, i);
   if (!(fl & DAL_ROW_CANDIDATE)) {
     s = __builtin_nan("");
     return false;
@@ -1787,6 +1798,7 @@ int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_
     hooks.n_groups = S.ng;
   }
   const bool folded = in_score && hooks.group_blocks > 1;  // atomic max: the buffer starts (and is left) zero
+  hooks.write_flags = false;  // the re-rank below derives its candidates' flags from the stamps
   if (!clean) {
     zero_words(reinterpret_cast<uint32_t*>(h1), kFastHdrWords, st);
     if (folded) zero_words(reinterpret_cast<uint32_t*>(gmin), 2 * S.ng * 2, st);
@@ -1797,7 +1809,8 @@ int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_
   if (!in_score) S = launch_group_min(keys_lo, keys_hi, n, gmin, nullptr, 0, st);
   if (colsum_ready && hipStreamWaitEvent(st, reinterpret_cast<hipEvent_t>(colsum_ready), 0) != hipSuccess)
     return DAL_ERR_HIP;
-  const DwRerank R{x, static_cast<int>(d), ldx, norm64, colsum, lut, votes, row_flags, beta};
+  const DwRerank R{x, static_cast<int>(d), ldx, norm64, colsum, lut, votes, row_flags, beta,
+                   hooks.base_flags, hooks.stamp, hooks.step_id};
   const int n_lut = n_trees < 64 ? n_trees + 1 : 0;  // LUT held in lanes when it fits a wave
   SortTail tail;
   tail.cap = cap;

@@ -304,8 +304,11 @@ int dal_dw_step(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t
  * dal_dw_plan_create captures dal_dw_step (DAL_STEP_RESET_STATUS |
  * DAL_STEP_WS_CLEAN, no colsum event) over the given caller-owned buffers as a
  * hipGraph (the workspace is zeroed once, synchronously on ``stream``).
- * ``flags`` is the step's row-flag buffer, rebuilt by every run from
- * ``base_flags`` (the pool's EXCLUDED bits) and the unlabeled list; the
+ * ``flags`` is the step's row-flag scratch: runs with the exact level 1
+ * (level1_passes = 0) rebuild it from ``base_flags`` (the pool's EXCLUDED
+ * bits) and the unlabeled list; with the fast level 1 the re-rank derives its
+ * candidates' flags from the step's row stamps and ``flags`` is not written
+ * (ABI v7); the
  * selection lands in out_pair[0..k) (indices) and out_pair[k..2k) (fp64
  * score bits).  dal_dw_plan_run(plan, unl, n_unl, out_idx, out_scores,
  * status, stream): flags <- base_flags, mark unl as DAL_ROW_CANDIDATE, replay
