@@ -74,30 +74,48 @@ __device__ __forceinline__ uint8_t row_flag(const ForestArgs& A, int64_t row) {
   return static_cast<uint8_t>(A.hooks.base_flags[row] | (cand ? DAL_ROW_CANDIDATE : 0));
 }
 
-// A tile's minimum keys bound for its row group's atomic max (thread 0).
+constexpr int kForestWaves = kForestThreads / 64;
+
+// A tile's group fold left for the persistent kernel's thread 0: the tile's
+// per-wave minimum keys sit in wmin[slot] (LDS, written by each wave's lane 0
+// at the end of its traversal -- no block barrier inside the tile); slot =
+// the block's iteration parity, so the next tile's waves write the other one
+// while thread 0 reads this one.
 struct GroupFold {
-  unsigned long long* lo_g = nullptr;  // null: nothing pending
-  unsigned long long lo = DAL_KEY_NONE, hi = DAL_KEY_NONE;
-  int64_t n_groups = 0;
+  int64_t tile = -1;  // -1: nothing pending
+  int slot = 0;       // this block's next free wmin slot / the pending tile's
 };
 
-__device__ __forceinline__ void issue_fold(GroupFold& f) {
-  if (!f.lo_g) return;
-  if (f.lo != DAL_KEY_NONE) atomicMax(f.lo_g, ~f.lo);
-  if (f.hi != DAL_KEY_NONE) atomicMax(f.lo_g + f.n_groups, ~f.hi);
-  f.lo_g = nullptr;
+// thread 0, after the next tile's DMA wait: reduce the pending tile's wave
+// minima and atomic-max them into its row group (the atomics then complete
+// during that tile's traversal: up to 16 blocks hit a group's two words at
+// once, and a contended atomic in flight would hold the next DMA wait)
+__device__ __forceinline__ void issue_fold(const ForestArgs& A, GroupFold& f,
+                                           const unsigned long long (*wmin)[2][kForestWaves]) {
+  if (f.tile < 0) return;
+  const unsigned long long(&m)[2][kForestWaves] = wmin[f.slot ^ 1];
+  unsigned long long lo = m[0][0], hi = m[1][0];
+#pragma unroll
+  for (int w = 1; w < kForestWaves; ++w) {
+    lo = m[0][w] < lo ? m[0][w] : lo;
+    hi = m[1][w] < hi ? m[1][w] : hi;
+  }
+  unsigned long long* lo_g = reinterpret_cast<unsigned long long*>(A.hooks.gmin) +
+                             static_cast<uint32_t>(f.tile) / static_cast<uint32_t>(A.hooks.group_blocks);
+  if (lo != DAL_KEY_NONE) atomicMax(lo_g, ~lo);
+  if (hi != DAL_KEY_NONE) atomicMax(lo_g + A.hooks.n_groups, ~hi);
+  f.tile = -1;
 }
 
 // Votes, score and keys of tile `tile` (R rows from LDS or global memory),
 // and the tile's minimum keys folded into its row group (hooks.gmin).  With
-// several blocks per group the fold is an atomic max that thread 0 returns
-// in `fold` instead of issuing (the persistent kernel issues it after the
-// next tile's DMA wait: up to 16 blocks hit a group's two words at once, and
-// a contended atomic still in flight would hold that wait).
+// several blocks per group in the persistent kernel (wmin non-null) the
+// fold is left pending (GroupFold, issue_fold).
 template <bool X_LDS>
 __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs, int xstride, int64_t tile, int R,
                                            int tpr, const int2* inner, const uint8_t* leaf, bool pre,
-                                           uint8_t fl_pre, long long dens_pre, GroupFold& fold) {
+                                           uint8_t fl_pre, long long dens_pre, GroupFold& fold,
+                                           unsigned long long (*wmin)[2][kForestWaves]) {
   const int n_inner = (1 << A.depth) - 1;
   const int n_leaf = 1 << A.depth;
   const int tid = threadIdx.x;
@@ -172,6 +190,15 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
     klo = a < klo ? a : klo;
     khi = b < khi ? b : khi;
   }
+  if (wmin && A.hooks.group_blocks > 1) {  // kernel-uniform
+    if ((tid & 63) == 0) {
+      wmin[fold.slot][0][tid >> 6] = klo;
+      wmin[fold.slot][1][tid >> 6] = khi;
+    }
+    fold.tile = tile;
+    fold.slot ^= 1;  // issue_fold reads slot ^ 1: this tile's
+    return;
+  }
   __shared__ unsigned long long s_min[2][kForestThreads / 64];
   if ((tid & 63) == 0) {
     s_min[0][tid >> 6] = klo;
@@ -191,10 +218,8 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
       *lo_g = ~klo;
       *hi_g = ~khi;
     } else {
-      fold.lo_g = lo_g;
-      fold.lo = klo;
-      fold.hi = khi;
-      fold.n_groups = A.hooks.n_groups;
+      if (klo != DAL_KEY_NONE) atomicMax(lo_g, ~klo);
+      if (khi != DAL_KEY_NONE) atomicMax(hi_g, ~khi);
     }
   }
 }
@@ -237,7 +262,8 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
   // lanes on consecutive banks; rows of a wave start 4 banks apart)
   const int xstride = A.d + (pad4 ? 4 : 1);
   const int r = tid / tpr, sub = tid - r * tpr;
-  GroupFold fold;  // thread 0: the previous tile's group fold, not yet issued
+  GroupFold fold;  // the previous tile's group fold, not yet issued (persistent kernel)
+  __shared__ unsigned long long wmin[2][2][kForestWaves];
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {  // block-uniform
     const int64_t row0 = tile * R;
     const int64_t row = row0 + r;
@@ -319,12 +345,13 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
       }
     }
     __syncthreads();
-    if (PERSIST && tid == 0) issue_fold(fold);  // after this tile's DMA wait: completes during the traversal
-    score_tile<X_LDS>(A, xs, xstride, tile, R, tpr, inner, leaf, pre, fl_pre, dens_pre, fold);
+    if (PERSIST && tid == 0) issue_fold(A, fold, wmin);  // after this tile's DMA wait
+    score_tile<X_LDS>(A, xs, xstride, tile, R, tpr, inner, leaf, pre, fl_pre, dens_pre, fold,
+                      PERSIST ? wmin : nullptr);
     if (!PERSIST) break;
     __syncthreads();  // every wave done with the tile before the next one is staged
   }
-  if (tid == 0) issue_fold(fold);
+  if (PERSIST && tid == 0) issue_fold(A, fold, wmin);  // the last tile's (its waves passed the loop barrier)
 }
 
 }  // namespace
