@@ -18,7 +18,11 @@ selection of the exact separable density path on the same pool.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-Prints ONE JSON line on rank 0.
+Output (rank 0): one compact JSON line per extra workload ({"extra": label,
+...}, <= 1 KB each), then the compact headline as the LAST stdout line
+(<= 4 KB: metric, value, roofline, cpu_baseline, self-checks, world size).
+The full result with every note and sub-field goes to --out
+(default gpurun_out/bench_full.json).
 """
 from __future__ import annotations
 
@@ -240,8 +244,10 @@ def gram_roofline(gram, achieved, traffic, gram_ms, gram_ms_max, flops, products
     names = {3: "h.h, h.l, l.h", 2: "H.H, H.L on the taker side + the exact closed-form remainder "
                                      "(dal_gram_sym_residual, included in launch_ms)"}
     return {"bound": "mfma",
-            "kernel": (f"dal_gram_rowsum_{'sym' if sym else 'split'} ({'symmetric block pairs once; ' if sym else ''}"
-                       f"{products} x v_mfma_f32_16x16x32_f16 per 32 features: {names.get(products, '')})"),
+            "kernel": (f"dal_gram_rowsum_{'sym + dal_gram_sym_residual' if sym else 'split'} "
+                       f"({products}x v_mfma_f32_16x16x32_f16 / 32 features)"),
+            "kernel_note": (f"{'symmetric block pairs once; ' if sym else ''}{products} fp16 products per 32 "
+                            f"features: {names.get(products, '')}"),
             "achieved": achieved, "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved / F16_MFMA_PEAK_TFLOPS,
             "peak_note": "dense fp16 MFMA peak (MI355X_MICROARCH.md); achieved counts the algorithmic "
@@ -454,6 +460,8 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
     for _ in range(warmup):
         step()
     state.gram_events, state.residual_events = [], []
+    if world > 1:
+        sel.exchange_events = []
     elapsed, (idx_g, sc_g) = _timed(step, steps, barrier)
     events, state.gram_events = state.gram_events, None
     res_events, state.residual_events = state.residual_events, []
@@ -461,6 +469,15 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
     # N > 1; plus the compensation's closed-form remainder), averaged over steps
     resid_ms = sum(a.elapsed_time(b) for a, b in res_events) / max(steps, 1)
     gram_ms = sum(a.elapsed_time(b) for a, b in events) / max(steps, 1) + resid_ms
+    ranks = None
+    if world > 1:  # the density exchange's collectives, per step, and their max over ranks
+        xev, sel.exchange_events = sel.exchange_events, None
+        ag_ms = sum(a.elapsed_time(b) for nm, a, b in xev if nm == "all_gather") / max(steps, 1)
+        rs_ms = sum(a.elapsed_time(b) for nm, a, b in xev if nm == "reduce_scatter") / max(steps, 1)
+        gram_min = -_max_over_ranks([-gram_ms], world, dist, tdev)[0]
+        g_max, ag_max, rs_max = _max_over_ranks([gram_ms, ag_ms, rs_ms], world, dist, tdev)
+        ranks = {"gram_ms_max": g_max, "gram_ms_min": gram_min, "all_gather_ms_max": ag_max,
+                 "reduce_scatter_ms_max": rs_max}
     elapsed, gram_ms_max = _max_over_ranks([elapsed, gram_ms], world, dist, tdev)
 
     # accuracy (outside the timed region): the timed step's
@@ -596,6 +613,7 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
         "roofline_topk": topk_roofline(state.n, select_ms, config, world,
                                        engine.LEVEL1_PASSES if state.level1_fast else 0),
         "cpu_baseline": None,
+        "ranks": ranks,
     }
     if rank == 0 and world == 1 and cpu and not args.no_cpu_baseline:
         from oracle import dal_oracle as O
@@ -772,6 +790,114 @@ def bench_rf_train(dev, n: int = 5000, d: int = 64, trees: int = 10, reps: int =
                     "a different (midpoint-threshold) algorithm timed for scale"}
 
 
+# ------------------------------------------------------------- output --
+HEADLINE_MAX_BYTES = 4000
+EXTRA_MAX_BYTES = 1024
+
+
+def _r(v, nd=4):
+    """A float rounded to ``nd`` significant digits (None passes)."""
+    if v is None or isinstance(v, (bool, int, str)):
+        return v
+    return float(f"{float(v):.{nd}g}")
+
+
+def _roof_short(r, keys=("bound", "achieved", "peak", "unit", "frac", "traffic", "launch_ms")):
+    if not r:
+        return None
+    return {k: _r(r.get(k), 5 if k in ("frac", "launch_ms") else 4) for k in keys if k in r}
+
+
+def _checks(sc):
+    """The boolean self-checks of a result (names kept, notes dropped)."""
+    if not sc:
+        return None
+    return {k: v for k, v in sc.items() if isinstance(v, bool) or v is None}
+
+
+def headline(out: dict) -> dict:
+    """The driver-parsed last stdout line: the contract's keys, numbers only
+    in the sub-objects, short kernel names; everything else stays in the full
+    result file."""
+    h = {k: out.get(k) for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                 "higher_is_better", "scaling", "vs_baseline", "dtype", "data")}
+    cfg = out.get("config") or {}
+    h["config"] = {k: cfg[k] for k in ("workload", "pool_rows", "features", "trees", "k", "labeled",
+                                       "parallelism") if k in cfg}
+    for k in ("world_size", "backend"):
+        h[k] = out.get(k)
+    h["value"], h["ms_per_step"] = _r(out.get("value"), 6), _r(out.get("ms_per_step"), 6)
+    h["warm_selection_latency_ms"] = _r(out.get("warm_selection_latency_ms"))
+    h["self_check"] = _checks(out.get("self_check"))
+    roof = out.get("roofline") or {}
+    h["roofline"] = dict(_roof_short(roof) or {}, kernel=str(roof.get("kernel", ""))[:80],
+                         launch_ms_max_over_ranks=_r(roof.get("launch_ms_max_over_ranks"), 5),
+                         algorithmic_flops_per_launch=_r(roof.get("algorithmic_flops_per_launch"), 6))
+    h["roofline_forest"] = _roof_short(out.get("roofline_forest"))
+    h["roofline_topk"] = _roof_short(out.get("roofline_topk"))
+    cb = out.get("cpu_baseline")
+    h["cpu_baseline"] = None if not cb else {"value": _r(cb.get("value")), "unit": cb.get("unit"),
+                                             "cores": cb.get("cores"), "kind": cb.get("kind"),
+                                             "sample": str(cb.get("sample", ""))[:160]}
+    acc = out.get("accuracy") or {}
+    if acc:
+        h["accuracy"] = {k: _r(acc.get(k), 3) for k in ("density_max_rel_err", "density_err_bound_rel",
+                                                         "kth_gap_rel") if k in acc}
+    if out.get("ranks"):
+        h["ranks"] = {k: _r(v) for k, v in out["ranks"].items()}
+    if out.get("full_result"):
+        h["full_result"] = out["full_result"]
+    return h
+
+
+def extra_line(label: str, r: dict) -> dict:
+    """One extra workload as a short JSON object (printed before the headline)."""
+    if "gpu_ms_per_fit" in r:  # rf_train
+        return {"extra": label, "gpu_ms_per_fit": _r(r["gpu_ms_per_fit"]),
+                "sklearn_host_ms_per_fit": _r(r["sklearn_host_ms_per_fit"]), "cores": r.get("cores")}
+    cfg = r.get("config") or {}
+    e = {"extra": label, "value": _r(r.get("value"), 5), "unit": r.get("unit"),
+         "ms_per_step": _r(r.get("ms_per_step"), 5), "steps": r.get("steps"),
+         "shape": f"{cfg.get('pool_rows')}x{cfg.get('features')}"
+                  + (f" T={cfg['trees']}" if "trees" in cfg else "") + f" k={cfg.get('k')}"
+                  + (f" m={cfg['labeled']}" if "labeled" in cfg else ""),
+         "warm_ms": _r(r.get("warm_selection_latency_ms"))}
+    for key, short in (("roofline", "gram"), ("roofline_forest", "forest"), ("roofline_topk", "topk")):
+        ro = r.get(key)
+        if ro:
+            e[short] = {"frac": _r(ro.get("frac")), "ms": _r(ro.get("launch_ms")), "bound": ro.get("bound")}
+    if "gram" in e and str(r["roofline"].get("kernel", "")).startswith("dal_max_cosine"):
+        e["maxcos"] = e.pop("gram")
+    cb = r.get("cpu_baseline")
+    if cb:
+        e["cpu_rows_per_s"] = _r(cb.get("value"))
+    sc = _checks(r.get("self_check"))
+    if sc is not None:
+        e["self_check_ok"] = all(v for v in sc.values() if v is not None)
+    acc = r.get("accuracy") or {}
+    if "density_max_rel_err" in acc:
+        e["density_max_rel_err"] = _r(acc["density_max_rel_err"], 3)
+    if acc.get("density_max_err_over_abs_rowsum") is not None:  # signed pools (config 3)
+        e["density_err_over_abs_rowsum"] = _r(acc["density_max_err_over_abs_rowsum"], 3)
+    return e
+
+
+def emit(out: dict, path: str | None):
+    """Write the full result to ``path`` and print the extras, then the
+    headline LAST (rank 0 only)."""
+    if path:
+        try:
+            os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+            with open(path, "w") as f:
+                json.dump(out, f, indent=1)
+            out = dict(out, full_result=os.path.relpath(os.path.abspath(path), REPO))
+        except OSError as e:  # the headline still prints
+            print(f"bench: could not write {path}: {e}", file=sys.stderr)
+    for label, r in (out.get("extra") or {}).items():
+        print(json.dumps(extra_line(label, r), separators=(",", ":")), flush=True)
+    print(json.dumps(headline(out)), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -784,6 +910,8 @@ def main():
     ap.add_argument("--warm-steps", type=int, default=None)
     ap.add_argument("--trees", type=int, default=None, help="override the config's forest size (config 4: T=100)")
     ap.add_argument("--k", type=int, default=None, help="override the config's selection size (config 4: k=1000)")
+    ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "bench_full.json"),
+                    help="file for the full result (every note and sub-field); '' to skip")
     args = ap.parse_args()
     main_cfg = resolve(f"{args.config}" + (f":T{args.trees}" if args.trees is not None else "")
                        + (f":k{args.k}" if args.k is not None else ""))[1]
@@ -841,8 +969,10 @@ def main():
                                                             "line's O(N^2) Gram row-sum (cpu_baseline above)")
     if world == 1 and CONFIGS[args.config].get("mode") != "div":
         out.setdefault("extra", {})["rf_train"] = bench_rf_train(dev)
+    out["world_size"] = dist.get_world_size() if world > 1 else 1
+    out["backend"] = dist.get_backend() if world > 1 else None
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out, args.out)
     if world > 1:
         dist.destroy_process_group()
 

@@ -68,14 +68,7 @@ struct dal_dw_plan {
   hipGraphNode_t mark_node = nullptr;  // the mark kernel's node (its arguments change every replay)
   hipKernelNodeParams mark_params{};   // its launch shape, reused by every SetParams
   uint32_t step = 0;
-  bool timing = false;            // DAL_PLAN_TIMING=1: host time per phase, printed by destroy
-  double t_refresh = 0, t_launch = 0, t_sync = 0;
-  int64_t runs = 0;
 };
-
-static double now_us() {
-  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
 
 using namespace dal;
 
@@ -186,8 +179,6 @@ extern "C" int dal_dw_plan_create(const float* x, int64_t n, int64_t d, int64_t 
   p->k = k;
   p->out_pair = out_pair;
   p->dev_status = dev_status;
-  const char* tm = getenv("DAL_PLAN_TIMING");
-  p->timing = tm && atoi(tm) != 0;
   *plan_out = p;
   return DAL_OK;
 }
@@ -198,7 +189,6 @@ extern "C" int dal_dw_plan_run(dal_dw_plan_t* p, const int64_t* unl, int64_t n_u
   hipStream_t st = as_stream(stream);
   const DeviceGuard guard(st);
   if (!guard.ok() || guard.device() != p->device) return DAL_ERR_ARG;  // a stream of another device
-  const double t0 = p->timing ? now_us() : 0.0;
   volatile PlanSlot* slot = p->slot;
   const uint32_t step = ++p->step;
   {
@@ -215,9 +205,7 @@ extern "C" int dal_dw_plan_run(dal_dw_plan_t* p, const int64_t* unl, int64_t n_u
   slot->out[1] = reinterpret_cast<int64_t*>(out_scores);
   slot->status = -1;  // overwritten by the graph's last kernel
   std::atomic_thread_fence(std::memory_order_seq_cst);
-  const double t1 = p->timing ? now_us() : 0.0;
   if (hipGraphLaunch(p->exec, st) != hipSuccess) return DAL_ERR_HIP;
-  const double t2 = p->timing ? now_us() : 0.0;
   // the graph's last kernel publishes the status word last: spin on it (a
   // blocking stream sync wakes up tens of microseconds late), bounded, then
   // fall back to the sync.  Later work on the stream is ordered after the
@@ -227,13 +215,6 @@ extern "C" int dal_dw_plan_run(dal_dw_plan_t* p, const int64_t* unl, int64_t n_u
   std::atomic_thread_fence(std::memory_order_seq_cst);
   if (slot->status < 0 && hipStreamSynchronize(st) != hipSuccess) return DAL_ERR_HIP;
   std::atomic_thread_fence(std::memory_order_seq_cst);
-  if (p->timing) {
-    const double t3 = now_us();
-    p->t_refresh += t1 - t0;
-    p->t_launch += t2 - t1;
-    p->t_sync += t3 - t2;
-    ++p->runs;
-  }
   const int32_t v = slot->status;
   if (v < 0) return DAL_ERR_HIP;  // the step did not publish its status
   *status_out = v;
@@ -264,9 +245,6 @@ extern "C" int dal_dw_plan_launch(dal_dw_plan_t* p, const int64_t* unl, int64_t 
 
 extern "C" void dal_dw_plan_destroy(dal_dw_plan_t* p) {
   if (!p) return;
-  if (p->timing && p->runs)
-    fprintf(stderr, "dal_dw_plan: %lld runs, host us per run: refresh %.1f, graph launch %.1f, sync %.1f\n",
-            static_cast<long long>(p->runs), p->t_refresh / p->runs, p->t_launch / p->runs, p->t_sync / p->runs);
   if (p->exec) (void)hipGraphExecDestroy(p->exec);
   if (p->graph) (void)hipGraphDestroy(p->graph);
   if (p->slot) (void)hipHostFree(p->slot);

@@ -8,7 +8,9 @@ Reference pipeline:
                     :148      e = -(1-v/T) log2(1-v/T)
                     :157-161  d_i = sum of the row's remaining S entries (includes j = i)
                     :166-172  score = e * d, descending sortBy, take(window_size)
-Here: a fused fp32-MFMA Gram row-sum (S never exists; the density is cached
+Here: a fused MFMA Gram row-sum -- fp16 MFMA on a two-term (hi/lo) fp16
+split of the unit rows, each symmetric block pair once, plus an exact
+closed-form remainder, accumulated in int64 fixed point (S never exists; the density is cached
 per pool because the reference's is constant across iterations), a fused
 forest + score kernel, and a device top-k whose boundary candidates are
 re-ranked in canonical fp64 so the selected set is bit-exact.
@@ -24,8 +26,9 @@ def information_density(pool, excluded_idx=None, device=None, mode: str = "gram"
     """d_i = sum_{j not in E} cos(x_i, x_j) for every row (fp64, NaN for i in E).
 
     excluded_idx  E; the reference uses L0 = range(window_size).
-    mode          "gram": fused fp32-MFMA Gram row-sum (the reference's N^2
-                  algorithm, within dal_density_error_bound of canonical);
+    mode          "gram": fused compensated fp16-split MFMA Gram row-sum (the
+                  reference's N^2 algorithm, fp32-class: within
+                  dal_density_error_bound_sym of canonical);
                   "separable": exact O(N*D) identity, canonical fp64 bits.
     """
     state = as_pool_state(pool, excluded=excluded_idx, device=device)

@@ -12,7 +12,6 @@ Reference loop body being replaced (one ``while True`` iteration):
 from __future__ import annotations
 
 
-import os
 import weakref
 
 import numpy as np
@@ -174,7 +173,7 @@ class PoolState:
         self.cap_scale = 1  # re-rank candidate capacity multiplier, kept after an overflow
         self.cap_base = None  # initial re-rank capacity override (tests: force the overflow path)
         self.level1_fast = True  # fast top-k level 1 allowed (cleared after an overflow on this pool)
-        self.use_graphs = os.environ.get("DAL_GRAPHS", "1") != "0"  # hipGraph replay of warm steps
+        self.use_graphs = True  # hipGraph replay of warm steps (tests compare with eager steps)
         self._graphs = {}  # warm-step graphs by (T, depth, k, beta, cap, level-1 passes)
         self.last_status = 0     # status word read by the last synchronising select
 
@@ -461,12 +460,10 @@ def _gram_kind(gram) -> str:
     """Density GEMM kernel: "sym" (default; fp16 MFMA on the two-term split,
     each symmetric block pair once, H-only taker side + exact closed-form
     remainder) or "f32" (fp32 MFMA on the unit rows, every pair: the
-    plain-precision reference kernel).  DAL_GRAM in the environment overrides
-    the default.  Both are within their rigorous bound of the canonical
-    density and give the same (bit-exact) selection."""
-    import os
-
-    g = gram if gram is not None else os.environ.get("DAL_GRAM", "sym")
+    plain-precision reference kernel, chosen per pool by the caller).  Both
+    are within their rigorous bound of the canonical density and give the
+    same (bit-exact) selection."""
+    g = "sym" if gram is None else gram
     if g not in GRAM_KINDS:
         raise ValueError(f"gram must be one of {GRAM_KINDS}, not {g!r}")
     return g
@@ -586,9 +583,9 @@ def candidate_cap(n: int, k: int) -> int:
 
 # Fast level 1 of the interval selections (ABI v6): tau = the k-th smallest
 # of <= 4096 row groups' minimum keys bounds the candidate search (group
-# minima + one launch instead of 6 radix passes + 3 compaction launches).
-# DAL_LEVEL1_PASSES overrides (0 = the exact radix level 1).
-LEVEL1_PASSES = int(os.environ.get("DAL_LEVEL1_PASSES", "1"))
+# minima + one launch instead of 6 radix passes + 3 compaction launches);
+# 0 selects the exact radix level 1 (after an overflow, per pool).
+LEVEL1_PASSES = 1
 
 
 def level1_passes(state, n: int, k: int, cap: int) -> int:

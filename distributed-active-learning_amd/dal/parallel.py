@@ -104,6 +104,10 @@ class ShardedSelector:
         self._colsum = None      # the global canonical column sum reduced from them (cached)
         self._plans = {}         # warm-step plans by (T, depth, k, beta, cap, level-1 passes)
         self.cap_scale = 1      # re-rank candidate capacity multiplier (grown on overflow)
+        # bench: list -> (name, start, end) HIP events around the density
+        # exchange's collectives ("all_gather": operand + partials, recorded on
+        # the stream that waits for them; "reduce_scatter": the density sum)
+        self.exchange_events = None
 
     def index_tensor(self, unlabeled_idx):
         from .engine import _as_index
@@ -204,8 +208,13 @@ class ShardedSelector:
             side = _side_stream(st.device)
             side.wait_event(ready)
             with torch.cuda.stream(side):
+                ev = self._event_start("all_gather")
                 parts_full, pwork = comm.all_gather_start(parts) if parts is not None else (None, None)
                 u_full, work = comm.all_gather_start(u_local)
+                if ev is not None:  # the side stream waits for the collectives, then records
+                    comm.wait(work)
+                    comm.wait(pwork)
+                    self._event_end(ev)
             for t in (u_full, parts_full):
                 if t is not None:
                     t.record_stream(main)
@@ -213,12 +222,18 @@ class ShardedSelector:
             comm.wait(work)   # the current (main) stream waits for the collectives
             comm.wait(pwork)
         else:
+            ev = self._event_start("all_gather")
             parts_full, pwork = comm.all_gather_start(parts) if parts is not None else (None, None)
             u_full, work = comm.all_gather_start(u_local)
+            if ev is not None and work is None and pwork is None:  # staged (gloo): already complete
+                self._event_end(ev)
+                ev = None
             if st.n:
                 st.gram_accumulate(acc, u_local, self.shard, col_row0=self.lo)
             comm.wait(work)
             comm.wait(pwork)
+            if ev is not None:
+                self._event_end(ev)
         if st.n and self.world > 1:
             if st.gram == "sym":  # one launch over every other column
                 st.gram_accumulate(acc, u_full, self.world * self.shard, col_row0=0,
@@ -229,9 +244,24 @@ class ShardedSelector:
         if st.gram == "sym":
             if st.n:  # the compensation's closed-form remainder of this rank's rows
                 st.gram_residual(acc, u_full)
+            ev = self._event_start("reduce_scatter")
             acc = comm.reduce_scatter_sum(acc)
+            self._event_end(ev)
         self.set_density(acc)
         return u_full, parts_full
+
+    def _event_start(self, name):
+        if self.exchange_events is None:
+            return None
+        torch = __import__("torch")
+        ev = (name, torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[1].record()
+        return ev
+
+    def _event_end(self, ev):
+        if ev is not None:
+            ev[2].record()
+            self.exchange_events.append(ev)
 
     def _new_acc(self):
         torch = __import__("torch")

@@ -8,6 +8,9 @@
 #   tests[=EXPR]          pytest -m gpu (optionally -k EXPR, ',' = space) -> gpurun_out/pytest_gpu.log
 #   smoke                 __graft_entry__.smoke()             -> gpurun_out/smoke.log
 #   bench[=ARGS]          python bench.py ARGS (',' = space)  -> gpurun_out/bench_<n>.log
+#                         (full result: gpurun_out/bench_full_<n>.json)
+#   gloo=N[=ARGS]         bench.py on N gloo ranks sharing the one GPU (torch.distributed.run)
+#                         -> gpurun_out/gloo_<n>.log
 #   stats=TAG[=ARGS]      rocprofv3 --kernel-trace --stats of bench.py ARGS -> gpurun_out/prof_TAG/
 #   pmc=TAG=CTRS[=ARGS]   rocprofv3 --pmc CTRS (',' = space) of bench.py ARGS -> gpurun_out/pmc_TAG/
 #   pmcpy=TAG=CTRS=SCRIPT[=ARGS]  rocprofv3 --pmc CTRS of python SCRIPT ARGS -> gpurun_out/pmc_TAG/
@@ -38,10 +41,22 @@ for step in "$@"; do
       echo "[$n] smoke rc=$rc: $(tail -1 gpurun_out/smoke.log)"
       ;;
     bench)
-      timeout -k 10 900 python -u bench.py ${rest//,/ } > gpurun_out/bench_$n.log 2>&1
+      timeout -k 10 900 python -u bench.py ${rest//,/ } --out gpurun_out/bench_full_$n.json \
+        > gpurun_out/bench_$n.log 2>&1
       rc=$?
       echo "[$n] bench ${rest//,/ } rc=$rc"
       tail -1 gpurun_out/bench_$n.log | cut -c1-600
+      ;;
+    gloo)
+      np=${rest%%=*}
+      args=""
+      [[ "$rest" == *=* ]] && args=${rest#*=}
+      DAL_BENCH_BACKEND=gloo timeout -k 10 900 python -u -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node $np --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus $np \
+        ${args//,/ } --out gpurun_out/gloo_full_$n.json > gpurun_out/gloo_$n.log 2>&1
+      rc=$?
+      echo "[$n] gloo $np ${args//,/ } rc=$rc"
+      tail -1 gpurun_out/gloo_$n.log | cut -c1-600
       ;;
     stats)
       tag=${rest%%=*}

@@ -117,3 +117,64 @@ def test_div_self_check_canonical_numpy():
     got = bench.canon_maxcos(X[50:], X[:20])
     ref, _ = O.max_cosine_canonical(X, np.arange(20))
     assert np.array_equal(got, ref[50:])
+
+
+def _canned_result():
+    """The full result of a real default run (round 3, config 4 + extras)."""
+    import json
+    import os
+
+    path = os.path.join(os.path.dirname(bench.__file__), "profiles", "r03", "final_s3", "bench_line.json")
+    with open(path) as f:
+        out = json.load(f)
+    out.update(world_size=1, backend=None)
+    return out
+
+
+def test_headline_is_compact_and_complete():
+    """The driver keeps an ~8 KB stdout tail: the LAST line (the headline)
+    must stay <= 4,000 bytes and carry the contract's keys, roofline and
+    cpu_baseline (the 25 KB line was unparseable)."""
+    import json
+
+    out = _canned_result()
+    out["roofline"]["kernel"] = "x" * 500  # long free text is cut, not carried
+    out["cpu_baseline"]["sample"] = "y" * 2000
+    h = bench.headline(out)
+    s = json.dumps(h)
+    assert len(s.encode()) <= bench.HEADLINE_MAX_BYTES
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "dtype", "config",
+                "warm_selection_latency_ms", "self_check", "roofline", "roofline_forest", "roofline_topk",
+                "cpu_baseline", "world_size", "backend"):
+        assert key in h, key
+    for key in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel"):
+        assert key in h["roofline"], key
+    assert len(h["roofline"]["kernel"]) <= 80
+    assert set(h["cpu_baseline"]) == {"value", "unit", "cores", "kind", "sample"}
+    assert all(isinstance(v, bool) for v in h["self_check"].values())
+    assert h["value"] == round(out["value"], -1) or abs(h["value"] / out["value"] - 1) < 1e-5
+    # a multi-GPU record names its rank count and the per-rank exchange maxima
+    out.update(world_size=8, backend="nccl", n_gpus=8,
+               ranks={"gram_ms_max": 160.1, "gram_ms_min": 158.0, "all_gather_ms_max": 3.2,
+                      "reduce_scatter_ms_max": 0.4})
+    h8 = bench.headline(out)
+    assert h8["world_size"] == 8 and h8["backend"] == "nccl" and h8["ranks"]["all_gather_ms_max"] == 3.2
+    assert len(json.dumps(h8).encode()) <= bench.HEADLINE_MAX_BYTES
+
+
+def test_emit_prints_extras_then_headline_last(tmp_path, capsys):
+    import json
+
+    out = _canned_result()
+    bench.emit(out, str(tmp_path / "full.json"))
+    lines = capsys.readouterr().out.strip().split("\n")
+    assert len(lines) == len(out["extra"]) + 1
+    for line, label in zip(lines, out["extra"]):
+        e = json.loads(line)
+        assert e["extra"] == label and len(line.encode()) <= bench.EXTRA_MAX_BYTES
+    last = json.loads(lines[-1])
+    assert last["metric"] == bench.METRIC and "roofline" in last and "cpu_baseline" in last
+    assert len(lines[-1].encode()) <= bench.HEADLINE_MAX_BYTES
+    full = json.load(open(tmp_path / "full.json"))  # every sub-field kept in the file
+    assert full["roofline"]["kernel_note"] if "kernel_note" in full["roofline"] else full["roofline"]["kernel"]
+    assert set(full["extra"]) == set(out["extra"])

@@ -309,17 +309,15 @@ def test_warm_plan_exact_level1_and_capacity_growth(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("setparams", ["1", "0"])
-def test_warm_plan_marking_modes(cuda, monkeypatch, setparams):
-    """The plan's per-step marking, both ways: kernel arguments rewritten per
-    replay (hipGraphExecKernelNodeSetParams, the default) and the host-mapped
-    slot read by a fetch kernel (DAL_PLAN_SETPARAMS=0).  The unlabeled list
-    shrinks every step (stale stamps of earlier steps must not count) and the
-    selections equal the oracle's."""
+def test_warm_plan_marking(cuda):
+    """The plan's per-step marking: the marking kernel's arguments (list
+    address, length, step stamp) are rewritten before every replay with
+    hipGraphExecKernelNodeSetParams.  The unlabeled list shrinks every step
+    (stale stamps of earlier steps must not count) and the selections equal
+    the oracle's."""
     from dal import engine
     from dal.forest import Forest
 
-    monkeypatch.setenv("DAL_PLAN_SETPARAMS", setparams)
     X, _, E, unl = _case(30_000, 64, seed=17)
     st = engine.PoolState(X, excluded=E, device=cuda)
     F = Forest.synthetic(10, 4, 64, seed=31)

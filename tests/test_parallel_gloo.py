@@ -1,5 +1,5 @@
-"""Multi-process orchestration of dal.parallel over gloo (CPU, world_size 2
-and 3).  The two exchanges (all-gather of normalised shards + canonical column
+"""Multi-process orchestration of dal.parallel over gloo (CPU, world_size 2,
+3, 4 and 8).  The two exchanges (all-gather of normalised shards + canonical column
 sum partials, all-gather of local top-k) and the deterministic merge are the
 product code; the per-shard arithmetic (HIP on the GPU) is replaced here by the
 oracle, so the test covers sharding, collectives and merge order on CPU."""
@@ -16,7 +16,7 @@ from dal import parallel
 from dal.luts import lut
 from oracle import dal_oracle as O
 
-N, D, K = 2600, 12, 40
+N, D, K = 2600, 12, 50
 
 
 def _free_port():
@@ -62,7 +62,16 @@ class OracleShard(parallel.ShardedSelector):
         return torch.as_tensor(np.asarray(unl), dtype=torch.int64)
 
     def status_word(self):
+        # a forced re-rank capacity overflow on one rank's first attempt: every
+        # rank must see it (OR of the gathered words) and redo the step
+        if getattr(self, "overflow_once", False) and not getattr(self, "retries", 0):
+            from dal import _lib
+
+            return torch.full((1,), _lib.DAL_FLAG_CAND_OVERFLOW, dtype=torch.int32)
         return torch.zeros(1, dtype=torch.int32)
+
+    def prepare_retry(self, sample_miss=False):
+        self.retries = getattr(self, "retries", 0) + 1
 
     def local_select(self, u_full, parts_full, unl, forest, k, mode="dw", strategy="least_confidence",
                      beta=1.0, density_mode="gram"):
@@ -107,50 +116,65 @@ def _cpu_sort_positions(keys, pos, k):
     return torch.from_numpy(order.astype(np.int64))
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, case="all"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        _run(rank, world, q)
+        _run(rank, world, q, case)
     except Exception as e:  # surface worker failures instead of a queue timeout
-        q.put((rank, repr(e), None))
+        q.put((rank, repr(e), None, None))
         raise
     finally:
         dist.destroy_process_group()
 
 
-def _run(rank, world, q):
-    if True:
-        X = O.synthetic_pool(N, D, seed=4)
-        of = O.synthetic_forest(10, 4, D, seed=1)
-        E = np.arange(10)
-        unl = np.arange(10, N)
-        sel = OracleShard(X, N, rank, world, E, of)
-        idx, sc = parallel.select(sel, parallel.TorchComm(), unl, None, K, mode="dw",
-                                  sort_fn=_cpu_sort_positions)
-        q.put((rank, idx.numpy(), sc.numpy()))
+def _unlabeled(case):
+    """The unlabeled set of a case: every row outside L0, or with holes --
+    all of rows [512, 1024) labeled (at world >= 4 one rank has no unlabeled
+    row at all) and a scatter of labeled rows elsewhere."""
+    unl = np.arange(10, N)
+    if case != "all":
+        unl = unl[(unl < 512) | (unl >= 1024)]
+        unl = unl[unl % 7 != 3]
+    return unl
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_sharded_density_select_matches_oracle(world):
+def _run(rank, world, q, case):
+    X = O.synthetic_pool(N, D, seed=4)
+    of = O.synthetic_forest(10, 4, D, seed=1)
+    E = np.arange(10)
+    sel = OracleShard(X, N, rank, world, E, of)
+    sel.overflow_once = case == "retry" and rank == world - 2
+    idx, sc = parallel.select(sel, parallel.TorchComm(), _unlabeled(case), None, K, mode="dw",
+                              sort_fn=_cpu_sort_positions)
+    q.put((rank, idx.numpy(), sc.numpy(), getattr(sel, "retries", 0)))
+
+
+@pytest.mark.parametrize("world,case", [(2, "all"), (3, "all"), (4, "holes"), (8, "holes"), (8, "retry")])
+def test_gloo_sharded_density_select_matches_oracle(world, case):
+    """World 4 / 8 shards are uneven (N = 2600: 512-row shards, the last
+    non-empty one holds 40 rows -- fewer than k -- and at world 8 two ranks
+    hold none); "holes": one rank's rows are all labeled; "retry": one rank
+    reports a re-rank capacity overflow and every rank redoes the step."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, case)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in range(world)]
+    res = [q.get(timeout=180) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     X = O.synthetic_pool(N, D, seed=4)
     of = O.synthetic_forest(10, 4, D, seed=1)
-    _, ref_idx, ref_sc = O.density_select(X, np.arange(10, N), of, K, 1.0, np.arange(10))
-    for rank, idx, sc in res:
+    _, ref_idx, ref_sc = O.density_select(X, _unlabeled(case), of, K, 1.0, np.arange(10))
+    for rank, idx, sc, retries in res:
         assert not isinstance(idx, str), idx
         assert np.array_equal(idx, ref_idx), rank
         assert np.array_equal(sc, ref_sc), rank
+        assert retries == (1 if case == "retry" else 0), (rank, retries)
 
 
 def test_shard_ranges_cover_pool():
