@@ -677,7 +677,10 @@ inline int64_t pairs_skip(int64_t P, int64_t a, int64_t b, int64_t skip_lo, int6
 // balance found (exact pair counts; cached per shape).  More chunks = a
 // smaller column working set swept by every block together (MALL hits; 2M x
 // 256: 16 chunks 3.9 % faster than 1), fewer = fewer A loads and row flushes.
-constexpr int64_t kMinChunks = 16;
+#ifndef DAL_GRAM_MIN_CHUNKS
+#define DAL_GRAM_MIN_CHUNKS 16
+#endif
+constexpr int64_t kMinChunks = DAL_GRAM_MIN_CHUNKS;
 int64_t choose_chunks(int64_t srow0, int64_t n_srb, int64_t lo, int64_t hi, int64_t skip_lo, int64_t skip_hi,
                       int64_t ns_active, int64_t G0) {
   struct Entry {
@@ -697,7 +700,8 @@ int64_t choose_chunks(int64_t srow0, int64_t n_srb, int64_t lo, int64_t hi, int6
   std::vector<int64_t> load;
   std::vector<std::pair<int64_t, int64_t>> cand;
   int tried = 0;
-  for (int64_t c = 1; c <= nj && tried < 32; ++c) {
+  // chunk counts from 1 up (from kMinChunks when it is above 16 and the columns allow)
+  for (int64_t c = kMinChunks > 16 && nj >= kMinChunks ? kMinChunks : 1; c <= nj && tried < 32; ++c) {
     const int64_t cbk = ceil_div(nj, c), ncc = ceil_div(nj, cbk);
     if (c > 1 && cbk == ceil_div(nj, c - 1)) continue;
     ++tried;
