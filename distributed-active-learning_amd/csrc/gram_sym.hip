@@ -55,9 +55,18 @@ namespace {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 #define AS3 __attribute__((address_space(3)))
 
-constexpr int kThreads = 256;  // 4 waves
+// Timing-only ablation builds (scripts/ab_build.sh -DDAL_GRAM_ABLATE=mask;
+// the results are wrong): 1 no column-sum epilogue, 2 no row fold, 4 no
+// per-stage barrier, 8 no B-stage DMA after the first, 16 no flushes, 32 every
+// DMA from the first column block (constant data, L2 hits), 64 DMA from 8
+// column blocks in turn (varying data, L2 hits).  0 in the product.
+#ifndef DAL_GRAM_ABLATE
+#define DAL_GRAM_ABLATE 0
+#endif
+constexpr int kAbl = DAL_GRAM_ABLATE;
 constexpr int kSB = 512;       // super block rows
 
 __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
@@ -105,8 +114,11 @@ __device__ __forceinline__ unsigned fresh_lane() {
   return v;
 }
 
-template <int KS>
+template <int KS, int W = 4>
 struct Cfg {
+  static constexpr int WAVES = W;                   // 4: one super block per block; 8: two (P, P + 2)
+  static constexpr int HALVES = W / 4;              // super blocks per block
+  static constexpr int NT = 64 * W;                 // threads
   static constexpr int ROWB = KS * 4;               // bytes per operand row of a slice (H + L)
   static constexpr int SLOTS = ROWB / 16;           // 16-B slots per row
   static constexpr int HI = KS / 8;                 // slots of the H part
@@ -117,7 +129,7 @@ struct Cfg {
   static constexpr int SPF = FOLD / SC;             // stages per fold group
   static constexpr int F4 = STAGE / 16;
   static constexpr int SWZ = (SLOTS < 16 ? SLOTS : 16) - 1;
-  static constexpr int PIECES = STAGE / (4 * 1024);  // 1-KiB DMA pieces per wave per stage
+  static constexpr int PIECES = STAGE / (W * 1024);  // 1-KiB DMA pieces per wave per stage
   static constexpr int RT = 8;                      // 16-row tiles per wave (128 rows)
   static constexpr int LG = 4;
   static constexpr int NKS = KS / 32;               // k-steps of v_mfma_f32_16x16x32_f16
@@ -125,20 +137,22 @@ struct Cfg {
   static constexpr bool SIG = KS == 32;             // column sums from sigma_P MFMAs
   static constexpr int NCH = SIG ? 1 : 2;           // row-sum chains per row tile
   static_assert(SPF >= 1 && SPP % SPF == 0 && PIECES >= 1 && NKS >= 1, "bad slice");
+  static_assert(W == 4 || (W == 8 && !SIG), "two super blocks per block: KS >= 64 only");
 };
 
-template <int KS>
-__global__ __launch_bounds__(kThreads, 2) void gram_csym_kernel(
+template <int KS, int W>
+__global__ __launch_bounds__(64 * W, 8 / W) void gram_csym_kernel(
     const uint16_t* __restrict__ urows, int srow0, int n_srb,
     const uint16_t* __restrict__ ucols, int jcol0, int j_lo, int j_hi, int skip_lo, int skip_hi,
     int ns_active, int64_t ldh, int slice_off, int chunk_j, int n_chunks,
     unsigned long long* __restrict__ acc_out, int contig) {
-  using C = Cfg<KS>;
+  using C = Cfg<KS, W>;
   constexpr bool SIG = C::SIG;
   constexpr int NCH = C::NCH;
+  constexpr int HV = C::HALVES;
   __shared__ __attribute__((aligned(16))) float4 lds[2 * C::F4];
   __shared__ double colacc[2][256];
-  __shared__ double rowacc[kSB];
+  __shared__ double rowacc[HV * kSB];
   // sigma_P (KS 32): per-wave partial sums of the H rows, then the sum split in
   // two fp16 terms (at 2^-6 of the operand's scale), read as an A fragment
   __shared__ float sig_part[SIG ? 4 : 1][SIG ? KS : 1];
@@ -146,32 +160,47 @@ __global__ __launch_bounds__(kThreads, 2) void gram_csym_kernel(
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int half = wave >> 2, wave4 = wave & 3;  // the block's super block of this wave, wave within it
   const int li = lane & 15, lq = lane >> 4;
   const int G = gridDim.x, g = blockIdx.x;
-  colacc[0][tid] = 0.0;
-  colacc[1][tid] = 0.0;
-  rowacc[tid] = 0.0;
-  rowacc[tid + 256] = 0.0;
+  if constexpr (HV == 1) {
+    colacc[0][tid] = 0.0;
+    colacc[1][tid] = 0.0;
+    rowacc[tid] = 0.0;
+    rowacc[tid + 256] = 0.0;
+  } else {
+    if (tid < 256) {
+      colacc[0][tid] = 0.0;
+      colacc[1][tid] = 0.0;
+    }
+    for (int e = tid; e < HV * kSB; e += C::NT) rowacc[e] = 0.0;
+  }
 
   // Work = the pairs (P, J) over row super blocks P and 256-column blocks J in
-  // [j_lo, j_hi) minus [skip_lo, skip_hi), as segments (P, raw column range
-  // [rlo, rhi)) walked by a raw column cursor r (J = jmap(r)):
-  //  contig: block g owns the g-th 1/G of the P-major raw grid (P, r);
-  //  chunk:  unit u = (P = u % n_srb, column chunk u / n_srb), dealt round-robin
+  // [j_lo, j_hi) minus [skip_lo, skip_hi), as segments (row unit, raw column
+  // range [rlo, rhi)) walked by a raw column cursor r (J = jmap(r)).  A row
+  // unit is one super block (W = 4) or two of the same parity, P and P + 2
+  // (W = 8: they take the same column blocks but near the diagonal, so one
+  // B stage feeds both; a half whose super block does not take J idles):
+  //  contig: block g owns the g-th 1/G of the unit-major raw grid (W = 4 only);
+  //  chunk:  unit u = (row unit u % n_ru, column chunk u / n_ru), dealt round-robin
   //          (all blocks sweep the same column chunks together: L2 / MALL reuse).
+  const int n_ru = HV == 1 ? n_srb : 2 * ((n_srb + 3) / 4);
+  auto rowP = [&](int ru, int h) { return HV == 1 ? srow0 + ru : srow0 + 4 * (ru >> 1) + (ru & 1) + 2 * h; };
+  auto live = [&](int P) { return P < srow0 + n_srb && P < ns_active; };
   const int sk_lo = skip_lo > j_lo ? skip_lo : j_lo, sk_hi = skip_hi < j_hi ? skip_hi : j_hi;
   const int skl = contig && sk_hi > sk_lo ? sk_hi - sk_lo : 0;  // chunk mode skips through takes()
   const int nje = j_hi - j_lo - skl;
   const int nre0 = ns_active - srow0, nre = nre0 < n_srb ? (nre0 > 0 ? nre0 : 0) : n_srb;
   const int64_t raw = static_cast<int64_t>(nre) * nje;
   const int64_t ka = raw * g / G, kb = raw * (g + 1) / G;
-  const int n_seg = contig ? (kb > ka ? static_cast<int>((kb - 1) / nje - ka / nje) + 1 : 0) : n_srb * n_chunks;
+  const int n_seg = contig ? (kb > ka ? static_cast<int>((kb - 1) / nje - ka / nje) + 1 : 0) : n_ru * n_chunks;
   const int seg_step = contig ? 1 : G;
-  auto seg_P = [&](int u) { return contig ? srow0 + static_cast<int>(ka / nje) + u : srow0 + u % n_srb; };
-  auto seg_rlo = [&](int u) { return contig ? (u == 0 ? static_cast<int>(ka % nje) : 0) : (u / n_srb) * chunk_j; };
+  auto seg_ru = [&](int u) { return contig ? static_cast<int>(ka / nje) + u : u % n_ru; };
+  auto seg_rlo = [&](int u) { return contig ? (u == 0 ? static_cast<int>(ka % nje) : 0) : (u / n_ru) * chunk_j; };
   auto seg_rhi = [&](int u) {
     if (contig) return u == n_seg - 1 ? static_cast<int>((kb - 1) % nje) + 1 : nje;
-    const int e = (u / n_srb + 1) * chunk_j;
+    const int e = (u / n_ru + 1) * chunk_j;
     return e < nje ? e : nje;
   };
   auto jmap = [&](int r) { return j_lo + r + (j_lo + r >= sk_lo ? skl : 0); };
@@ -180,52 +209,75 @@ __global__ __launch_bounds__(kThreads, 2) void gram_csym_kernel(
     if (J >= skip_lo && J < skip_hi) return false;
     return Q == P || (Q > P && ((P + Q) & 1) == 0) || (Q < P && ((P + Q) & 1));
   };
-  auto first_r = [&](int P, int r, int rhi) -> int {
-    if (P >= ns_active) return -1;
-    while (r < rhi && !takes(P, jmap(r))) ++r;
+  // the unit's super block h takes J (and exists)
+  auto takes_h = [&](int ru, int h, int J) { return live(rowP(ru, h)) && takes(rowP(ru, h), J); };
+  auto takes_u = [&](int ru, int J) { return takes_h(ru, 0, J) || (HV == 2 && takes_h(ru, HV - 1, J)); };
+  auto first_r = [&](int ru, int r, int rhi) -> int {
+    if constexpr (HV == 1) {
+      const int P = srow0 + ru;
+      if (P >= ns_active) return -1;
+      while (r < rhi && !takes(P, jmap(r))) ++r;
+    } else {
+      if (!live(rowP(ru, 0))) return -1;
+      while (r < rhi && !takes_u(ru, jmap(r))) ++r;
+    }
     return r < rhi ? r : -1;
   };
   auto seek = [&](int u, int& r) {
     while (u < n_seg) {
-      r = first_r(seg_P(u), seg_rlo(u), seg_rhi(u));
+      r = first_r(seg_ru(u), seg_rlo(u), seg_rhi(u));
       if (r >= 0) break;
       u += seg_step;
     }
     return u;
   };
 
-  auto voff = [&](int q) {
-    const int p = (wave * C::PIECES + q) * 64 + static_cast<int>(fresh_lane());
-    const int row = p / C::SLOTS;
-    const int slot = (p % C::SLOTS) ^ (row & C::SWZ);
-    return static_cast<unsigned>(row * ldh * 2 + slot * 16);
-  };
+  // DMA source offsets.  Piece q of wave w covers stage rows
+  // Wr + q * RPP + lane / SLOTS (Wr = w * PIECES * RPP, RPP = 64 / SLOTS rows
+  // per piece), slot (lane % SLOTS) ^ (row & SWZ).  Wr (a multiple of
+  // PIECES * RPP), q * RPP and lane / SLOTS occupy disjoint bits, so row & SWZ
+  // = ((Wr + lane / SLOTS) & SWZ) ^ ((q * RPP) & SWZ): the offset is a per-lane
+  // value XOR a per-piece constant (bits 4.. of the byte offset, below the row
+  // part) plus the piece's row offset.
+  constexpr int RPP = 64 / C::SLOTS;
+  const unsigned rowbytes = static_cast<unsigned>(ldh * 2);
   const unsigned dst0 = __builtin_amdgcn_readfirstlane(
       static_cast<unsigned>(reinterpret_cast<uintptr_t>((AS3 float4*)(lds + wave * C::PIECES * 64))));
   // stage h of 256-column block J into LDS buffer buf.  Inline asm so the
   // compiler does not track the DMA on vmcnt (block_sync waits for it).
   auto issue = [&](int buf, int J, int h) {
-    const uint16_t* sbase = ucols + (static_cast<int64_t>(J - jcol0) * 256 + h * C::SC) * ldh + slice_off;
+    if constexpr ((kAbl & 32) != 0) J = j_lo, h = 0;
+    if constexpr ((kAbl & 64) != 0) J = j_lo + (J & 7), h = 0;
+    const char* sbase = reinterpret_cast<const char*>(
+        ucols + (static_cast<int64_t>(J - jcol0) * 256 + h * C::SC) * ldh + slice_off);
+    const unsigned fl = fresh_lane();
+    const unsigned lrow = fl / C::SLOTS + static_cast<unsigned>(wave * C::PIECES * RPP);
+    const unsigned vlane = lrow * rowbytes + (((fl % C::SLOTS) ^ (lrow & C::SWZ)) << 4);
 #pragma unroll
     for (int q = 0; q < C::PIECES; ++q) {
       const unsigned dst = dst0 + static_cast<unsigned>(buf * C::STAGE + q * 1024);
+      const unsigned voff = (vlane ^ (static_cast<unsigned>((q * RPP) & C::SWZ) << 4)) +
+                            static_cast<unsigned>(q * RPP) * rowbytes;
       unsigned keep;
       asm volatile(
           "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
           "global_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %0"
           : "=&s"(keep)
-          : "v"(voff(q)), "s"(dst), "s"(sbase)
+          : "v"(voff), "s"(dst), "s"(sbase)
           : "memory");
     }
   };
 
-  // resident A fragments: H of rows P*512 + wave*128 + rt*16 + (lane & 15),
-  // features of k-step c and lane group lq
+  // resident A fragments: H of rows P*512 + wave4*128 + rt*16 + (lane & 15)
+  // (P = this wave's super block of the unit), features of k-step c and lane
+  // group lq
   f16x8 ah[C::RT][C::NKS];
-  auto load_a = [&](int P) {
+  auto load_a = [&](int ru) {
+    const int P = rowP(ru, half);
+    if (HV > 1 && !live(P)) return;  // (this half idles for the unit)
     const uint16_t* pb = urows + static_cast<int64_t>(P - srow0) * kSB * ldh + slice_off;
     const unsigned fl = fresh_lane();
-    const unsigned lrow = static_cast<unsigned>((wave * 128 + (fl & 15)) * ldh + (fl >> 4) * 8);
+    const unsigned lrow = static_cast<unsigned>((wave4 * 128 + (fl & 15)) * ldh + (fl >> 4) * 8);
     const unsigned tstep = static_cast<unsigned>(16 * ldh);
 #pragma unroll
     for (int rt = 0; rt < C::RT; ++rt)
@@ -321,19 +373,18 @@ __global__ __launch_bounds__(kThreads, 2) void gram_csym_kernel(
         if (sig && lq == 0)
           colacc[cbuf][col0 + ct * 16 + li] = static_cast<double>(__builtin_rintf(sg[0] * cmul * 64.0f));
       }
-      if (!SIG && ct > 0) {
+      if (!SIG && ct > 0 && !(kAbl & 1)) {
         // tile ct-1's column sums: growth of its chain's lane total
+        // (even, odd) register sums as one packed pair: v_pk_add_f32, the
+        // same two sequential chains as separate adds, half the instructions
         const int ch = (ct - 1) & 1;
-        float t0 = mc[ch % NCH][0][0], t1 = mc[ch % NCH][0][1];
+        f32x2 t = mc[ch % NCH][0].xy;
 #pragma unroll
         for (int rt = 0; rt < C::RT; ++rt) {
-#pragma unroll
-          for (int r = rt == 0 ? 2 : 0; r < 4; r += 2) {
-            t0 += mc[ch % NCH][rt][r];
-            t1 += mc[ch % NCH][rt][r + 1];
-          }
+          if (rt > 0) t += mc[ch % NCH][rt].xy;
+          t += mc[ch % NCH][rt].zw;
         }
-        const float T = t0 + t1;
+        const float T = t.x + t.y;
         const float cp = (fresh_stage && ct - 1 < 2) ? T : T - tprev[ch];
         tprev[ch] = T;
         atomicAdd(&colacc[cbuf][col0 + (ct - 1) * 16 + li], static_cast<double>(__builtin_rintf(cp * cmul)));
@@ -357,6 +408,13 @@ __global__ __launch_bounds__(kThreads, 2) void gram_csym_kernel(
   // reduce-scatter over the 16 column lanes leaves each lane 2 fully summed
   // rows, added by all 64 lanes at distinct LDS addresses.
   auto fold_rows = [&]() {
+    if constexpr ((kAbl & 2) != 0) {  // keep the chains live (their MFMAs stay)
+#pragma unroll
+      for (int rt = 0; rt < C::RT; ++rt)
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) asm volatile("" ::"v"(mc[ch][rt]));
+      return;
+    }
     float v[32];
 #pragma unroll
     for (int rt = 0; rt < C::RT; ++rt)
@@ -372,14 +430,25 @@ __global__ __launch_bounds__(kThreads, 2) void gram_csym_kernel(
     atomicAdd(&rowacc[row + 1], static_cast<double>(__builtin_rintf(v[1] * kFold)));
   };
   auto flush_one = [&](double& slot, int64_t out_row) {
+    if constexpr ((kAbl & 16) != 0) return;
     const double v = slot;
     if (v != 0.0) atomicAdd(acc_out + out_row, static_cast<unsigned long long>(static_cast<long long>(v)));
     slot = 0.0;
   };
-  auto flush_cols = [&](int cbuf, int Jf) { flush_one(colacc[cbuf][tid], static_cast<int64_t>(Jf) * 256 + tid); };
-  auto flush_rows = [&](int Pf) {
-    flush_one(rowacc[tid], static_cast<int64_t>(Pf) * kSB + tid);
-    flush_one(rowacc[tid + 256], static_cast<int64_t>(Pf) * kSB + tid + 256);
+  auto flush_cols = [&](int cbuf, int Jf) {
+    if (tid < 256) flush_one(colacc[cbuf][tid], static_cast<int64_t>(Jf) * 256 + tid);
+  };
+  auto flush_rows = [&](int ru) {  // rowacc[h * 512 + r] -> row r of the unit's super block h
+    if constexpr (HV == 1) {
+      const int P = srow0 + ru;
+      flush_one(rowacc[tid], static_cast<int64_t>(P) * kSB + tid);
+      flush_one(rowacc[tid + 256], static_cast<int64_t>(P) * kSB + tid + 256);
+    } else {
+      for (int e = tid; e < HV * kSB; e += C::NT) {
+        const int P = rowP(ru, e / kSB);
+        if (live(P)) flush_one(rowacc[e], static_cast<int64_t>(P) * kSB + e % kSB);
+      }
+    }
   };
   // every barrier waits for this wave's LDS adds and DMA first (hipcc may
   // omit the lgkmcnt wait at a loop-top barrier after no-return LDS adds)
@@ -387,37 +456,50 @@ __global__ __launch_bounds__(kThreads, 2) void gram_csym_kernel(
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
   };
+  auto stage_sync = [&]() {
+    if constexpr ((kAbl & 4) != 0) return;
+    block_sync();
+  };
 
   int r = -1;
   int unit = seek(contig ? 0 : g, r);
   if (unit >= n_seg) return;
-  int P = seg_P(unit), rhi_u = seg_rhi(unit);
+  int ru = seg_ru(unit), rhi_u = seg_rhi(unit);
   int J = jmap(r);
   issue(0, J, 0);
-  load_a(P);
+  load_a(ru);
   bool sig_fresh = true;
-  int cb = 0;       // colacc buffer of the current pair
-  int buf = 0;      // LDS stage buffer of the next stage to compute
-  int flushJ = -1;  // column block whose sums wait in colacc[cb ^ 1]
-  int flushP = -1;  // row super block whose sums wait in rowacc
+  int cb = 0;        // colacc buffer of the current pair
+  int buf = 0;       // LDS stage buffer of the next stage to compute
+  int flushJ = -1;   // column block whose sums wait in colacc[cb ^ 1]
+  int flushRU = -1;  // row unit whose sums wait in rowacc
 
   while (true) {
-    int nr = first_r(P, r + 1, rhi_u), n_unit = unit;
+    int nr = first_r(ru, r + 1, rhi_u), n_unit = unit;
     if (nr < 0) n_unit = seek(unit + seg_step, nr);
     const bool has_next = n_unit < n_seg;
-    const int nP = has_next ? seg_P(n_unit) : -1;
-    const bool new_rows = nP != P;
+    const int nru = has_next ? seg_ru(n_unit) : -1;
+    const bool new_rows = nru != ru;
     const int nJ = has_next ? jmap(nr) : -1;
-    const bool diag = (J >> 1) == P;
-    const float cmul = diag ? 0.0f : kFold;  // diagonal super block: row sums only
+    // this wave's super block: takes J?  diagonal (row sums only)?  The
+    // column block gets column sums when any half takes it off the diagonal.
+    const int Pw = rowP(ru, half);
+    const bool act = HV == 1 || takes_h(ru, half, J);
+    const float cmul = (J >> 1) == Pw ? 0.0f : kFold;
+    bool colsums = (J >> 1) != Pw;  // (W = 4: every visited J is taken)
+    if constexpr (HV > 1) {
+      colsums = false;
+#pragma unroll
+      for (int h = 0; h < HV; ++h) colsums |= takes_h(ru, h, J) && (J >> 1) != rowP(ru, h);
+    }
 
 #pragma unroll
     for (int s = 0; s < C::SPP; ++s) {
-      block_sync();
+      stage_sync();
       if (s == 0) {
         if (flushJ >= 0) flush_cols(cb ^ 1, flushJ);
-        if (flushP >= 0) flush_rows(flushP);
-        flushP = -1;
+        if (flushRU >= 0) flush_rows(flushRU);
+        flushRU = -1;
         if (SIG && sig_fresh) {
           build_sigma();
           block_sync();
@@ -430,24 +512,28 @@ __global__ __launch_bounds__(kThreads, 2) void gram_csym_kernel(
           }
         }
       }
-      if (s + 1 < C::SPP)
+      if ((kAbl & 8) != 0) {
+      } else if (s + 1 < C::SPP) {
         issue(buf ^ 1, J, s + 1);
-      else if (has_next)
+      } else if (has_next) {
         issue(buf ^ 1, nJ, 0);
-      compute(buf, cmul, cb, s * C::SC, s % C::SPF == 0);
-      if (s % C::SPF == C::SPF - 1) fold_rows();
+      }
+      if (act) {  // (wave-uniform: a half whose super block does not take J idles)
+        compute(buf, cmul, cb, s * C::SC, s % C::SPF == 0);
+        if (s % C::SPF == C::SPF - 1) fold_rows();
+      }
       buf ^= 1;
     }
 
-    flushJ = diag ? -1 : J;
+    flushJ = colsums ? J : -1;
     cb ^= 1;
-    if (new_rows) flushP = P;
+    if (new_rows) flushRU = ru;
     if (!has_next) break;
     unit = n_unit;
     rhi_u = seg_rhi(unit);
     if (new_rows) {
-      P = nP;
-      load_a(P);
+      ru = nru;
+      load_a(ru);
       sig_fresh = true;
     }
     r = nr;
@@ -455,7 +541,7 @@ __global__ __launch_bounds__(kThreads, 2) void gram_csym_kernel(
   }
   block_sync();
   if (flushJ >= 0) flush_cols(cb ^ 1, flushJ);
-  if (flushP >= 0) flush_rows(flushP);
+  if (flushRU >= 0) flush_rows(flushRU);
 }
 
 // ---------------------------------------------------------------------------
@@ -681,20 +767,25 @@ inline int64_t pairs_skip(int64_t P, int64_t a, int64_t b, int64_t skip_lo, int6
 #define DAL_GRAM_MIN_CHUNKS 16
 #endif
 constexpr int64_t kMinChunks = DAL_GRAM_MIN_CHUNKS;
+// hv = super blocks per row unit (gram_csym_kernel W / 4); a two-super-block
+// unit costs the pairs of the busier one (they take the same column blocks but
+// near the diagonal).
 int64_t choose_chunks(int64_t srow0, int64_t n_srb, int64_t lo, int64_t hi, int64_t skip_lo, int64_t skip_hi,
-                      int64_t ns_active, int64_t G0) {
+                      int64_t ns_active, int64_t G0, int hv) {
   struct Entry {
-    int64_t k[8];
+    int64_t k[9];
     int64_t nc;
   };
   static thread_local Entry cache[8] = {};
   static thread_local int cache_next = 0;
-  const int64_t key[8] = {srow0, n_srb, lo, hi, skip_lo, skip_hi, ns_active, G0};
+  const int64_t key[9] = {srow0, n_srb, lo, hi, skip_lo, skip_hi, ns_active, G0, hv};
   for (const Entry& e : cache) {
     bool hit = e.nc > 0;
-    for (int i = 0; i < 8 && hit; ++i) hit = e.k[i] == key[i];
+    for (int i = 0; i < 9 && hit; ++i) hit = e.k[i] == key[i];
     if (hit) return e.nc;
   }
+  const int64_t n_ru = hv == 1 ? n_srb : 2 * ceil_div(n_srb, 4);
+  auto rowP = [&](int64_t ru, int h) { return hv == 1 ? srow0 + ru : srow0 + 4 * (ru >> 1) + (ru & 1) + 2 * h; };
   const int64_t nj = hi - lo;
   int64_t best_max = -1;
   std::vector<int64_t> load;
@@ -705,13 +796,18 @@ int64_t choose_chunks(int64_t srow0, int64_t n_srb, int64_t lo, int64_t hi, int6
     const int64_t cbk = ceil_div(nj, c), ncc = ceil_div(nj, cbk);
     if (c > 1 && cbk == ceil_div(nj, c - 1)) continue;
     ++tried;
-    const int64_t units = n_srb * ncc, G = units < G0 ? units : G0;
+    const int64_t units = n_ru * ncc, G = units < G0 ? units : G0;
     load.assign(static_cast<size_t>(G), 0);
     for (int64_t u = 0; u < units; ++u) {
-      const int64_t P = srow0 + u % n_srb;
-      if (P >= ns_active) continue;
-      const int64_t clo = lo + (u / n_srb) * cbk, chi = clo + cbk < hi ? clo + cbk : hi;
-      load[static_cast<size_t>(u % G)] += pairs_skip(P, clo, chi, skip_lo, skip_hi);
+      const int64_t clo = lo + (u / n_ru) * cbk, chi = clo + cbk < hi ? clo + cbk : hi;
+      int64_t w = 0;
+      for (int h = 0; h < hv; ++h) {
+        const int64_t P = rowP(u % n_ru, h);
+        if (P >= ns_active || P >= srow0 + n_srb) continue;
+        const int64_t pw = pairs_skip(P, clo, chi, skip_lo, skip_hi);
+        w = pw > w ? pw : w;
+      }
+      load[static_cast<size_t>(u % G)] += w;
     }
     int64_t mx = 0;
     for (int64_t v : load) mx = v > mx ? v : mx;
@@ -728,22 +824,25 @@ int64_t choose_chunks(int64_t srow0, int64_t n_srb, int64_t lo, int64_t hi, int6
   if (best_nc < 0) best_nc = cand.back().first;
   Entry& e = cache[cache_next];
   cache_next = (cache_next + 1) % 8;
-  for (int i = 0; i < 8; ++i) e.k[i] = key[i];
+  for (int i = 0; i < 9; ++i) e.k[i] = key[i];
   e.nc = best_nc;
   return best_nc;
 }
 
-template <int KS>
-int launch_csym(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint16_t* cols, int64_t jcol0,
-                int64_t j_lo, int64_t j_hi, int64_t skip_lo, int64_t skip_hi, int64_t ns_active, int64_t ldh,
-                int slice_off, int64_t* acc, int grid_blocks, hipStream_t stream) {
-  const int G0 = grid_blocks > 0 ? grid_blocks : 2 * device_cus();
+// Two super blocks per block (8 waves, one block per CU: each B stage feeds
+// 1,024 rows, half the L2 -> LDS bytes per flop of the 4-wave form) for the
+// round-robin schedule at KS 128.
+#ifndef DAL_GRAM_WAVES8
+#define DAL_GRAM_WAVES8 1
+#endif
+
+template <int KS, int W>
+int launch_csym_w(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint16_t* cols, int64_t jcol0,
+                  int64_t j_lo, int64_t j_hi, int64_t skip_lo, int64_t skip_hi, int64_t ns_active, int64_t ldh,
+                  int slice_off, int64_t* acc, int grid_blocks, int contig, hipStream_t stream) {
+  // grid_blocks counts 4-wave blocks (two per CU); 8-wave blocks are one per CU
+  const int G0 = (grid_blocks > 0 ? grid_blocks : 2 * device_cus()) * 4 / W;
   const int64_t nj = j_hi - j_lo;
-  // contiguous equal shares of the pair grid per block for a small column
-  // operand (<= 32 MB: 100k x 64 is 2-5 % faster), else round-robin column
-  // chunks whose blocks sweep the same column stages together.  Exact integer
-  // accumulation: the schedule never changes the bits.
-  const int contig = nj * 256 * ldh * 2 <= (int64_t{32} << 20);
   int64_t cbk = nj, n_chunks = 1, G;
   if (contig) {
     const int64_t sl = skip_lo > j_lo ? skip_lo : j_lo, sh = skip_hi < j_hi ? skip_hi : j_hi;
@@ -752,19 +851,36 @@ int launch_csym(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint16
     if (raw <= 0) return DAL_OK;
     G = raw < G0 ? raw : G0;
   } else {
-    const int64_t nc = choose_chunks(srow0, n_srb, j_lo, j_hi, skip_lo, skip_hi, ns_active, G0);
+    const int64_t nc = choose_chunks(srow0, n_srb, j_lo, j_hi, skip_lo, skip_hi, ns_active, G0, W / 4);
     cbk = ceil_div(nj, nc);
     n_chunks = ceil_div(nj, cbk);
-    const int64_t n_units = n_srb * n_chunks;
+    const int64_t n_units = (W == 4 ? n_srb : 2 * ceil_div(n_srb, 4)) * n_chunks;
     G = n_units < G0 ? n_units : G0;
   }
-  hipLaunchKernelGGL((gram_csym_kernel<KS>), dim3(static_cast<unsigned>(G)), dim3(kThreads), 0, stream, rows,
+  hipLaunchKernelGGL((gram_csym_kernel<KS, W>), dim3(static_cast<unsigned>(G)), dim3(64 * W), 0, stream, rows,
                      static_cast<int>(srow0), static_cast<int>(n_srb), cols, static_cast<int>(jcol0),
                      static_cast<int>(j_lo), static_cast<int>(j_hi), static_cast<int>(skip_lo),
                      static_cast<int>(skip_hi), static_cast<int>(ns_active), ldh, slice_off, static_cast<int>(cbk),
                      static_cast<int>(n_chunks), reinterpret_cast<unsigned long long*>(acc), contig);
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
+}
+
+template <int KS>
+int launch_csym(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint16_t* cols, int64_t jcol0,
+                int64_t j_lo, int64_t j_hi, int64_t skip_lo, int64_t skip_hi, int64_t ns_active, int64_t ldh,
+                int slice_off, int64_t* acc, int grid_blocks, hipStream_t stream) {
+  // contiguous equal shares of the pair grid per block for a small column
+  // operand (<= 32 MB: 100k x 64 is 2-5 % faster), else round-robin column
+  // chunks whose blocks sweep the same column stages together.  Exact integer
+  // accumulation: the schedule never changes the bits.
+  const int contig = (j_hi - j_lo) * 256 * ldh * 2 <= (int64_t{32} << 20);
+  if constexpr (KS == 128 && DAL_GRAM_WAVES8)
+    if (!contig)
+      return launch_csym_w<KS, 8>(rows, srow0, n_srb, cols, jcol0, j_lo, j_hi, skip_lo, skip_hi, ns_active, ldh,
+                                  slice_off, acc, grid_blocks, contig, stream);
+  return launch_csym_w<KS, 4>(rows, srow0, n_srb, cols, jcol0, j_lo, j_hi, skip_lo, skip_hi, ns_active, ldh,
+                              slice_off, acc, grid_blocks, contig, stream);
 }
 
 struct ResidualLayout {

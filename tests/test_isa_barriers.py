@@ -84,7 +84,8 @@ def _check(body):
 def test_every_gram_barrier_waits_for_lds():
     funcs = _functions(_disassemble())
     grams = {k: v for k, v in funcs.items() if "gram_csym_kernel" in k}
-    assert len(grams) == 3, "gram_csym_kernel<32|64|128> not found in libdal.so"
+    # <KS, waves>: 32/64/128 with 4 waves, 128 with 8 (two super blocks per block)
+    assert len(grams) == 4, "gram_csym_kernel<32|64|128, 4> / <128, 8> not found in libdal.so"
     for name, body in grams.items():
         n, bad = _check(body)
         assert n > 0, name
