@@ -27,6 +27,7 @@
 namespace {
 
 inline bool is_space(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\v' || c == '\f'; }
+inline bool is_digit(char c) { return c >= '0' && c <= '9'; }
 
 // Start of the line containing position p (or p itself if it starts a line).
 size_t line_start(const char* t, size_t len, size_t p) {
@@ -71,38 +72,52 @@ locale_t c_numeric_locale() {
   return loc;
 }
 
-// Parse one field [a, b) as fp64 (the token must be consumed entirely).
-// Python's float() accepts decimal literals, inf/infinity/nan (any case, with
-// a sign); strtod also takes hex floats ("0x1p3") and "nan(chars)", which
-// float() rejects -- such tokens are rejected here too.
-bool parse_double(const char* t, size_t a, size_t b, double& v) {
-  char buf[128];
+// Copy token [a, b) into buf (NUL-terminated) without its PEP 515 digit-group
+// underscores, as Python's float() / int() read them ("1_000.5" = 1000.5):
+// an underscore must sit between two digits, anything else rejects the token.
+bool copy_token(const char* t, size_t a, size_t b, char* buf, size_t cap) {
   const size_t n = b - a;
-  if (n == 0 || n >= sizeof(buf)) return false;
+  if (n == 0 || n >= cap) return false;
+  size_t m = 0;
   for (size_t i = 0; i < n; ++i) {
     const char c = t[a + i];
-    if (c == 'x' || c == 'X' || c == '(') return false;
-    buf[i] = c;
+    if (c == '_') {
+      const bool ok = i > 0 && i + 1 < n && is_digit(t[a + i - 1]) && is_digit(t[a + i + 1]);
+      if (!ok) return false;
+      continue;
+    }
+    buf[m++] = c;
   }
-  buf[n] = 0;
+  buf[m] = 0;
+  return true;
+}
+
+// Parse one field [a, b) as fp64 (the token must be consumed entirely).
+// Python's float() accepts decimal literals with digit-group underscores,
+// inf/infinity/nan (any case, with a sign); strtod also takes hex floats
+// ("0x1p3") and "nan(chars)", which float() rejects -- such tokens are
+// rejected here too.  Fields are whitespace-delimited, so a token never
+// carries the surrounding whitespace float() would strip.
+bool parse_double(const char* t, size_t a, size_t b, double& v) {
+  char buf[128];
+  for (size_t i = a; i < b; ++i)
+    if (t[i] == 'x' || t[i] == 'X' || t[i] == '(') return false;
+  if (!copy_token(t, a, b, buf, sizeof(buf))) return false;
   const locale_t loc = c_numeric_locale();
   if (!loc) return false;
   char* end = nullptr;
   errno = 0;
   v = strtod_l(buf, &end, loc);
-  return end == buf + n;
+  return end != buf && *end == 0;
 }
 
 bool parse_int(const char* t, size_t a, size_t b, long long& v) {
   char buf[64];
-  const size_t n = b - a;
-  if (n == 0 || n >= sizeof(buf)) return false;
-  for (size_t i = 0; i < n; ++i) buf[i] = t[a + i];
-  buf[n] = 0;
+  if (!copy_token(t, a, b, buf, sizeof(buf))) return false;
   char* end = nullptr;
   errno = 0;
   v = std::strtoll(buf, &end, 10);
-  return end == buf + n && errno == 0;
+  return end != buf && *end == 0 && errno == 0;
 }
 
 // Parse the rows of [a, b) into x[row0..], labels[row0..]; stops after

@@ -123,9 +123,17 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
                      labeled_rows=None):
     """Select the k candidate rows least similar to the labeled set (smallest
     max-cosine, ties -> lower index), exact against the canonical fp64
-    max-cosine.  Returns Selection(scores = fp32 max-cos of the candidates
-    (within dal_maxcos_unit_error_bound of the canonical values),
+    max-cosine.  Returns Selection(scores = fp32 max-cos of the candidates,
     indices [k], selected_scores = canonical fp64 max-cos).
+
+    The fp32 values come from the folded-operand kernel (dal_max_cosine_unit,
+    within dal_maxcos_unit_error_bound(d) ~ 2^-11 of the canonical values, about
+    1000x the bf16 kernel's (3d + 6) 2^-24): the bound only widens the interval
+    keys, the selection stays exact through the fp64 re-rank.  When the
+    candidate list overflows on that bound (near-tied pools: duplicates,
+    clusters), the values are recomputed once with the tighter dal_max_cosine
+    (d = 64 / 128 / 256) before the capacity grows; ``scores`` then carry that
+    kernel's precision.
 
     For a row shard (multi-GPU) pass ``row_base`` (global index of row 0),
     global ``candidates`` and the labeled set as ``labeled_rows`` ([m, d],
@@ -151,6 +159,8 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
     # only widens the interval keys -- the fp64 re-rank keeps the selection exact
     _lib.call("dal_max_cosine_unit", _ptr(x), n, d, _ptr(lab.unit16), lab.m_pad, _ptr(mx), _ptr(status),
               _stream(dev))
+    bound = float(lib.dal_maxcos_unit_error_bound(d))
+    tight = d not in (64, 128, 256)  # the bf16 kernel's shapes; elsewhere the unit values are final
     in_range = None  # device count of the candidates inside this shard (read with the status)
     if candidates is None:
         flags = torch.full((n,), DAL_ROW_CANDIDATE, dtype=torch.uint8, device=dev)
@@ -173,8 +183,8 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
     kk = min(int(k), n_cand)
     lo = torch.empty(n, dtype=torch.int64, device=dev)
     hi = torch.empty(n, dtype=torch.int64, device=dev)
-    _lib.call("dal_interval_keys_f32", _ptr(mx), n, float(lib.dal_maxcos_unit_error_bound(d)), _ptr(flags),
-              DAL_ASCENDING, _ptr(lo), _ptr(hi), _stream(dev))
+    _lib.call("dal_interval_keys_f32", _ptr(mx), n, bound, _ptr(flags), DAL_ASCENDING, _ptr(lo), _ptr(hi),
+              _stream(dev))
     cap = candidate_cap(n, kk)
     passes = LEVEL1_PASSES if cap <= _lib.DAL_SORT_CAP_PAYLOAD else 0
     while True:
@@ -203,6 +213,17 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
             cap = candidate_cap(n, kk)
             passes = LEVEL1_PASSES if cap <= _lib.DAL_SORT_CAP_PAYLOAD else 0
             status.zero_()
+            continue
+        if not tight and st & (DAL_FLAG_SAMPLE_MISS | DAL_FLAG_CAND_OVERFLOW):
+            # too many rows within the folded kernel's bound of the boundary:
+            # the bf16 kernel's values (bound ~1000x tighter) and their keys
+            tight = True
+            status.zero_()
+            _lib.call("dal_max_cosine", _ptr(x), n, d, _ptr(lab.rows), lab.m_pad, _ptr(lab.inv), 0, _ptr(mx), 0,
+                      _ptr(status), _stream(dev))
+            bound = float(lib.dal_maxcos_error_bound(d))
+            _lib.call("dal_interval_keys_f32", _ptr(mx), n, bound, _ptr(flags), DAL_ASCENDING, _ptr(lo), _ptr(hi),
+                      _stream(dev))
             continue
         if st & DAL_FLAG_SAMPLE_MISS:  # the fast level 1 overflowed: exact level 1
             passes = 0

@@ -4,7 +4,7 @@ libdal.so: AB_BASE (default ab/k3_base/libdal.so) and the in-tree library,
 switched by rebinding dal._lib between calls.  Per shape: selections
 (indices + fp64 score bits) must be identical; then back-to-back calls
 between two HIP events, interleaved A/B, median of the rounds.
-usage: python scripts/k3_lib_ab.py [NxD[xT] ...]"""
+usage: python scripts/k3_lib_ab.py [NxD[xT][:kK] ...]"""
 import ctypes
 import os
 import statistics
@@ -34,7 +34,9 @@ def bind(path):
 libs = {"base": bind(os.environ.get("AB_BASE", os.path.join(REPO, "ab", "k3_base", "libdal.so"))),
         "new": bind(_lib.LIB_PATH)}
 dev = torch.device("cuda:0")
-for sh in sys.argv[1:] or ["100000x64", "2000000x256", "284807x30x100"]:
+for spec in sys.argv[1:] or ["100000x64", "2000000x256", "284807x30x100", "2000000x256:k1000"]:
+    sh, _, kk = spec.partition(":k")
+    K = int(kk) if kk else 100
     parts = [int(v) for v in sh.split("x")]
     n, d = parts[:2]
     trees = parts[2] if len(parts) > 2 else 10
@@ -52,7 +54,7 @@ for sh in sys.argv[1:] or ["100000x64", "2000000x256", "284807x30x100"]:
     res, t = {}, {"base": [], "new": []}
     for name in ("base", "new"):
         _lib._lib = libs[name]
-        idx, sc, _ = engine.dw_select_local(st, flags, votes, klo, khi, lut, 100, 1.0, cs)
+        idx, sc, _ = engine.dw_select_local(st, flags, votes, klo, khi, lut, K, 1.0, cs)
         res[name] = (idx.cpu().numpy(), sc.cpu().numpy())
     same = np.array_equal(res["base"][0], res["new"][0]) and np.array_equal(
         res["base"][1].view(np.int64), res["new"][1].view(np.int64))
@@ -62,11 +64,11 @@ for sh in sys.argv[1:] or ["100000x64", "2000000x256", "284807x30x100"]:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(20):
-                engine.dw_select_local(st, flags, votes, klo, khi, lut, 100, 1.0, cs, sync=False)
+                engine.dw_select_local(st, flags, votes, klo, khi, lut, K, 1.0, cs, sync=False)
             e1.record()
             torch.cuda.synchronize()
             t[name].append(e0.elapsed_time(e1) / 20 * 1000)
-    print(f"{n} x {d} x T{trees}: base {statistics.median(t['base']):.1f} us  new {statistics.median(t['new']):.1f} us"
+    print(f"{n} x {d} x T{trees} k={K}: base {statistics.median(t['base']):.1f} us  new {statistics.median(t['new']):.1f} us"
           f"  {'selection identical' if same else 'SELECTION DIFFERS'}", flush=True)
     _lib._lib = libs["new"]
     del st, x

@@ -88,12 +88,14 @@ def test_diversity_select_scale(cuda):
     assert np.array_equal(_np(sel.selected_scores), ref_sc)
 
 
-@pytest.mark.parametrize("case", ["bucket_overflow", "foreign_candidates"])
+@pytest.mark.parametrize("case", ["bucket_overflow", "foreign_candidates", "near_ties"])
 def test_diversity_select_fallbacks(cuda, case):
     """The fast level 1 overflowing its 4,096 slots (5,000 identical
-    least-similar rows: DAL_FLAG_SAMPLE_MISS, exact re-run), and candidate
-    lists holding indices outside the pool (filtered after the status read,
-    then re-selected with the true count)."""
+    least-similar rows: DAL_FLAG_SAMPLE_MISS, exact re-run), candidate lists
+    holding indices outside the pool (filtered after the status read, then
+    re-selected with the true count), and 5,000 distinct near-tied rows (max-cos
+    within ~1e-4 of each other: inside the folded kernel's 2^-11 bound, so the
+    values are recomputed with the tighter bf16 kernel)."""
     from dal import similarity as sim
 
     n, d, m, k = 12000, 64, 256, 100
@@ -104,6 +106,14 @@ def test_diversity_select_fallbacks(cuda, case):
         far = np.zeros(d, dtype=np.float32)
         far[0] = 1.0  # a corner of the positive orthant: every copy has the same, smallest max-cosine
         X[3000:8000] = O.bf16_round(far[None, :])
+    elif case == "near_ties":
+        rng = np.random.default_rng(5)
+        near = np.zeros((5000, d), dtype=np.float32)
+        near[:, 0] = 1.0
+        rows = np.arange(5000)
+        near[rows, rng.integers(1, d, 5000)] += rng.integers(1, 9, 5000) * 2.0 ** -10
+        near[rows, rng.integers(1, d, 5000)] += rng.integers(1, 9, 5000) * 2.0 ** -12
+        X[3000:8000] = O.bf16_round(near)
     else:
         cand = np.concatenate([cand, np.arange(n, n + 500)])  # not rows of this pool
     sel = sim.diversity_select(X, L, k, candidates=cand, device=cuda)

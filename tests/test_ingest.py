@@ -99,6 +99,26 @@ def test_parse_rejects_tokens_python_float_rejects(tmp_path):
     assert np.array_equal(got_y, ref_y)
 
 
+def test_parse_digit_group_underscores_like_python(tmp_path):
+    """PEP 515 underscores between digits parse as the reference's
+    astype(float) / int() read them; any other underscore rejects the token."""
+    from dal import _lib
+    from dal.ingest import parse_labeled_text
+
+    p = tmp_path / "us.txt"
+    p.write_text("1_000.5 2_5e1_0 1\n1e1_0 -0_5 1_0\n")
+    got_x, got_y = parse_labeled_text(str(p))
+    ref_x, ref_y = _ref_parse(str(p))
+    assert np.array_equal(got_x.view(np.int32), ref_x.view(np.int32))
+    assert np.array_equal(got_y, ref_y)
+    for tok in ("1__0", "_1", "1_", "1_.5", "1._5", "1_e5"):
+        with pytest.raises(ValueError):
+            float(tok)
+        p.write_text(f"1 {tok} 1\n")
+        with pytest.raises(_lib.DalError):
+            parse_labeled_text(str(p))
+
+
 def test_parse_ignores_process_numeric_locale(tmp_path):
     """Python float() ignores LC_NUMERIC; so does the native parser (a
     comma-decimal locale must not break '0.5')."""
