@@ -87,6 +87,10 @@ __device__ __forceinline__ void st_sc1(double* p, double v) {
   st_sc1(reinterpret_cast<long long*>(p), __double_as_longlong(v));
 }
 
+// summary_select_kernel's blocks, each owning a candidate region (<= 32 row
+// groups per block: the candidate scoring spreads over up to 128 CUs)
+constexpr int kMaxRegions = 128;
+
 struct TopkHdr {
   // fast level 1 (summary_select_kernel): candidate count, the blocks'
   // arrival counter and tau -- the words a fast-path call needs zero
@@ -99,7 +103,7 @@ struct TopkHdr {
   unsigned long long krem[kPasses + 1];
   uint32_t hist[kPasses][kBins];
   // fast level 1: candidates found by each summary_select block (its region)
-  unsigned int reg_count[32];
+  unsigned int reg_count[kMaxRegions];
 };
 
 struct TopkLayout {
@@ -772,6 +776,10 @@ struct SortTail {
   int64_t reg_stride = 0;
   const unsigned int* reg_count = nullptr;
   int64_t reg_uniform = 0;  // > 0: every region holds this many (no reg_count)
+  // > 0: a region holding at most this many entries is sorted by (key, index)
+  // (summary_select_kernel ranks its own candidates); when every region is,
+  // the tail merges them instead of sorting
+  int64_t sorted_max = 0;
   int32_t* status = nullptr;
   uint32_t* clear = nullptr;
   int64_t clear_words = 0;
@@ -836,6 +844,7 @@ struct RegionMap {
 
 constexpr int64_t kSelMin = 1024;    // below this the full bitonic is cheap
 constexpr int64_t kRankMax = 512;    // at most this many: rank selection, no sorting network
+
 constexpr int64_t kSelMaxK = 1536;   // k + kSelSmall must fit the sort arrays
 constexpr int kSelSmall = 512;
 
@@ -945,22 +954,47 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
   __shared__ int64_t* s_dest[2];
   const int tid = threadIdx.x;
   if (tid < 2) s_dest[tid] = load_out_slot(tail.out_slot, tid);  // host round trips, overlapping the sort
-  __shared__ unsigned int s_pre[33];
+  __shared__ unsigned int s_pre[kMaxRegions + 1];
+  __shared__ int s_runs_sorted, s_run_max;
   RegionMap M;
   int64_t m;
   if (tail.n_reg) {
-    if (tid < tail.n_reg)  // the counts' loads in parallel
-      s_pre[tid] = tail.reg_uniform ? static_cast<unsigned>(tail.reg_uniform) : ld_sc1(tail.reg_count + tid);
-    __syncthreads();
-    if (tid == 0) {
-      unsigned long long tot = 0;
-      for (int r = 0; r < tail.n_reg; ++r) {
-        const unsigned c = s_pre[r];
-        s_pre[r] = static_cast<unsigned>(tot);
-        tot += c < tail.reg_stride ? c : static_cast<unsigned>(tail.reg_stride);
-        if (c > tail.reg_stride) tot = ~0ull >> 1;  // a region over capacity: miss
+    if (tid < 64) {
+      // wave 0: the counts' loads in parallel, two regions per lane, and a
+      // shuffle scan of the clamped counts (one thread summing 128 regions
+      // serially cost ~4 us); a region over capacity makes the total a miss
+      // while the offsets stay monotonic (every gather below stays inside its
+      // region; the selection is then discarded by the host)
+      const int r = 2 * tid;
+      const unsigned long long stride = static_cast<unsigned long long>(tail.reg_stride);
+      unsigned long long c0 = 0, c1 = 0;
+      if (r < tail.n_reg) c0 = tail.reg_uniform ? tail.reg_uniform : ld_sc1(tail.reg_count + r);
+      if (r + 1 < tail.n_reg) c1 = tail.reg_uniform ? tail.reg_uniform : ld_sc1(tail.reg_count + r + 1);
+      const bool over = c0 > stride || c1 > stride;
+      const unsigned long long smax = static_cast<unsigned long long>(tail.sorted_max);
+      const bool unsorted = c0 > smax || c1 > smax;
+      c0 = c0 < stride ? c0 : stride;
+      c1 = c1 < stride ? c1 : stride;
+      unsigned long long x = c0 + c1;
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(x, o);
+        if (tid >= o) x += y;
       }
-      s_pre[tail.n_reg] = tot > 0xFFFFFFFFull ? 0xFFFFFFFFu : static_cast<unsigned>(tot);
+      const unsigned long long ex = x - c0 - c1;
+      if (r < tail.n_reg) s_pre[r] = static_cast<unsigned>(ex);
+      if (r + 1 < tail.n_reg) s_pre[r + 1] = static_cast<unsigned>(ex + c0);
+      const bool miss = __ballot(over) != 0 || x > 0xFFFFFFFFull;
+      const bool all_sorted = smax > 0 && __ballot(unsorted) == 0;
+      unsigned long long cm = c0 > c1 ? c0 : c1;  // the longest region
+      for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long y = __shfl_xor(cm, o);
+        cm = y > cm ? y : cm;
+      }
+      if (tid == 63) {
+        s_run_max = static_cast<int>(cm);
+        s_pre[tail.n_reg] = miss ? 0xFFFFFFFFu : static_cast<unsigned>(x);
+        s_runs_sorted = all_sorted && !miss;
+      }
     }
     __syncthreads();
     M = RegionMap{tail.n_reg, tail.reg_stride, s_pre};
@@ -976,6 +1010,147 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
   // below its bucket plus the bucket itself (<= kSelSmall) are sorted -- the
   // full bitonic over 4,096 keys is LDS-bound (~95 us).  Same result: every
   // key of the top k lies in the sorted subset.
+  // Sorted regions are merged when the rank selection is too long (m >
+  // kRankMax) and the radix pre-selection would not shorten the sort much
+  // (k + kSelSmall >= m: config 4 at k = 1,000, m = 1,261: bitonic 31 us,
+  // merge 19 us); short lists keep the rank selection (k = 100, m = 135: 5 us
+  // vs 8 us for the merge's seven levels) and long lists with a small k the
+  // pre-selection (config 3: m = 1,700, k = 100).
+  if constexpr (PAY) if (tail.n_reg > 1 && s_runs_sorted && static_cast<int64_t>(s_pre[tail.n_reg]) == m && m > kRankMax &&
+      (m <= kSelMin || k + kSelSmall >= m) && m <= CAP / 2) {  // (every run whole: no capacity clamp above)
+    // every region is a sorted run (summary_select_kernel ranked its own
+    // candidates): a tree of pairwise merges, ceil(log2 regions) levels --
+    // an entry's place in the merged pair is its offset in its own run plus
+    // the count below it in the partner run (a binary search; ties between
+    // runs, impossible for distinct indices, go to the left run).  The two
+    // halves of the arrays alternate as source and destination.  Measured at
+    // config 4, k = 1,000 (123 runs, m = 1,261): 19 us; 4- and 8-way groups
+    // with their searches advanced together (branch-free, every probe's reads
+    // issued at once) 41-45 us -- the probes' LDS reads, not their latency,
+    // bound it.
+    constexpr int H = CAP / 2;
+    static_assert(H <= 2 * kSortThreads, "two entries per thread");
+    __shared__ unsigned int s_bd2[kMaxRegions + 1];
+    __shared__ unsigned char s_rid[2][H];  // each entry's run at the current level (< kMaxRegions)
+    for (int i = tid; i < m; i += kSortThreads) {
+      const int64_t q = M(i);
+      sk[i] = ld_sc1(keys + q);
+      si[i] = ld_sc1(idx + q);
+      if (PAY) sp[i] = ld_sc1(pay + q);
+      s_rid[0][i] = static_cast<unsigned char>(q / tail.reg_stride);
+    }
+    __syncthreads();
+    if (tail.clear) {  // every thread read the header above
+      for (int64_t w = tid; w < tail.clear_words; w += kSortThreads) tail.clear[w] = 0u;
+      for (int64_t w = tid; w < tail.clear2_words; w += kSortThreads) tail.clear2[w] = 0u;
+    }
+    const int mm = static_cast<int>(m);
+    const unsigned int* bd = s_pre;
+    unsigned int* nbd = s_bd2;
+    int nr = tail.n_reg, src = 0, run_max = s_run_max;
+    while (nr > 1) {  // (block-uniform)
+      int steps = 0;  // probes that settle a search over any run of this level
+      while ((1 << steps) <= run_max) ++steps;
+      const unsigned long long* ks = sk + src * H;
+      const long long* is = si + src * H;
+      const double* ps = sp + (PAY ? src * H : 0);
+      unsigned long long* kd = sk + (src ^ 1) * H;
+      long long* id = si + (src ^ 1) * H;
+      double* pd = sp + (PAY ? (src ^ 1) * H : 0);
+      // a thread's two entries (tid, tid + 1024) searched together: their
+      // probes' reads in flight at once
+      int e[2], a[2], lo[2], hi[2], base[2], pos[2];
+      bool left[2];
+      unsigned long long ke[2];
+      long long ie[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        e[u] = tid + u * kSortThreads;
+        const bool live = e[u] < mm;
+        a[u] = live ? s_rid[src][e[u]] : 0;
+        ke[u] = live ? ks[e[u]] : 0ull;
+        ie[u] = live ? is[e[u]] : 0ll;
+        const int r0 = a[u] & ~1;
+        pos[u] = e[u];
+        lo[u] = hi[u] = base[u] = 0;
+        left[u] = a[u] == r0;
+        if (live && r0 + 1 < nr) {
+          const int lo0 = static_cast<int>(bd[r0]), mid0 = static_cast<int>(bd[r0 + 1]);
+          const int hi0 = static_cast<int>(bd[r0 + 2]);
+          lo[u] = base[u] = left[u] ? mid0 : lo0;  // the partner run
+          hi[u] = left[u] ? hi0 : mid0;
+          pos[u] = left[u] ? e[u] : lo0 + (e[u] - mid0);
+        }
+      }
+      for (int s = 0; s < steps; ++s) {
+        unsigned long long km[2];
+        int mid[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          mid[u] = lo[u] < hi[u] ? (lo[u] + hi[u]) >> 1 : 0;
+          km[u] = ks[mid[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const bool open = lo[u] < hi[u];
+          // the index only on equal keys (LDS bandwidth bounds the probes)
+          bool below = km[u] < ke[u];
+          if (km[u] == ke[u]) {
+            const long long im = is[mid[u]];
+            below = left[u] ? im < ie[u] : im <= ie[u];
+          }
+          lo[u] = open && below ? mid[u] + 1 : lo[u];
+          hi[u] = open && !below ? mid[u] : hi[u];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (e[u] < mm) {
+          const int p = pos[u] + (lo[u] - base[u]);
+          kd[p] = ke[u];
+          id[p] = ie[u];
+          if (PAY) pd[p] = ps[e[u]];
+          s_rid[src ^ 1][p] = static_cast<unsigned char>(a[u] >> 1);
+        }
+      }
+      const int nn = (nr + 1) >> 1;
+      for (int j = tid; j <= nn; j += kSortThreads) nbd[j] = j < nn ? bd[2 * j] : bd[nr];
+      __syncthreads();
+      const unsigned int* t0 = bd;
+      bd = nbd;
+      nbd = const_cast<unsigned int*>(t0);
+      nr = nn;
+      src ^= 1;
+      run_max = 2 * run_max < mm ? 2 * run_max : mm;
+    }
+    const unsigned long long* ks = sk + src * H;
+    const long long* is = si + src * H;
+    const double* ps = sp + (PAY ? src * H : 0);
+    int64_t* const di = s_dest[0];  // written before the first barrier
+    double* const ds = reinterpret_cast<double*>(s_dest[1]);
+    const int64_t kk = k < m ? k : m;
+    for (int i = tid; i < kk; i += kSortThreads) {
+      if (out_keys) out_keys[i] = ks[i];
+      out_idx[i] = is[i];
+      if (PAY && out_pay) out_pay[i] = ps[i];
+      if (di) di[i] = is[i];
+      if (PAY && ds) ds[i] = ps[i];
+    }
+    if (PAY && h) {
+      for (int64_t i = kk + tid; i < k; i += kSortThreads) {
+        if (out_keys) out_keys[i] = DAL_KEY_NONE;
+        out_idx[i] = -1;
+        if (out_pay) out_pay[i] = __builtin_nan("");
+        if (di) di[i] = -1;
+        if (ds) ds[i] = __builtin_nan("");
+      }
+    }
+    if (tail.status_mirror) {
+      __syncthreads();
+      if (tid == 0) publish_status(tail.status, tail.status_mirror);
+    }
+    return;
+  }
   if (m <= kRankMax) {
     // short lists (the common case: ~100-300 candidates): rank selection.
     // Every element's rank -- the count of smaller (key, index, position)
@@ -1322,11 +1497,25 @@ __global__ __launch_bounds__(256) void group_min_kernel(const uint64_t* __restri
 // owns groups [b * per, (b + 1) * per): those whose optimistic minimum is
 // <= tau are listed in LDS and scanned by the block's waves (a group's rows,
 // 8 x 64 keys in flight per wave); each 64-row slice with candidates reserves
-// its slots with one atomic.  DW: each candidate's canonical fp64 score is
-// computed in place (<= 2 per slice: the whole wave per candidate; more: one
-// lane each), and the block that arrives last sorts the candidates
-// (sort_tail_body: capacity check, selection, header clear).  !DW: indices
-// only (a separate re-rank follows).
+// its slots with one atomic.  DW: the candidates are listed in LDS, then
+// scored by all of the block's waves (canonical fp64: <= one per wave by the
+// whole wave, more by one lane each), and the block that arrives last sorts
+// the candidates (sort_tail_body: capacity check, selection, header clear).
+// !DW: indices only (a separate re-rank follows).
+// candidates per wave scored by whole waves (one after another) before the
+// lane form takes over: at d = 256 a whole-wave score costs ~4.4 us with four
+// waves per SIMD, a wave's lane pass ~17 us whatever it holds
+constexpr int kWaveScoreMax = 3;
+// a block whose list holds at most this many ranks them and writes its region
+// sorted (SortTail::sorted_max): the last block then merges instead of sorting
+constexpr int kLocalSort = 256;
+// features per load round of a lane-scored candidate (all of a round's loads
+// in flight before its divisions: 8 left a d = 256 row 32 dependent HBM round
+// trips, ~86 us for a block holding a few dozen candidates)
+#ifndef DAL_K3_LANE_CHUNK
+#define DAL_K3_LANE_CHUNK 64
+#endif
+
 template <bool DW>
 __global__ __launch_bounds__(kSumThreads) void summary_select_kernel(
     const uint64_t* __restrict__ keys_hi, int64_t n, int64_t k, int64_t idx_base, GroupSummary S,
@@ -1335,6 +1524,12 @@ __global__ __launch_bounds__(kSumThreads) void summary_select_kernel(
   constexpr int W = kSumThreads / 64;
   __shared__ int s_hits[kMaxGroups / 32];  // per <= 128 groups (summary_grid)
   __shared__ unsigned s_nh, s_nc, s_last;
+  // DW: the block's candidate rows, listed by the scan and scored after it;
+  // a short list's (key, index, score) staged for its rank sort
+  __shared__ int s_cand[DW ? DAL_SORT_CAP_PAYLOAD : 1];
+  __shared__ unsigned long long s_lk[DW ? kLocalSort : 1];
+  __shared__ long long s_li[DW ? kLocalSort : 1];
+  __shared__ double s_lp[DW ? kLocalSort : 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const unsigned long long tau = group_threshold(S, k);
   if (blockIdx.x == 0 && tid == 0) h->kstar = tau;
@@ -1352,8 +1547,9 @@ __global__ __launch_bounds__(kSumThreads) void summary_select_kernel(
   }
   __syncthreads();
   const int nh = static_cast<int>(s_nh);
-  const double lut_lane = DW && lane < n_lut ? AR.R.lut[lane] : 0.0;
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
+  // DW: the list holds at most this many (the region's capacity)
+  const int64_t kept = DW ? (cap < DAL_SORT_CAP_PAYLOAD ? cap : DAL_SORT_CAP_PAYLOAD) : cap;
   constexpr int kIlp = 8;
   for (int q = w; q < nh; q += W) {
     const int64_t r0 = static_cast<int64_t>(s_hits[q]) * S.group_rows;
@@ -1376,35 +1572,12 @@ __global__ __launch_bounds__(kSumThreads) void summary_select_kernel(
         const unsigned long long cm = __ballot(cand);
         if (!cm) continue;
         if constexpr (DW) {
-          double my_s = 0.0;
-          bool my_ok = false;
-          if (__popcll(cm) > 2) {
-            const int v = cand ? AR.R.votes[i] : 0;
-            const double e = n_lut ? __shfl(lut_lane, v) : 0.0;
-            if (cand) my_ok = dw_canonical_score_lane<8>(AR.R, i, my_s, e, n_lut);
-          } else {
-            for (unsigned long long t = cm; t;) {
-              const int l = __ffsll(static_cast<long long>(t)) - 1;
-              t &= t - 1;
-              double sc;
-              const bool okl = dw_canonical_score_wave(AR.R, i - lane + l, sc, lut_lane, n_lut);
-              if (lane == l) {
-                my_s = sc;
-                my_ok = okl;
-              }
-            }
-          }
-          // slots in this block's region (an LDS counter: same-address device
+          // slots in this block's list (an LDS counter: same-address device
           // atomics from ~100 waves serialised at ~0.1 us each)
           unsigned base = 0;
           if (lane == 0) base = atomicAdd(&s_nc, static_cast<unsigned>(__popcll(cm)));
           const int64_t p = static_cast<int64_t>(__shfl(base, 0)) + __popcll(cm & lt_mask);
-          if (cand && p < cap) {
-            const int64_t q = static_cast<int64_t>(blockIdx.x) * cap + p;
-            st_sc1(cidx + q, static_cast<int64_t>(idx_base + i));
-            st_sc1(AR.cpay + q, my_s);
-            st_sc1(AR.ckey + q, static_cast<uint64_t>(my_ok ? score_key(my_s, DAL_DESCENDING) : DAL_KEY_NONE));
-          }
+          if (cand && p < kept) s_cand[p] = static_cast<int>(i);
         } else {
           unsigned base = 0;
           if (lane == 0) base = atomicAdd(&h->cand_count, static_cast<unsigned>(__popcll(cm)));
@@ -1415,8 +1588,70 @@ __global__ __launch_bounds__(kSumThreads) void summary_select_kernel(
     }
   }
   if constexpr (!DW) return;
-  // this block's count, then the last block to arrive sorts the candidates
+  // Score the listed candidates (canonical fp64, density_weighting.py:148,
+  // 157-167), spread over the block's waves whichever waves found them: up to
+  // kWaveScoreMax per wave, each by the whole wave (its features' loads and divisions in
+  // flight together, the oracle's sequential sum through the lanes); more, by
+  // one lane each in as few waves as hold them: a wave's lane pass is fp64
+  // division-bound and costs the same for 1 candidate as for 64 (dealing 40
+  // candidates round-robin put every wave, four per SIMD, through it: ~60 us).
   __syncthreads();
+  const int nc = static_cast<int>(s_nc < kept ? s_nc : kept);
+  const double lut_lane = lane < n_lut ? AR.R.lut[lane] : 0.0;
+  const int64_t reg0 = static_cast<int64_t>(blockIdx.x) * cap;
+  // a short list is staged in LDS and written to the region sorted by (key,
+  // index) -- each entry at its rank -- so the last block merges the regions
+  const bool local = nc <= kLocalSort;  // (block-uniform)
+  auto put = [&](int c, int64_t i, double sc, bool ok) {
+    const unsigned long long key = ok ? score_key(sc, DAL_DESCENDING) : DAL_KEY_NONE;
+    if (local) {
+      s_lk[c] = key;
+      s_li[c] = idx_base + i;
+      s_lp[c] = sc;
+    } else {
+      st_sc1(cidx + reg0 + c, static_cast<int64_t>(idx_base + i));
+      st_sc1(AR.cpay + reg0 + c, sc);
+      st_sc1(AR.ckey + reg0 + c, static_cast<uint64_t>(key));
+    }
+  };
+  if (nc <= kWaveScoreMax * W) {  // (block-uniform)
+    for (int c = w; c < nc; c += W) {  // (wave-uniform)
+      const int64_t i = s_cand[c];
+      double sc;
+      const bool ok = dw_canonical_score_wave(AR.R, i, sc, lut_lane, n_lut);
+      if (lane == 0) put(c, i, sc, ok);
+    }
+  } else {
+    for (int c0 = 0; c0 < nc; c0 += kSumThreads) {  // (block-uniform trip count)
+      const int c = c0 + tid;  // packed: as few waves as hold them, waves 0-3 on four SIMDs
+      const bool live = c < nc;
+      const int64_t i = live ? s_cand[c] : 0;
+      const int v = live ? AR.R.votes[i] : 0;
+      const double e = n_lut ? __shfl(lut_lane, v) : 0.0;  // (every lane takes part)
+      if (live) {
+        double sc;
+        const bool ok = dw_canonical_score_lane<DAL_K3_LANE_CHUNK>(AR.R, i, sc, e, n_lut);
+        put(c, i, sc, ok);
+      }
+    }
+  }
+  __syncthreads();
+  if (local) {
+    for (int c = tid; c < nc; c += kSumThreads) {
+      const unsigned long long kc = s_lk[c];
+      const long long ic = s_li[c];
+      int r = 0;
+      for (int j = 0; j < nc; ++j) {
+        const unsigned long long kj = s_lk[j];
+        const long long ij = s_li[j];
+        r += kj < kc || (kj == kc && ij < ic);
+      }
+      st_sc1(cidx + reg0 + r, static_cast<int64_t>(ic));
+      st_sc1(AR.cpay + reg0 + r, s_lp[c]);
+      st_sc1(AR.ckey + reg0 + r, static_cast<uint64_t>(kc));
+    }
+  }
+  // this block's count, then the last block to arrive sorts the candidates
   if (tid == 0) st_sc1(&h->reg_count[blockIdx.x], s_nc);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1471,11 +1706,18 @@ GroupSummary launch_group_min(const uint64_t* keys_lo, const uint64_t* keys_hi, 
   return S;
 }
 
-// summary_select_kernel's grid: <= 128 groups per block (each block derives
-// tau itself; 32 blocks x 128 = kMaxGroups), so a block's hits fit its list.
+// summary_select_kernel's grid: <= 32 groups per block (each block derives
+// tau itself; 128 blocks x 32 = kMaxGroups), so a block's hits fit its list
+// and its candidates' canonical scores (fp64 divisions: VALU-bound when a CU
+// holds many) spread over up to 128 CUs -- 32 blocks of 128 groups left
+// config 4 at k = 1,000 ~2.5 candidates per wave on a quarter of the CUs.
+#ifndef DAL_K3_GROUPS_PER_BLOCK
+#define DAL_K3_GROUPS_PER_BLOCK 32
+#endif
+static_assert(kMaxGroups / DAL_K3_GROUPS_PER_BLOCK <= kMaxRegions, "regions");
 int summary_grid(int64_t ng) {
-  int64_t g = ceil_div(ng, 128);
-  if (g > 32) g = 32;
+  int64_t g = ceil_div(ng, DAL_K3_GROUPS_PER_BLOCK);
+  if (g > kMaxRegions) g = kMaxRegions;
   if (g < 1) g = 1;
   return static_cast<int>(g);
 }
@@ -1553,7 +1795,7 @@ struct RerankWs {
   TopkLayout L1, L2;
   size_t l2, pos, gmin, reg, total;
 };
-constexpr int kMaxSumBlocks = 32;  // summary_select_kernel blocks (candidate regions)
+constexpr int kMaxSumBlocks = kMaxRegions;  // summary_select_kernel blocks (candidate regions)
 
 static RerankWs rerank_ws(int64_t n, int64_t k, int64_t cap) {
   RerankWs W;
@@ -1597,6 +1839,7 @@ static DwRegions dw_regions(void* ws, const RerankWs& W, int64_t cap) {
 static void set_regions(SortTail& tail, TopkHdr* h, int64_t cap, int blocks) {
   tail.n_reg = blocks;
   tail.reg_stride = cap;
+  tail.sorted_max = kLocalSort;
   tail.reg_count = h->reg_count;
 }
 

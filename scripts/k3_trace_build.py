@@ -21,7 +21,7 @@ def sub(old, new):
     s = s.replace(old, new, 1)
 
 
-sub("struct TopkHdr {", """__device__ unsigned long long g_k3[256];
+sub("struct TopkHdr {", """__device__ unsigned long long g_k3[1024];
 #define K3T(slot) do { if (threadIdx.x == 0) g_k3[slot] = __builtin_amdgcn_s_memrealtime(); } while (0)
 struct TopkHdr {""")
 sub("""  const unsigned long long tau = group_threshold(S, k);
@@ -31,10 +31,11 @@ sub("""  const unsigned long long tau = group_threshold(S, k);
   if (blockIdx.x == 0 && tid == 0) h->kstar = tau;""")
 sub("""  const int nh = static_cast<int>(s_nh);""", """  const int nh = static_cast<int>(s_nh);
   if (blockIdx.x == 0) K3T(2);
-  if (tid == 0) g_k3[128 + blockIdx.x] = nh;""")
+  if (tid == 0) g_k3[512 + blockIdx.x] = nh;
+  const unsigned long long ta = __builtin_amdgcn_s_memrealtime();""")
 sub("""  if (!s_last) return;
   sort_tail_body<true>(AR.ckey, cidx, AR.cpay, h, int64_t{0}, k, out_keys, out_idx, out_scores, tail);
-}""", """  K3T(64 + blockIdx.x);
+}""", """  K3T(256 + blockIdx.x);
   if (!s_last) return;
   K3T(3);
   if (tid == 0) g_k3[5] = gridDim.x;
@@ -47,9 +48,9 @@ sub("""  if (nv < k) return DAL_KEY_NONE;  // (block-uniform)""", """  if (block
 sub("""  // the upper edge of the k-th key's bucket: >= the k-th group minimum, and at""", """  if (blockIdx.x == 0) K3T(11);
   if (blockIdx.x == 0 && threadIdx.x == 0) g_k3[13] = cnt;
   // the upper edge of the k-th key's bucket: >= the k-th group minimum, and at""")
-sub("""  if (m <= kRankMax) {""", """  if (threadIdx.x == 0) g_k3[4] = m;
+sub("""  if constexpr (PAY) if (tail.n_reg > 1 && s_runs_sorted &&""", """  if (threadIdx.x == 0) g_k3[4] = m;
   K3T(7);
-  if (m <= kRankMax) {""")
+  if constexpr (PAY) if (tail.n_reg > 1 && s_runs_sorted &&""")
 sub("""      if (PAY) sp[i] = ld_sc1(pay + q);
     }
     __syncthreads();
@@ -63,18 +64,12 @@ sub("""    if (PAY && h) {
     K3T(9);
     if (PAY && h) {
       for (int64_t i = kk + tid; i < k; i += kSortThreads) {""")
-sub("""    const int64_t r0 = static_cast<int64_t>(s_hits[q]) * S.group_rows;""", """    const unsigned long long ta = __builtin_amdgcn_s_memrealtime();
-    const int64_t r0 = static_cast<int64_t>(s_hits[q]) * S.group_rows;""")
-sub("""      if (!__ballot(cbits != 0)) continue;""", """      const unsigned long long tb = __builtin_amdgcn_s_memrealtime();
-      if (lane == 0) atomicMax(&g_k3[20], tb - ta);
-      if (!__ballot(cbits != 0)) continue;""")
-sub("""          const int64_t p = static_cast<int64_t>(__shfl(base, 0)) + __popcll(cm & lt_mask);
-          if (cand && p < cap) {
-            const int64_t q = static_cast<int64_t>(blockIdx.x) * cap + p;""", """          const int64_t p = static_cast<int64_t>(__shfl(base, 0)) + __popcll(cm & lt_mask);
-          const unsigned long long tc = __builtin_amdgcn_s_memrealtime();
-          if (lane == 0) atomicMax(&g_k3[21], tc - tb);
-          if (cand && p < cap) {
-            const int64_t q = static_cast<int64_t>(blockIdx.x) * cap + p;""")
+sub("""  const int nc = static_cast<int>(s_nc < kept ? s_nc : kept);""", """  const int nc = static_cast<int>(s_nc < kept ? s_nc : kept);
+  const unsigned long long tb = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) atomicMax(&g_k3[20], tb - ta);
+  if (threadIdx.x == 0) atomicMax(&g_k3[23], static_cast<unsigned long long>(nc));""")
+sub("""  // this block's count, then the last block to arrive sorts the candidates""", """  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(&g_k3[21], __builtin_amdgcn_s_memrealtime() - tb);""")
 sub("""  if (tid == 0) st_sc1(&h->reg_count[blockIdx.x], s_nc);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();""", """  if (tid == 0) st_sc1(&h->reg_count[blockIdx.x], s_nc);
@@ -84,10 +79,10 @@ sub("""  if (tid == 0) st_sc1(&h->reg_count[blockIdx.x], s_nc);
   if (threadIdx.x == 0) atomicMax(&g_k3[22], __builtin_amdgcn_s_memrealtime() - te);""")
 s += """
 extern "C" int dal_k3_trace(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dal::g_k3), sizeof(unsigned long long) * 256) == hipSuccess ? 0 : 1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dal::g_k3), sizeof(unsigned long long) * 1024) == hipSuccess ? 0 : 1;
 }
 extern "C" int dal_k3_trace_reset() {
-  unsigned long long z[256] = {};
+  unsigned long long z[1024] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(dal::g_k3), z, sizeof(z)) == hipSuccess ? 0 : 1;
 }
 """
