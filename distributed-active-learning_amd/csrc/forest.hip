@@ -27,7 +27,10 @@ namespace dal {
 namespace {
 
 constexpr int kForestThreads = 256;
-constexpr int kTreeIlp = 4;
+#ifndef DAL_FOREST_ILP
+#define DAL_FOREST_ILP 4
+#endif
+constexpr int kTreeIlp = DAL_FOREST_ILP;  // independent tree walks in flight per lane
 
 struct ForestArgs {
   const float* x;
@@ -387,7 +390,10 @@ ForestTiling forest_tiling(const float* x, int64_t d, int64_t ldx, int32_t n_tre
   }
   // many trees (config 3: T = 100): spread a row's trees over more lanes --
   // the traversal's dependent LDS round trips, not HBM, bound that case
-  const int tpr_min = n_trees >= 64 ? 2 : 1;  // config 3: 60.7 -> 51.8 us (4: 53.5, 8: 60.9)
+#ifndef DAL_FOREST_TPR
+#define DAL_FOREST_TPR 2
+#endif
+  const int tpr_min = n_trees >= 64 ? DAL_FOREST_TPR : 1;  // config 3: 60.7 -> 51.8 us (4: 53.5, 8: 60.9)
   if (T.x_lds) {
     while (T.R > 1 && kForestThreads / T.R < tpr_min) T.R >>= 1;
   }

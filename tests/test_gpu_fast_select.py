@@ -24,7 +24,7 @@ def _case(n, d, seed=0):
 
 
 @pytest.mark.parametrize("n,d,k", [(100_000, 64, 100), (20_000, 32, 10), (5_000, 48, 100), (1_500, 16, 1),
-                                   (250_000, 30, 1000)])
+                                   (250_000, 30, 1000), (100_000, 64, 1000)])
 def test_fast_level1_select_bit_exact(cuda, n, d, k):
     from dal import density_weighting as dw
     from dal.engine import PoolState, level1_passes
