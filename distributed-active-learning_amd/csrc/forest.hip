@@ -26,7 +26,10 @@
 namespace dal {
 namespace {
 
-constexpr int kForestThreads = 256;
+#ifndef DAL_FOREST_THREADS
+#define DAL_FOREST_THREADS 256
+#endif
+constexpr int kForestThreads = DAL_FOREST_THREADS;
 #ifndef DAL_FOREST_ILP
 #define DAL_FOREST_ILP 4
 #endif
@@ -380,7 +383,7 @@ ForestTiling forest_tiling(const float* x, int64_t d, int64_t ldx, int32_t n_tre
   // 100: 264 -> 290 us, 100k x 64: 18.4 -> 19.8) holds no registers: 32 KiB
   // tiles there (2M x 256: 441 -> 411 us; 64 KiB 1248)
   T.dma = d >= 128 && d % 4 == 0 && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0;
-  const int64_t tile_cap = T.dma ? 33280 : 16640;
+  const int64_t tile_cap = T.dma ? 33280 : 16640 * (kForestThreads / 256);
   while (T.R > 16 && static_cast<int64_t>(T.R) * (d + 1) * 4 > tile_cap) T.R >>= 1;
   // wide rows: 16 rows may exceed the preferred tile; LDS staging up to 64 KiB
   if (static_cast<int64_t>(T.R) * (d + 1) * 4 > 65536) {
