@@ -114,6 +114,9 @@ __device__ __forceinline__ unsigned fresh_lane() {
   return v;
 }
 
+#ifndef DAL_GRAM_PRIO8
+#define DAL_GRAM_PRIO8 1  // 8-wave kernel: s_setprio 1 for waves 4-7 (> 0) or 0-3 (< 0)
+#endif
 template <int KS, int W = 4>
 struct Cfg {
   static constexpr int WAVES = W;                   // 4: one super block per block; 8: two (P, P + 2)
@@ -161,6 +164,15 @@ __global__ __launch_bounds__(64 * W, 8 / W) void gram_csym_kernel(
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int half = wave >> 2, wave4 = wave & 3;  // the block's super block of this wave, wave within it
+  // 8-wave block: the two waves of a SIMD (w, w + 4) run the same program in
+  // lockstep; a static priority for one half settles their VALU arbitration
+  // once instead of by age at every segment (MI355X_MICROARCH.md, two waves per
+  // SIMD): waves 4-7 at priority 1, 2M x 256 1266.9 -> 1262.3 ms (waves 0-3:
+  // 1265.0; deferring waves 4-7's last column epilogue of each stage into the
+  // next one, a stagger, 1274.5)
+  if constexpr (W == 8 && DAL_GRAM_PRIO8 != 0) {
+    if (DAL_GRAM_PRIO8 > 0 ? half == 1 : half == 0) __builtin_amdgcn_s_setprio(1);
+  }
   const int li = lane & 15, lq = lane >> 4;
   const int G = gridDim.x, g = blockIdx.x;
   if constexpr (HV == 1) {
