@@ -114,6 +114,9 @@ __device__ __forceinline__ unsigned fresh_lane() {
   return v;
 }
 
+#ifndef DAL_GRAM_SIGMA_COLS
+#define DAL_GRAM_SIGMA_COLS 1  // KS 64 / 128: column sums from sigma_P MFMAs
+#endif
 #ifndef DAL_GRAM_PRIO8
 #define DAL_GRAM_PRIO8 1  // 8-wave kernel: s_setprio 1 for waves 4-7 (> 0) or 0-3 (< 0)
 #endif
@@ -137,10 +140,17 @@ struct Cfg {
   static constexpr int LG = 4;
   static constexpr int NKS = KS / 32;               // k-steps of v_mfma_f32_16x16x32_f16
   static constexpr int NCT = SC / 16;               // column tiles per stage
-  static constexpr bool SIG = KS == 32;             // column sums from sigma_P MFMAs
+  // column sums from sigma_P MFMAs (sigma_P = the sum of the super block's H
+  // rows): KS 32 always, KS 64 / 128 unless DAL_GRAM_SIGMA_COLS = 0 (then the
+  // growth of the row chains' lane totals, one epilogue per 16-column tile)
+  static constexpr bool SIG = KS == 32 || DAL_GRAM_SIGMA_COLS != 0;
+  // KS >= 64: sigma_P's two fp16 terms packed as rows 0-7 / 8-15 of one A
+  // fragment, two MFMAs per k-step (KS 32 keeps its three-MFMA form)
+  static constexpr bool PACK = SIG && KS >= 64;
   static constexpr int NCH = SIG ? 1 : 2;           // row-sum chains per row tile
   static_assert(SPF >= 1 && SPP % SPF == 0 && PIECES >= 1 && NKS >= 1, "bad slice");
-  static_assert(W == 4 || (W == 8 && !SIG), "two super blocks per block: KS >= 64 only");
+  static_assert(W == 4 || (W == 8 && KS >= 64), "two super blocks per block: KS >= 64 only");
+  static_assert(!SIG || KS <= 128, "sigma partials: <= 32 values per lane");
 };
 
 template <int KS, int W>
@@ -158,8 +168,8 @@ __global__ __launch_bounds__(64 * W, 8 / W) void gram_csym_kernel(
   __shared__ double rowacc[HV * kSB];
   // sigma_P (KS 32): per-wave partial sums of the H rows, then the sum split in
   // two fp16 terms (at 2^-6 of the operand's scale), read as an A fragment
-  __shared__ float sig_part[SIG ? 4 : 1][SIG ? KS : 1];
-  __shared__ f16x8 sig_row[SIG ? 2 * C::HI : 1];
+  __shared__ float sig_part[SIG ? W : 1][SIG ? KS : 1];
+  __shared__ f16x8 sig_row[SIG ? HV : 1][SIG ? 2 * C::HI : 1];
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -312,21 +322,36 @@ __global__ __launch_bounds__(64 * W, 8 / W) void gram_csym_kernel(
           sp[c * 8 + e] = t;
         }
       const int fl2 = static_cast<int>(fresh_lane()), fli = fl2 & 15, flq = fl2 >> 4;
-      row_sum_scatter<V>(sp, fli);
-      if (fli < V) sig_part[wave][(fli >> 3) * 32 + flq * 8 + (fli & 7)] = sp[0];
+      if constexpr (V == 32) {
+        // 16-lane reduce-scatter of 32 values: lane li keeps values 2 li, 2 li + 1
+        rs_step<16, 0x140, 32>(sp, fli & 8);
+        rs_step<8, 0x141, 32>(sp, fli & 4);
+        rs_step<4, 0x4E, 32>(sp, fli & 2);
+        rs_step<2, 0xB1, 32>(sp, fli & 1);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int idx = 2 * fli + q;
+          sig_part[wave][(idx >> 3) * 32 + flq * 8 + (idx & 7)] = sp[q];
+        }
+      } else {
+        row_sum_scatter<V>(sp, fli);
+        if (fli < V) sig_part[wave][(fli >> 3) * 32 + flq * 8 + (fli & 7)] = sp[0];
+      }
     }
   };
   // after a block_sync that follows load_a: sigma_P = the four waves' partials
   // (fixed order), scaled by 2^-6 (exact) and split into two fp16 terms
   auto build_sigma = [&]() {
     if constexpr (SIG) {
-      if (tid < KS) {
-        const float sg = ((sig_part[0][tid] + sig_part[1][tid]) + sig_part[2][tid]) + sig_part[3][tid];
+      if (tid < HV * KS) {  // super block hh of the block: its four waves' partials
+        const int hh = tid / KS, f = tid % KS;
+        const float sg = ((sig_part[4 * hh][f] + sig_part[4 * hh + 1][f]) + sig_part[4 * hh + 2][f]) +
+                         sig_part[4 * hh + 3][f];
         const float s6 = sg * 0x1p-6f;
         const _Float16 h = static_cast<_Float16>(s6);
         const _Float16 l = static_cast<_Float16>(s6 - static_cast<float>(h));
-        reinterpret_cast<_Float16*>(sig_row)[tid] = h;
-        reinterpret_cast<_Float16*>(sig_row)[KS + tid] = l;
+        reinterpret_cast<_Float16*>(sig_row[hh])[f] = h;
+        reinterpret_cast<_Float16*>(sig_row[hh])[KS + f] = l;
       }
     }
   };
@@ -342,7 +367,12 @@ __global__ __launch_bounds__(64 * W, 8 / W) void gram_csym_kernel(
 
   f32x4 mc[NCH][C::RT];
   float tprev[2];
-  f16x8 sgh[SIG ? C::NKS : 1], sgl[SIG ? C::NKS : 1];
+  // KS 32: sigma_P's high and low terms as two A fragments (every row the
+  // same), three MFMAs per k-step; KS >= 64 (PACK): one A fragment, rows 0-7
+  // the high term and rows 8-15 the low one (output row 0 + row 8 = the
+  // column sum), two MFMAs per k-step -- the same for 4- and 8-wave blocks,
+  // so the density bits do not depend on the block form
+  f16x8 sgh[SIG ? C::NKS : 1], sgl[SIG && !C::PACK ? C::NKS : 1];
   // one stage of SC columns (col0 = its first column within the pair);
   // fresh = first stage of a fold group (chains restart).  B fragments go
   // through two register sets: k-step i+1's are read while k-step i's MFMAs
@@ -360,7 +390,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void gram_csym_kernel(
       if (ct < C::NCT) {
         const int ch = ct % NCH;
         const bool fresh = fresh_stage && ct < NCH;
-        const bool sig = SIG && (ct & 3) == wave;  // column tile ct's sums: this wave's turn
+        const bool sig = SIG && (ct & 3) == wave4;  // column tile ct's sums: this wave's turn (per super block)
         f32x4 sg = {};
 #pragma unroll
         for (int c = 0; c < C::NKS; ++c) {
@@ -378,12 +408,20 @@ __global__ __launch_bounds__(64 * W, 8 / W) void gram_csym_kernel(
           if (sig) {
             sg = mfma16(sgh[c], bh[cur], sg);
             sg = mfma16(sgh[c], bl[cur], sg);
-            sg = mfma16(sgl[c], bh[cur], sg);
+            if constexpr (!C::PACK) sg = mfma16(sgl[c], bh[cur], sg);
           }
         }
-        // every output row of the sigma tile is the column sum (units 2^-18)
-        if (sig && lq == 0)
-          colacc[cbuf][col0 + ct * 16 + li] = static_cast<double>(__builtin_rintf(sg[0] * cmul * 64.0f));
+        // every output row of the sigma tile is the column sum (units 2^-18);
+        // PACK: rows 0 (lane group 0) and 8 (lane group 2) its two terms, each
+        // rounded to 2^-32 and added exactly (both super blocks of an 8-wave
+        // block add theirs)
+        if constexpr (!C::PACK) {
+          if (sig && lq == 0)
+            colacc[cbuf][col0 + ct * 16 + li] = static_cast<double>(__builtin_rintf(sg[0] * cmul * 64.0f));
+        } else {
+          if (sig && (lq & 1) == 0)
+            atomicAdd(&colacc[cbuf][col0 + ct * 16 + li], static_cast<double>(__builtin_rintf(sg[0] * cmul * 64.0f)));
+        }
       }
       if (!SIG && ct > 0 && !(kAbl & 1)) {
         // tile ct-1's column sums: growth of its chain's lane total
@@ -518,9 +556,13 @@ __global__ __launch_bounds__(64 * W, 8 / W) void gram_csym_kernel(
           sig_fresh = false;
 #pragma unroll
           for (int c = 0; c < (SIG ? C::NKS : 0); ++c) {
-            const int flq = static_cast<int>(fresh_lane()) >> 4;
-            sgh[c] = sig_row[c * C::LG + flq];
-            sgl[c] = sig_row[C::HI + c * C::LG + flq];
+            const int fl = static_cast<int>(fresh_lane()), flq = fl >> 4;
+            if constexpr (!C::PACK) {
+              sgh[c] = sig_row[0][c * C::LG + flq];
+              sgl[c] = sig_row[0][C::HI + c * C::LG + flq];
+            } else {
+              sgh[c] = sig_row[SIG ? half : 0][((fl & 8) ? C::HI : 0) + c * C::LG + flq];
+            }
           }
         }
       }
@@ -928,21 +970,28 @@ extern "C" double dal_density_error_bound_sym(int64_t n_cols) {
   // conservative unit roundoff for the MFMA's internal fp32 adds, counted as
   // sequential adds), products exact (f16 x f16), c = 1 + 2^-8 >= sum_d |h_i
   // h_j| + |h_i l_j| over sum_d |u_i u_j| <= 1 (Cauchy-Schwarz on unit rows):
-  //   row side   two chains of <= 4 (KS 128) / 8 (KS 64) tiles x 2 KS products
-  //              (one chain of 16 tiles x 64 at KS 32), <= 1024 products, joined
-  //              by one add and 4 cross-lane adds: gamma_1029 * c
-  //   column side  a tile's partial is T_k - T_{k-1}, T = sum of the lane's 16
-  //              chain values: (8 gamma_128 + 15 gamma_15 + u) * c (KS 128: 4
-  //              tiles of 256 products; the same total); sigma form (KS 32):
-  //              (gamma_22 + gamma_96 + 3 * 2^-22) * c
+  //   row side   one chain per row tile of <= 8 (KS 128) / 16 (KS 64) tiles x
+  //              2 KS products (16 tiles x 64 at KS 32), <= 1024 products, and
+  //              4 cross-lane adds: gamma_1029 * c
+  //   column side  sigma_P MFMAs: sigma_P = the fp32 sum of the super block's
+  //              H rows (8 row tiles, 4 DPP steps, 4 waves: <= 15 adds), split
+  //              into two fp16 terms (2^-22), then <ũ_j, sigma_P> over KS
+  //              features -- KS >= 64: the two terms as rows of one A fragment,
+  //              2 x KS products, each row rounded to 2^-32: (gamma_15 +
+  //              gamma_256 + 3 * 2^-22) * c at KS 128; KS 32 (three MFMAs per
+  //              k-step): (gamma_22 + gamma_96 + 3 * 2^-22) * c.  The chain-
+  //              growth form (DAL_GRAM_SIGMA_COLS = 0): (8 gamma_128 + 15
+  //              gamma_15 + u) * c
   //   residual   <L_i, R_B> + <u~_i, C_B> in fp64: below 2^-40 per column
   //   split + fp32 unit rows  5 * 2^-22;  fixed-point roundings <= 2^-33 each
   const double u = 1.0 / 8388608.0;  // 2^-23
   auto gamma = [u](double n) { return n * u / (1.0 - n * u); };
-  const double row = gamma(1029.0);
-  const double col = 8.0 * gamma(128.0) + 15.0 * gamma(15.0) + u;
-  const double c = 1.0 + 1.0 / 256.0;
   const double s = 1.0 / 4194304.0;  // 2^-22
+  const double row = gamma(1029.0);
+  const double col_growth = 8.0 * gamma(128.0) + 15.0 * gamma(15.0) + u;
+  const double col_sigma = (gamma(22.0) > gamma(15.0) ? gamma(22.0) : gamma(15.0)) + gamma(256.0) + 3.0 * s;
+  const double col = col_growth > col_sigma ? col_growth : col_sigma;
+  const double c = 1.0 + 1.0 / 256.0;
   return ((row > col ? row : col) * c + 5.0 * s + 1e-10) * static_cast<double>(n_cols) + 1e-9;
 }
 
