@@ -120,6 +120,12 @@ __device__ __forceinline__ unsigned fresh_lane() {
 #ifndef DAL_GRAM_PRIO8
 #define DAL_GRAM_PRIO8 1  // 8-wave kernel: s_setprio 1 for waves 4-7 (> 0) or 0-3 (< 0)
 #endif
+#ifndef DAL_GRAM_KS64_OCC3
+#define DAL_GRAM_KS64_OCC3 1  // KS 64: three 4-wave blocks per CU (16 KiB stages; 100k x 64 -3.2 %, 200k x 64 -3.9 %, 1M x 64 +0.6 %)
+#endif
+#ifndef DAL_GRAM_KS32_OCC
+#define DAL_GRAM_KS32_OCC 4  // KS 32: 4-wave blocks per CU (3: 16 KiB stages; 4: 8 KiB stages. Config 3: 2 -> 3 -> 4 blocks 3.944 -> 3.827 -> 3.745 ms)
+#endif
 template <int KS, int W = 4>
 struct Cfg {
   static constexpr int WAVES = W;                   // 4: one super block per block; 8: two (P, P + 2)
@@ -128,7 +134,11 @@ struct Cfg {
   static constexpr int ROWB = KS * 4;               // bytes per operand row of a slice (H + L)
   static constexpr int SLOTS = ROWB / 16;           // 16-B slots per row
   static constexpr int HI = KS / 8;                 // slots of the H part
-  static constexpr int STAGE = 32768;               // bytes per LDS stage
+  // three 4-wave blocks per CU at KS 64 (OCC3): 16 KiB stages so three fit the LDS
+  static constexpr int OCC = (W == 4 && KS == 32 && DAL_GRAM_KS32_OCC > 3) ? DAL_GRAM_KS32_OCC
+                             : (W == 4 && ((KS == 64 && DAL_GRAM_KS64_OCC3 != 0) || (KS == 32 && DAL_GRAM_KS32_OCC != 0)))
+                                 ? 3 : 8 / W;
+  static constexpr int STAGE = OCC >= 4 ? 8192 : OCC == 3 ? 16384 : 32768;  // bytes per LDS stage
   static constexpr int SC = STAGE / ROWB;           // columns per stage: 64 / 128 / 256
   static constexpr int SPP = 256 / SC;              // stages per 512 x 256 pair: 4 / 2 / 1
   static constexpr int FOLD = KS == 128 ? 128 : 256;  // columns per row fold (chains <= 1024 products)
@@ -154,7 +164,7 @@ struct Cfg {
 };
 
 template <int KS, int W>
-__global__ __launch_bounds__(64 * W, 8 / W) void gram_csym_kernel(
+__global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
     const uint16_t* __restrict__ urows, int srow0, int n_srb,
     const uint16_t* __restrict__ ucols, int jcol0, int j_lo, int j_hi, int skip_lo, int skip_hi,
     int ns_active, int64_t ldh, int slice_off, int chunk_j, int n_chunks,
@@ -895,7 +905,9 @@ int launch_csym_w(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint
                   int64_t j_lo, int64_t j_hi, int64_t skip_lo, int64_t skip_hi, int64_t ns_active, int64_t ldh,
                   int slice_off, int64_t* acc, int grid_blocks, int contig, hipStream_t stream) {
   // grid_blocks counts 4-wave blocks (two per CU); 8-wave blocks are one per CU
-  const int G0 = (grid_blocks > 0 ? grid_blocks : 2 * device_cus()) * 4 / W;
+  constexpr int kOcc = Cfg<KS, W>::OCC;
+  const int G0 = W == 4 ? (grid_blocks > 0 ? grid_blocks * kOcc / 2 : kOcc * device_cus())
+                        : (grid_blocks > 0 ? grid_blocks : 2 * device_cus()) * 4 / W;
   const int64_t nj = j_hi - j_lo;
   int64_t cbk = nj, n_chunks = 1, G;
   if (contig) {
