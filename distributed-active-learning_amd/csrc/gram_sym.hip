@@ -690,11 +690,15 @@ __global__ __launch_bounds__(256) void csym_sigma_kernel(const uint16_t* __restr
 // block = 8 waves; lane = one of 64 features (blockIdx.x * 64 + lane), wave w
 // owns super blocks [w*ns/8, (w+1)*ns/8).  R_B, C_B written as fp64 for B in
 // [b0, b1).
-__global__ __launch_bounds__(512) void csym_scan_kernel(const long long* __restrict__ sig_u,
+#ifndef DAL_CSYM_SCAN_WAVES
+#define DAL_CSYM_SCAN_WAVES 16
+#endif
+constexpr int kScanWaves = DAL_CSYM_SCAN_WAVES;  // super-block ranges per feature (one wave each)
+__global__ __launch_bounds__(64 * kScanWaves) void csym_scan_kernel(const long long* __restrict__ sig_u,
                                                          const long long* __restrict__ sig_l, int ns, int d_pad,
                                                          int b0, int b1, double* __restrict__ rb,
                                                          double* __restrict__ cb) {
-  constexpr int kW = 8;  // waves
+  constexpr int kW = kScanWaves;
   __shared__ long long part[kW][4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int f = blockIdx.x * 64 + lane;
@@ -1079,7 +1083,7 @@ extern "C" int dal_gram_sym_residual(const uint16_t* ops, int64_t nb_active, int
                      dim3(static_cast<unsigned>(na), static_cast<unsigned>(ceil_div(ldh / 8, 256))), dim3(256), 0, st,
                      ops, ldh, ks, static_cast<int>(d_pad), sig_u, sig_l);
   DAL_RETURN_IF_LAUNCH_FAILED();
-  hipLaunchKernelGGL(csym_scan_kernel, dim3(static_cast<unsigned>(ceil_div(d_pad, 64))), dim3(512), 0, st, sig_u,
+  hipLaunchKernelGGL(csym_scan_kernel, dim3(static_cast<unsigned>(ceil_div(d_pad, 64))), dim3(64 * kScanWaves), 0, st, sig_u,
                      sig_l, static_cast<int>(na), static_cast<int>(d_pad), static_cast<int>(s0),
                      static_cast<int>(s0 + ns), rb, cb);
   DAL_RETURN_IF_LAUNCH_FAILED();
