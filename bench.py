@@ -242,7 +242,8 @@ def gram_roofline(gram, achieved, traffic, gram_ms, gram_ms_max, flops, products
     sym = gram == "sym"
     executed = achieved * products / (2.0 if sym else 1.0)
     names = {3: "h.h, h.l, l.h", 2: "H.H, H.L on the taker side + the exact closed-form remainder "
-                                     "(dal_gram_sym_residual, included in launch_ms)"}
+                                     "(dal_gram_sym_residual, included in launch_ms); column sums from "
+                                     "sigma_P MFMAs (+3 % executed, not counted in achieved)"}
     return {"bound": "mfma",
             "kernel": (f"dal_gram_rowsum_{'sym + dal_gram_sym_residual' if sym else 'split'} "
                        f"({products}x v_mfma_f32_16x16x32_f16 / 32 features)"),
