@@ -720,9 +720,12 @@ def bench_div(args, steps, warmup, world, rank, dev, dist, backend, cpu=12.0):
                   _stream(dev))
 
     # back-to-back launches between two events (an event pair around each
-    # launch also times the host's submission of that launch)
-    reps = 10
-    for _ in range(2):
+    # launch also times the host's submission of that launch), after 30
+    # untimed ones: the host-side self-check leaves the GPU idle and its clock
+    # takes tens of milliseconds to ramp back (first 5-launch window 1.69 ms
+    # vs 1.42-1.44 ms held, scripts/maxcos_window_probe.py)
+    reps = 20
+    for _ in range(30):
         launch()
     e0.record()
     for _ in range(reps):
@@ -954,12 +957,15 @@ def main():
             c, cfg, label = resolve(spec)
             t0 = time.perf_counter()
             variant = ":" in spec  # config-4 T=100 / k=1000: the same 2M x 256 pool, fewer steps
+            # 60 untimed steps (0.06-0.25 s of GPU work): after the previous
+            # config's host-side checks the clock needs tens of milliseconds
+            # to ramp back, longer than 5 steps of a 1-4 ms config
             if cfg.get("mode") == "div":
-                r = bench_div(args, 20, 5, world, rank, dev, dist, backend, cpu=8.0)
+                r = bench_div(args, 20, 60, world, rank, dev, dist, backend, cpu=8.0)
             elif variant:
                 r = bench_dw(args, c, 3, 1, 5, world, rank, dev, dist, backend, cpu=False, cfg=cfg)
             else:
-                r = bench_dw(args, c, 20, 5, 20, world, rank, dev, dist, backend, cpu=8.0, cfg=cfg)
+                r = bench_dw(args, c, 20, 60, 20, world, rank, dev, dist, backend, cpu=8.0, cfg=cfg)
             out["extra"][label] = {kk: r[kk] for kk in (
                 "metric", "value", "unit", "steps", "warmup", "ms_per_step", "dtype", "config",
                 "warm_selection_latency_ms", "self_check", "accuracy", "roofline", "roofline_forest",
