@@ -485,9 +485,12 @@ __device__ __forceinline__ uint8_t rerank_flag(const DwRerank& R, int64_t i) {
 // (x_f / norm) * s_f -- the loads and divisions of 256 features in flight
 // together (one memory round trip per 256 features: a round trip per
 // 64-feature chunk made a d = 256 row cost ~13 us) -- and the sequential sum
-// over f takes the products from the lanes in order (the oracle's operations
-// in the oracle's order).  false (NONE key, NaN payload) when the row is not
-// an unlabeled candidate (a shard with < k candidates).
+// over f takes the products in order (the oracle's operations in the
+// oracle's order) from the wave's 64-double LDS slot `tr`: each chunk's
+// products are written there and read back as broadcasts, two per
+// ds_read_b128 (two v_readlane per product before).  false (NONE key, NaN
+// payload) when the row is not an unlabeled candidate (a shard with < k
+// candidates).
 __device__ __forceinline__ double readlane_f64(double v, int l) {  // l wave-uniform
   const long long b = __double_as_longlong(v);
   const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(b), l));
@@ -500,7 +503,7 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {  // l wave-uni
 // scalar registers.
 __device__ __attribute__((noinline)) double density_pow_canon(double d, double beta) { return pow(d, beta); }
 
-__device__ __forceinline__ bool dw_canonical_score_wave(const DwRerank& R, int64_t i, double& s,
+__device__ __forceinline__ bool dw_canonical_score_wave(const DwRerank& R, int64_t i, double& s, double* tr,
                                                         double lut_lane = 0.0, int n_lut = 0) {
   constexpr int kC = 4;  // 64-feature chunks per round: every chunk's loads and divisions in flight together
   const int lane = threadIdx.x & 63;
@@ -520,19 +523,30 @@ __device__ __forceinline__ bool dw_canonical_score_wave(const DwRerank& R, int64
     for (int c = 0; c < kC; ++c) {
       const int rest = __builtin_amdgcn_readfirstlane(R.d - f0 - 64 * c);
       if (rest <= 0) break;
+      // the previous chunk's reads are issued before this write (LDS
+      // operations of one wave complete in order)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      tr[lane] = p[c];
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
       if (rest >= 64) {
-        // v_readlane (no LDS round trip), 16 lanes' products into distinct
-        // scalar registers ahead of their adds: only the add chain is serial
+        // 16 products' broadcast reads ahead of their adds: only the add
+        // chain is serial
+        const double2* tr2 = reinterpret_cast<const double2*>(tr);
 #pragma unroll
-        for (int q0 = 0; q0 < 64; q0 += 16) {
-          double t[16];
+        for (int q0 = 0; q0 < 32; q0 += 8) {
+          double2 t[8];
 #pragma unroll
-          for (int j = 0; j < 16; ++j) t[j] = readlane_f64(p[c], q0 + j);
+          for (int j = 0; j < 8; ++j) t[j] = tr2[q0 + j];
 #pragma unroll
-          for (int j = 0; j < 16; ++j) acc = acc + t[j];
+          for (int j = 0; j < 8; ++j) {
+            acc = acc + t[j].x;
+            acc = acc + t[j].y;
+          }
         }
       } else {
-        for (int q = 0; q < rest; ++q) acc = acc + readlane_f64(p[c], q);
+        for (int q = 0; q < rest; ++q) acc = acc + tr[q];
       }
     }
   }
@@ -605,8 +619,9 @@ __global__ __launch_bounds__(256) void rerank_kernel(const TopkHdr* __restrict__
     if (lead) ckey[c] = DAL_KEY_NONE;
     return;
   }
+  __shared__ __attribute__((aligned(16))) double s_tr[4][64];
   double s;
-  const bool ok = dw_canonical_score_wave(R, cidx[c] - idx_base, s);
+  const bool ok = dw_canonical_score_wave(R, cidx[c] - idx_base, s, s_tr[threadIdx.x >> 6]);
   if (lead) {
     cpay[c] = s;
     ckey[c] = ok ? score_key(s, DAL_DESCENDING) : DAL_KEY_NONE;
@@ -1615,10 +1630,11 @@ __global__ __launch_bounds__(kSumThreads) void summary_select_kernel(
     }
   };
   if (nc <= kWaveScoreMax * W) {  // (block-uniform)
+    __shared__ __attribute__((aligned(16))) double s_tr[DW ? W : 1][64];
     for (int c = w; c < nc; c += W) {  // (wave-uniform)
       const int64_t i = s_cand[c];
       double sc;
-      const bool ok = dw_canonical_score_wave(AR.R, i, sc, lut_lane, n_lut);
+      const bool ok = dw_canonical_score_wave(AR.R, i, sc, s_tr[DW ? w : 0], lut_lane, n_lut);
       if (lane == 0) put(c, i, sc, ok);
     }
   } else {

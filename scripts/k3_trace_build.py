@@ -15,10 +15,20 @@ os.makedirs(out, exist_ok=True)
 s = open(os.path.join(CSRC, "topk.hip")).read()
 
 
-def sub(old, new):
+# K3_TRACE_PATH=rank: the sort stamps 8 / 9 in the rank-selection path (short
+# lists) instead of the first match, the region merge; stamp 14 after its
+# workspace clear
+RANK = os.environ.get("K3_TRACE_PATH") == "rank"
+
+
+def sub(old, new, last=False):
     global s
     assert old in s, old[:60]
-    s = s.replace(old, new, 1)
+    if last:
+        i = s.rindex(old)
+        s = s[:i] + new + s[i + len(old):]
+    else:
+        s = s.replace(old, new, 1)
 
 
 sub("struct TopkHdr {", """__device__ unsigned long long g_k3[1024];
@@ -58,12 +68,16 @@ sub("""      if (PAY) sp[i] = ld_sc1(pay + q);
     }
     __syncthreads();
     K3T(8);
-    if (tail.clear) {  // every thread read the header above""")
+    if (tail.clear) {  // every thread read the header above""", last=RANK)
+if RANK:
+    sub("""    int tpe = 1;  // lanes per element""", """    __syncthreads();
+    K3T(14);
+    int tpe = 1;  // lanes per element""")
 sub("""    if (PAY && h) {
       for (int64_t i = kk + tid; i < k; i += kSortThreads) {""", """    __syncthreads();
     K3T(9);
     if (PAY && h) {
-      for (int64_t i = kk + tid; i < k; i += kSortThreads) {""")
+      for (int64_t i = kk + tid; i < k; i += kSortThreads) {""", last=RANK)
 sub("""  const int nc = static_cast<int>(s_nc < kept ? s_nc : kept);""", """  const int nc = static_cast<int>(s_nc < kept ? s_nc : kept);
   const unsigned long long tb = __builtin_amdgcn_s_memrealtime();
   if (threadIdx.x == 0) atomicMax(&g_k3[20], tb - ta);
