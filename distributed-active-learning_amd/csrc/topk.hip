@@ -877,16 +877,46 @@ __device__ bool select_compact(const uint64_t* __restrict__ keys, const int64_t*
     const int64_t e = tid + static_cast<int64_t>(j) * kSortThreads;
     key[j] = e < m ? ld_sc1(keys + M(e)) : 0ull;
   }
-  unsigned long long prefix = 0, mask = 0;
+  // the digits start below the keys' common high bits (for density-weighted
+  // keys the sign and most of the exponent: the first 8-bit pass over them
+  // put every key in one bin)
+  __shared__ unsigned long long s_mn[kSortThreads / 64], s_mx[kSortThreads / 64];
+  unsigned long long mn = ~0ull, mx = 0ull;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    if (tid + static_cast<int64_t>(j) * kSortThreads < m) {
+      mn = key[j] < mn ? key[j] : mn;
+      mx = key[j] > mx ? key[j] : mx;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if (lane == 0) {
+    s_mn[tid >> 6] = mn;
+    s_mx[tid >> 6] = mx;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kSortThreads / 64; ++q) {
+    mn = s_mn[q] < mn ? s_mn[q] : mn;
+    mx = s_mx[q] > mx ? s_mx[q] : mx;
+  }
+  int top = 64 - __clzll(static_cast<long long>(mn ^ mx));  // bits [0, top) still to resolve (0: all equal)
+  unsigned long long mask = top == 64 ? 0ull : ~((1ull << top) - 1ull);
+  unsigned long long prefix = mn & mask;
   unsigned int krem = static_cast<unsigned int>(k), neq = static_cast<unsigned int>(m);
-  for (int pass = 0; pass < 8 && neq > static_cast<unsigned int>(kSelSmall); ++pass) {
-    const int shift = 56 - 8 * pass;
+  while (neq > static_cast<unsigned int>(kSelSmall) && top > 0) {  // (block-uniform)
+    const int width = top < 8 ? top : 8, shift = top - width;
+    const unsigned long long dmask = (1ull << width) - 1ull;
     if (tid < 256) hist[tid] = 0u;
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const bool valid = tid + j * kSortThreads < m && (key[j] & mask) == prefix;
-      const unsigned bin = static_cast<unsigned>((key[j] >> shift) & 255ull);
+      const unsigned bin = static_cast<unsigned>((key[j] >> shift) & dmask);
       // the wave's most common bin (the first valid lane's) with one atomic
       const unsigned long long vm = __ballot(valid);
       if (vm) {
@@ -927,7 +957,8 @@ __device__ bool select_compact(const uint64_t* __restrict__ keys, const int64_t*
     prefix = s_prefix;
     krem = s_krem;
     neq = s_neq;
-    mask |= 255ull << shift;
+    mask |= dmask << shift;
+    top = shift;
     __syncthreads();
   }
   if (neq > static_cast<unsigned int>(kSelSmall)) return false;
@@ -1020,11 +1051,6 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
   if (tail.cap_miss && tid == 0 && m > tail.cap) atomicOr(tail.status, DAL_FLAG_SAMPLE_MISS);
   if (tail.cap && m > tail.cap) m = tail.cap;
   if (m > CAP) m = CAP;
-  // Large candidate lists (config 3: ~4,000): a block radix select of the
-  // k-th key first (8-bit digits, keys in registers), then only the keys
-  // below its bucket plus the bucket itself (<= kSelSmall) are sorted -- the
-  // full bitonic over 4,096 keys is LDS-bound (~95 us).  Same result: every
-  // key of the top k lies in the sorted subset.
   // Sorted regions are merged when the rank selection is too long (m >
   // kRankMax) and the radix pre-selection would not shorten the sort much
   // (k + kSelSmall >= m: config 4 at k = 1,000, m = 1,261: bitonic 31 us,
@@ -1166,6 +1192,16 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
     }
     return;
   }
+  // Long lists (config 3: ~1,750 candidates, k = 100): a block radix select of
+  // the k-th key first (8-bit digits, keys in registers), then only the keys
+  // below its bucket plus the bucket itself (<= kSelSmall) are kept -- the
+  // full bitonic over 4,096 keys is LDS-bound (~95 us).  Same result: every
+  // key of the top k lies in the kept subset, which the rank selection below
+  // orders when it is short (config 3: 168 kept; the bitonic over them took
+  // 8.6 us) and the bitonic network otherwise.
+  bool loaded = false;
+  if (PAY && (h || tail.n_reg) && m > kSelMin && k <= kSelMaxK && k < m)
+    loaded = select_compact(keys, idx, pay, M, m, k, sk, si, sp, m);
   if (m <= kRankMax) {
     // short lists (the common case: ~100-300 candidates): rank selection.
     // Every element's rank -- the count of smaller (key, index, position)
@@ -1174,13 +1210,15 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
     // one wave share an element (each counts every tpe-th pair, a butterfly
     // adds them): m / tpe dependent LDS reads per lane instead of m (one
     // lane per element: ~10 us at m = 110).
-    for (int i = tid; i < m; i += kSortThreads) {
-      const int64_t q = M(i);
-      sk[i] = ld_sc1(keys + q);
-      si[i] = ld_sc1(idx + q);
-      if (PAY) sp[i] = ld_sc1(pay + q);
+    if (!loaded) {  // (block-uniform)
+      for (int i = tid; i < m; i += kSortThreads) {
+        const int64_t q = M(i);
+        sk[i] = ld_sc1(keys + q);
+        si[i] = ld_sc1(idx + q);
+        if (PAY) sp[i] = ld_sc1(pay + q);
+      }
+      __syncthreads();
     }
-    __syncthreads();
     if (tail.clear) {  // every thread read the header above
       for (int64_t w = tid; w < tail.clear_words; w += kSortThreads) tail.clear[w] = 0u;
       for (int64_t w = tid; w < tail.clear2_words; w += kSortThreads) tail.clear2[w] = 0u;
@@ -1196,17 +1234,36 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
       const bool live = e < m;
       const unsigned long long ke = live ? sk[e] : 0ull;
       const long long ie = live ? si[e] : 0ll;
-      int r = 0;
+      // keys only (one 8-B read and two compares per pair); an element whose
+      // key occurs more than once (equal scores, the merge's NONE padding)
+      // is recounted on (key, index, position)
+      int r = 0, eq = 0;
       if (live) {
 #pragma unroll 4
         for (int j = part; j < m; j += tpe) {
           const unsigned long long kj = sk[j];
-          const long long ij = si[j];
-          // equal pairs (the merge's padding: NONE key, index -1) rank by position
-          r += kj < ke || (kj == ke && (ij < ie || (ij == ie && j < e)));
+          r += kj < ke;
+          eq += kj == ke;
         }
       }
-      for (int o = 1; o < tpe; o <<= 1) r += __shfl_xor(r, o);
+      for (int o = 1; o < tpe; o <<= 1) {
+        r += __shfl_xor(r, o);
+        eq += __shfl_xor(eq, o);
+      }
+      if (__ballot(live && eq > 1)) {  // (wave-uniform; rare)
+        const bool again = live && eq > 1;  // (the same for an element's tpe lanes)
+        int rr = 0;
+        if (again) {
+          for (int j = part; j < m; j += tpe) {
+            const unsigned long long kj = sk[j];
+            const long long ij = si[j];
+            // equal pairs (the merge's padding: NONE key, index -1) rank by position
+            rr += kj < ke || (kj == ke && (ij < ie || (ij == ie && j < e)));
+          }
+        }
+        for (int o = 1; o < tpe; o <<= 1) rr += __shfl_xor(rr, o);
+        if (again) r = rr;
+      }
       if (live && part == 0 && r < kk) {
         if (out_keys) out_keys[r] = ke;
         out_idx[r] = ie;
@@ -1230,9 +1287,6 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
     }
     return;
   }
-  bool loaded = false;
-  if (PAY && (h || tail.n_reg) && m > kSelMin && k <= kSelMaxK && k < m)
-    loaded = select_compact(keys, idx, pay, M, m, k, sk, si, sp, m);
   int mp = 2;
   while (mp < m) mp <<= 1;
   for (int i = tid; i < mp; i += kSortThreads) {

@@ -19,6 +19,9 @@ s = open(os.path.join(CSRC, "topk.hip")).read()
 # lists) instead of the first match, the region merge; stamp 14 after its
 # workspace clear
 RANK = os.environ.get("K3_TRACE_PATH") == "rank"
+# K3_TRACE_PATH=select: stamps 8 / 9 after the radix pre-selection and after
+# the bitonic sort of the long-list path (config 3), slot 15 the compacted count
+SELECT = os.environ.get("K3_TRACE_PATH") == "select"
 
 
 def sub(old, new, last=False):
@@ -73,6 +76,14 @@ if RANK:
     sub("""    int tpe = 1;  // lanes per element""", """    __syncthreads();
     K3T(14);
     int tpe = 1;  // lanes per element""")
+if SELECT:
+    sub("""    loaded = select_compact(keys, idx, pay, M, m, k, sk, si, sp, m);""",
+        """    loaded = select_compact(keys, idx, pay, M, m, k, sk, si, sp, m);
+  K3T(16);
+  if (threadIdx.x == 0) g_k3[15] = m;""")
+    sub("""  if (tail.clear) {  // every thread read the header before the first barrier above""",
+        """  K3T(17);
+  if (tail.clear) {  // every thread read the header before the first barrier above""")
 sub("""    if (PAY && h) {
       for (int64_t i = kk + tid; i < k; i += kSortThreads) {""", """    __syncthreads();
     K3T(9);
