@@ -64,14 +64,22 @@ sub("""  // the upper edge of the k-th key's bucket: >= the k-th group minimum, 
 sub("""  if constexpr (PAY) if (tail.n_reg > 1 && s_runs_sorted &&""", """  if (threadIdx.x == 0) g_k3[4] = m;
   K3T(7);
   if constexpr (PAY) if (tail.n_reg > 1 && s_runs_sorted &&""")
-sub("""      if (PAY) sp[i] = ld_sc1(pay + q);
+if RANK:
+    sub("""      __syncthreads();
+    }
+    if (tail.clear) {  // every thread read the header above""", """      __syncthreads();
+    }
+    K3T(8);
+    if (tail.clear) {  // every thread read the header above""")
+else:
+    sub("""      if (PAY) sp[i] = ld_sc1(pay + q);
     }
     __syncthreads();
     if (tail.clear) {  // every thread read the header above""", """      if (PAY) sp[i] = ld_sc1(pay + q);
     }
     __syncthreads();
     K3T(8);
-    if (tail.clear) {  // every thread read the header above""", last=RANK)
+    if (tail.clear) {  // every thread read the header above""")
 if RANK:
     sub("""    int tpe = 1;  // lanes per element""", """    __syncthreads();
     K3T(14);
