@@ -158,10 +158,17 @@ struct Cfg {
   // fragment, two MFMAs per k-step (KS 32 keeps its three-MFMA form)
   static constexpr bool PACK = SIG && KS >= 64;
   static constexpr int NCH = SIG ? 1 : 2;           // row-sum chains per row tile
+  // products summed by one row-chain element between two folds (the FOLD
+  // columns' tiles dealt over NCH chains, 2 KS products per tile): the length
+  // dal_density_error_bound_sym_d charges the row side with
+  static constexpr int CHAIN = FOLD / 16 / NCH * 2 * KS;
   static_assert(SPF >= 1 && SPP % SPF == 0 && PIECES >= 1 && NKS >= 1, "bad slice");
   static_assert(W == 4 || (W == 8 && KS >= 64), "two super blocks per block: KS >= 64 only");
   static_assert(!SIG || KS <= 128, "sigma partials: <= 32 values per lane");
+  static_assert(CHAIN <= 2048, "row chain longer than the density bound's worst case");
 };
+// the 8-wave form folds like the 4-wave one (one bound per KS)
+static_assert(Cfg<128, 8>::CHAIN == Cfg<128, 4>::CHAIN, "block forms must share the chain length");
 
 template <int KS, int W>
 __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
@@ -980,18 +987,34 @@ int split_ks(int64_t d_pad) { return d_pad == 32 ? 32 : (d_pad % 128 == 0 ? 128 
 
 using namespace dal;
 
-extern "C" double dal_density_error_bound_sym(int64_t n_cols) {
+namespace {
+// Row-side chain length of the kernel that runs d_pad (split_ks), 0 = the
+// longest over every KS.
+int row_chain_products(int64_t d_pad) {
+  if (d_pad <= 0) {
+    int m = Cfg<32, 4>::CHAIN;
+    m = Cfg<64, 4>::CHAIN > m ? Cfg<64, 4>::CHAIN : m;
+    return Cfg<128, 4>::CHAIN > m ? Cfg<128, 4>::CHAIN : m;
+  }
+  const int ks = split_ks(d_pad);
+  return ks == 32 ? Cfg<32, 4>::CHAIN : ks == 64 ? Cfg<64, 4>::CHAIN : Cfg<128, 4>::CHAIN;
+}
+}  // namespace
+
+extern "C" double dal_density_error_bound_sym_d(int64_t n_cols, int64_t d_pad) {
   // dal_gram_rowsum_sym + dal_gram_sym_residual against the canonical fp64
   // density, per density entry (one column j of row i), u = 2^-23 (a
   // conservative unit roundoff for the MFMA's internal fp32 adds, counted as
   // sequential adds), products exact (f16 x f16), c = 1 + 2^-8 >= sum_d |h_i
   // h_j| + |h_i l_j| over sum_d |u_i u_j| <= 1 (Cauchy-Schwarz on unit rows):
-  //   row side   one chain per row tile of <= 8 (KS 128) / 16 (KS 64) tiles x
-  //              2 KS products (16 tiles x 64 at KS 32), <= 1024 products, and
-  //              4 cross-lane adds: gamma_1029 * c
+  //   row side   one chain per row tile between folds: Cfg<KS>::CHAIN
+  //              products (FOLD / 16 / NCH tiles x 2 KS: 1,024 at KS 32,
+  //              2,048 at KS 64 and 128 with the sigma column sums, one chain
+  //              per row tile), then 4 cross-lane adds (+1 with two chains):
+  //              gamma_(CHAIN + 5) * c
   //   column side  sigma_P MFMAs: sigma_P = the fp32 sum of the super block's
   //              H rows (8 row tiles, 4 DPP steps, 4 waves: <= 15 adds), split
-  //              into two fp16 terms (2^-22), then <ũ_j, sigma_P> over KS
+  //              into two fp16 terms (2^-22), then <u~_j, sigma_P> over KS
   //              features -- KS >= 64: the two terms as rows of one A fragment,
   //              2 x KS products, each row rounded to 2^-32: (gamma_15 +
   //              gamma_256 + 3 * 2^-22) * c at KS 128; KS 32 (three MFMAs per
@@ -1003,13 +1026,19 @@ extern "C" double dal_density_error_bound_sym(int64_t n_cols) {
   const double u = 1.0 / 8388608.0;  // 2^-23
   auto gamma = [u](double n) { return n * u / (1.0 - n * u); };
   const double s = 1.0 / 4194304.0;  // 2^-22
-  const double row = gamma(1029.0);
+  const double row = gamma(static_cast<double>(row_chain_products(d_pad)) + 5.0);
   const double col_growth = 8.0 * gamma(128.0) + 15.0 * gamma(15.0) + u;
   const double col_sigma = (gamma(22.0) > gamma(15.0) ? gamma(22.0) : gamma(15.0)) + gamma(256.0) + 3.0 * s;
-  const double col = col_growth > col_sigma ? col_growth : col_sigma;
+  // (the chain-growth column form runs only at KS >= 64 with DAL_GRAM_SIGMA_COLS = 0)
+  const bool growth = !Cfg<128, 4>::SIG && (d_pad <= 0 || split_ks(d_pad) >= 64);
+  const double col = growth && col_growth > col_sigma ? col_growth : col_sigma;
   const double c = 1.0 + 1.0 / 256.0;
   return ((row > col ? row : col) * c + 5.0 * s + 1e-10) * static_cast<double>(n_cols) + 1e-9;
 }
+
+// Feature-width-free form (ABI v5): the bound of the longest row chain of any
+// KS, valid for every pool.
+extern "C" double dal_density_error_bound_sym(int64_t n_cols) { return dal_density_error_bound_sym_d(n_cols, 0); }
 
 extern "C" int dal_gram_rowsum_sym_skip(const uint16_t* rows, int64_t row_block0, int64_t n_row_blocks,
                                         const uint16_t* cols, int64_t col_block0, int64_t j_lo, int64_t j_hi,

@@ -62,6 +62,7 @@ SIGNATURES = {
     "dal_prep_split": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64, c_int64,
                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "dal_density_error_bound_sym": (c_double, [c_int64]),
+    "dal_density_error_bound_sym_d": (c_double, [c_int64, c_int64]),
     "dal_gram_rowsum_sym": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64, c_int64,
                                     c_int64, c_int64, c_void_p, c_int, c_void_p]),
     "dal_gram_rowsum_sym_skip": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64, c_int64,

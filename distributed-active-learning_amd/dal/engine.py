@@ -572,7 +572,7 @@ def density_error(state: PoolState) -> float:
     lib = _lib.load()
     if state.gram == "f32":
         return float(lib.dal_density_error_bound(n_cols))
-    return float(lib.dal_density_error_bound_sym(n_cols))
+    return float(lib.dal_density_error_bound_sym_d(n_cols, state.d_pad))
 
 
 def candidate_cap(n: int, k: int) -> int:

@@ -203,6 +203,12 @@ size_t dal_gram_sym_residual_workspace_bytes(int64_t nb_active, int64_t n_row_bl
 int dal_gram_sym_residual(const uint16_t* ops, int64_t nb_active, int64_t row_block0, int64_t n_row_blocks,
                           int64_t d_pad, int64_t* acc, void* ws, size_t ws_bytes, dal_stream_t stream);
 double dal_density_error_bound_sym(int64_t n_cols);
+/* The same bound for the kernel that runs features padded to d_pad (ABI v8):
+ * the row-side chain length depends on the slice width KS (1,024 products at
+ * KS 32, 2,048 at KS 64 / 128); dal_density_error_bound_sym(n) ==
+ * dal_density_error_bound_sym_d(n, 0) is the longest chain's, valid for any
+ * d_pad. */
+double dal_density_error_bound_sym_d(int64_t n_cols, int64_t d_pad);
 
 /* ---- (a5-a10) forest votes + uncertainty / density-weighted score ------
  * Replaces uncertainty_sampling.py:88-98 / density_weighting.py:136-167:

@@ -36,7 +36,7 @@ def test_library_exports_every_header_symbol():
 
 def test_host_helpers():
     lib = _lib.load()
-    assert lib.dal_abi_version() == 7
+    assert lib.dal_abi_version() == 8
     assert lib.dal_pad_rows(1) == 512 and lib.dal_pad_rows(100000) == 100352
     assert [lib.dal_pad_features(d) for d in (1, 30, 33, 64, 65, 128, 129, 256, 500, 784)] == \
         [32, 32, 64, 64, 128, 128, 256, 256, 512, 1024]
@@ -44,7 +44,21 @@ def test_host_helpers():
     b = lib.dal_density_error_bound(100000)
     assert 1.0 < b < 10.0  # ~3.1e-5 * N
     bsym = lib.dal_density_error_bound_sym(100000)
-    assert b < bsym < 20.0  # ~1.25e-4 * N (chains of <= 1,024 fp32 adds, conservative MFMA model)
+    assert b < bsym < 30.0  # ~2.45e-4 * N (chains of <= 2,048 fp32 adds, conservative MFMA model)
+    # row-side chain by slice width (one chain per row tile at KS
+    # 64 / 128 sums 2,048 products between folds, KS 32 1,024)
+    u = 2.0 ** -23
+    c = 1.0 + 1.0 / 256.0
+
+    def expect(chain, n):
+        g = (chain + 5) * u / (1 - (chain + 5) * u)
+        return (g * c + 5 * 2.0 ** -22 + 1e-10) * n + 1e-9
+
+    for d_pad, chain in ((32, 1024), (64, 2048), (128, 2048), (256, 2048), (0, 2048)):
+        got = lib.dal_density_error_bound_sym_d(100000, d_pad)
+        assert abs(got - expect(chain, 100000)) <= 1e-12 * got, (d_pad, got)
+    assert lib.dal_density_error_bound_sym_d(100000, 0) == bsym
+    assert lib.dal_density_error_bound_sym_d(100000, 32) < bsym
     assert lib.dal_gram_sym_residual_workspace_bytes(392, 392, 64) == 2 * 196 * 64 * 8 + 2 * 196 * 64 * 8
     assert lib.dal_gram_sym_residual_workspace_bytes(0, 2, 64) == 0
     assert lib.dal_split_f16_halves(512, 64) == 512 * 128
