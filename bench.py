@@ -18,6 +18,10 @@ selection of the exact separable density path on the same pool.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py launches its
+own N ranks (child processes, 127.0.0.1 rendezvous) before any GPU call and
+re-prints rank 0's output, headline last; under torchrun it runs as one rank.
+
 Output (rank 0): one compact JSON line per extra workload ({"extra": label,
 ...}, <= 1 KB each), then the compact headline as the LAST stdout line
 (<= 4 KB: metric, value, roofline, cpu_baseline, self-checks, world size).
@@ -902,7 +906,81 @@ def emit(out: dict, path: str | None):
     print(json.dumps(headline(out)), flush=True)
 
 
+# ------------------------------------------------------------ launcher --
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n: int, cmd: list, env: dict | None = None, poll_s: float = 0.05) -> int:
+    """Run ``cmd`` as ``n`` ranks of one node (the self-launch of
+    ``bench.py --gpus N`` when no outside launcher set WORLD_SIZE).
+
+    The parent never touches the GPU: it starts ``n`` child processes (never an
+    exec of itself) with RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE and a
+    127.0.0.1 rendezvous, forwards rank 0's stdout line by line to its own
+    stdout (so rank 0's headline stays the LAST stdout line) and every other
+    rank's stdout to stderr.  When a rank exits nonzero the others are
+    terminated (they would wait in a collective) and the parent returns that
+    rank's exit code (a signal -s as 128 + s); 0 when all ranks exit 0."""
+    import subprocess
+    import threading
+
+    base = dict(os.environ if env is None else env)
+    base.setdefault("MASTER_ADDR", "127.0.0.1")
+    base["MASTER_PORT"] = str(base.get("DAL_BENCH_MASTER_PORT") or _free_port())
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", ROLE_RANK=str(r))
+        procs.append(subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE, text=True, bufsize=1))
+
+    def pump(p, dst):
+        for line in p.stdout:
+            dst.write(line)
+            dst.flush()
+
+    pumps = [threading.Thread(target=pump, args=(p, sys.stdout if r == 0 else sys.stderr), daemon=True)
+             for r, p in enumerate(procs)]
+    for t in pumps:
+        t.start()
+    rc = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.discard(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print(f"bench launcher: rank {r} exited with {c}; stopping the other ranks", file=sys.stderr)
+                for q in live:
+                    procs[q].terminate()
+        if live:
+            time.sleep(poll_s)
+    for r, p in enumerate(procs):
+        if p.returncode is None:  # (terminated above and still not reaped)
+            p.kill()
+            p.wait()
+    for t in pumps:
+        t.join(timeout=10)
+    return rc
+
+
 def main():
+    # --gpus N > 1 without an outside launcher (no WORLD_SIZE in the
+    # environment): start N ranks as child processes before anything here
+    # touches torch or the GPU, and exit with their status
+    if "WORLD_SIZE" not in os.environ:
+        pre = argparse.ArgumentParser(add_help=False)
+        pre.add_argument("--gpus", type=int, default=1)
+        ngpus = pre.parse_known_args()[0].gpus
+        if ngpus > 1:
+            sys.exit(launch_ranks(ngpus, [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]))
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="timed steps (default: config 4: 5, else 50)")
@@ -933,8 +1011,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if world != args.gpus:  # (an outside launcher set a different WORLD_SIZE)
+        raise SystemExit(f"--gpus {args.gpus} but the launcher's WORLD_SIZE={world}")
     # DAL_BENCH_BACKEND=gloo rehearses the multi-process path with several
     # ranks on one GPU (all-gathers staged through the host); default: RCCL.
     backend = os.environ.get("DAL_BENCH_BACKEND", "nccl")

@@ -11,6 +11,8 @@
 #                         (full result: gpurun_out/bench_full_<n>.json)
 #   gloo=N[=ARGS]         bench.py on N gloo ranks sharing the one GPU (torch.distributed.run)
 #                         -> gpurun_out/gloo_<n>.log
+#   selfgloo=N[=ARGS]     bench.py --gpus N on gloo with NO outside launcher (bench.py starts its ranks)
+#                         -> gpurun_out/selfgloo_<n>.log
 #   stats=TAG[=ARGS]      rocprofv3 --kernel-trace --stats of bench.py ARGS -> gpurun_out/prof_TAG/
 #   pmc=TAG=CTRS[=ARGS]   rocprofv3 --pmc CTRS (',' = space) of bench.py ARGS -> gpurun_out/pmc_TAG/
 #   pmcpy=TAG=CTRS=SCRIPT[=ARGS]  rocprofv3 --pmc CTRS of python SCRIPT ARGS -> gpurun_out/pmc_TAG/
@@ -57,6 +59,16 @@ for step in "$@"; do
       rc=$?
       echo "[$n] gloo $np ${args//,/ } rc=$rc"
       tail -1 gpurun_out/gloo_$n.log | cut -c1-600
+      ;;
+    selfgloo)
+      np=${rest%%=*}
+      args=""
+      [[ "$rest" == *=* ]] && args=${rest#*=}
+      env -u WORLD_SIZE DAL_BENCH_BACKEND=gloo timeout -k 10 900 python -u bench.py --gpus $np \
+        ${args//,/ } --out gpurun_out/selfgloo_full_$n.json > gpurun_out/selfgloo_$n.log 2>&1
+      rc=$?
+      echo "[$n] selfgloo $np ${args//,/ } rc=$rc"
+      tail -1 gpurun_out/selfgloo_$n.log | cut -c1-600
       ;;
     stats)
       tag=${rest%%=*}
