@@ -1712,25 +1712,37 @@ __global__ __launch_bounds__(kSumThreads) void summary_select_kernel(
       st_sc1(AR.ckey + reg0 + c, static_cast<uint64_t>(key));
     }
   };
+  // Every listed row is < n by construction (the scan writes slot p < kept
+  // only, nc <= kept is read after the barrier above).  The row is still
+  // checked before it forms an address (x + i * ldx, norm64, votes, flags): a
+  // slot read before its write -- the round-4 work-in-progress aperture
+  // violation ("Aperture violation") -- then costs a
+  // DAL_FLAG_SAMPLE_MISS (exact re-run) instead of a wild load.
+  auto row_ok = [&](int64_t i) { return static_cast<uint64_t>(i) < static_cast<uint64_t>(n); };
   if (nc <= kWaveScoreMax * W) {  // (block-uniform)
     __shared__ __attribute__((aligned(16))) double s_tr[DW ? W : 1][64];
     for (int c = w; c < nc; c += W) {  // (wave-uniform)
       const int64_t i = s_cand[c];
-      double sc;
-      const bool ok = dw_canonical_score_wave(AR.R, i, sc, s_tr[DW ? w : 0], lut_lane, n_lut);
+      double sc = __builtin_nan("");
+      bool ok = false;
+      if (row_ok(i)) ok = dw_canonical_score_wave(AR.R, i, sc, s_tr[DW ? w : 0], lut_lane, n_lut);
+      else if (lane == 0) atomicOr(tail.status, DAL_FLAG_SAMPLE_MISS);
       if (lane == 0) put(c, i, sc, ok);
     }
   } else {
     for (int c0 = 0; c0 < nc; c0 += kSumThreads) {  // (block-uniform trip count)
       const int c = c0 + tid;  // packed: as few waves as hold them, waves 0-3 on four SIMDs
-      const bool live = c < nc;
-      const int64_t i = live ? s_cand[c] : 0;
+      const int64_t i = c < nc ? s_cand[c] : 0;
+      const bool live = c < nc && row_ok(i);
+      if (c < nc && !live) atomicOr(tail.status, DAL_FLAG_SAMPLE_MISS);
       const int v = live ? AR.R.votes[i] : 0;
       const double e = n_lut ? __shfl(lut_lane, v) : 0.0;  // (every lane takes part)
       if (live) {
         double sc;
         const bool ok = dw_canonical_score_lane<DAL_K3_LANE_CHUNK>(AR.R, i, sc, e, n_lut);
         put(c, i, sc, ok);
+      } else if (c < nc) {
+        put(c, i, __builtin_nan(""), false);
       }
     }
   }
@@ -1819,6 +1831,14 @@ int summary_grid(int64_t ng) {
   if (g > kMaxRegions) g = kMaxRegions;
   if (g < 1) g = 1;
   return static_cast<int>(g);
+}
+// The LDS lists of summary_select_kernel hold a block's groups (s_hits:
+// kMaxGroups / 32) and its regions' counts (kMaxRegions): a grid / group
+// summary outside them is rejected on the host before the launch.
+bool summary_shape_ok(const GroupSummary& S, int G, int64_t cap) {
+  if (S.ng < 1 || S.ng > kMaxGroups || S.group_rows < 1 || G < 1 || G > kMaxRegions) return false;
+  if (ceil_div(S.ng, static_cast<int64_t>(G)) > kMaxGroups / 32) return false;
+  return cap >= 1 && cap <= DAL_SORT_CAP_PAYLOAD;
 }
 
 // Radix passes 0 .. passes-1 (zero: clear the header first).
@@ -1961,6 +1981,7 @@ static int launch_fast_level1(const uint64_t* keys_lo, const uint64_t* keys_hi, 
   tail.clear = reinterpret_cast<uint32_t*>(h1);
   tail.clear_words = kFastHdrWords;
   const int G = summary_grid(S.ng);
+  if (!summary_shape_ok(S, G, cap)) return DAL_ERR_SHAPE;
   AppendRerank A = AR;
   int64_t* cidx = reinterpret_cast<int64_t*>(base + W.L1.cidx);
   if (DW) {  // candidates in per-block regions, gathered by the last block
@@ -2167,6 +2188,7 @@ int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_
   tail.out_slot = out_slot;
   tail.status_mirror = status_mirror;
   const int G = summary_grid(S.ng);
+  if (!summary_shape_ok(S, G, cap)) return DAL_ERR_SHAPE;
   const DwRegions Rg = dw_regions(ws, W, cap);
   set_regions(tail, h1, cap, G);
   hipLaunchKernelGGL(summary_select_kernel<true>, dim3(static_cast<unsigned>(G)), dim3(kSumThreads), 0, st, keys_hi,

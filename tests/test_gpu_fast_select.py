@@ -380,3 +380,82 @@ def test_topk_merge_packed(cuda, n_ranks, k, pad):
         assert np.array_equal(oi.cpu().numpy(), I[want])
         assert np.array_equal(os_.cpu().numpy().view(np.int64), S[want].view(np.int64))
         assert st == sum(1 << r for r in range(min(n_ranks, 3)))
+
+
+def _crafted_select(cuda, n, d, special, key_special, k, cap, seed=29):
+    """dal_dw_select's fast level 1 on crafted interval keys: the rows in
+    ``special`` carry the point key ``key_special``, every other row a larger
+    one, so tau = key_special and exactly those rows are candidates.  Returns
+    (selected indices, scores, status, expected indices, expected scores) --
+    the expectation is the canonical fp64 top-k over the special rows."""
+    import torch
+
+    from dal import _lib, engine
+    from dal._lib import call
+
+    X = O.synthetic_pool(n, d, seed=seed)
+    E = np.arange(10)
+    st = engine.PoolState(X, excluded=E, device=cuda)
+    colsum, norm64 = st.colsum(), st.norms()
+    flags, _, _ = st.row_flags(np.arange(10, n))
+    rng = np.random.default_rng(seed)
+    votes_h = rng.integers(0, 11, size=n).astype(np.int32)
+    lut_h = O.lut_entropy(10)
+    keys_h = np.full(n, key_special + 1000, dtype=np.uint64)
+    keys_h[special] = key_special
+    keys = torch.from_numpy(keys_h.view(np.int64)).to(cuda)
+    votes = torch.from_numpy(votes_h).to(cuda)
+    lut = torch.from_numpy(lut_h).to(cuda)
+    lib = _lib.load()
+    wsb = int(lib.dal_dw_select_workspace_bytes(n, k, cap))
+    ws, wsp = engine.workspace(wsb, cuda)
+    ws.zero_()
+    out_i = torch.empty(k, dtype=torch.int64, device=cuda)
+    out_s = torch.empty(k, dtype=torch.float64, device=cuda)
+    st.status.zero_()
+    P = lambda t: t.data_ptr()  # noqa: E731
+    call("dal_dw_select", P(keys), P(keys), P(votes), P(flags), n, k, 0, P(lut), 1.0, P(st.x), d, d, P(norm64),
+         P(colsum), cap, 1, wsp, wsb, P(out_i), P(out_s), 0, P(st.status), 0,
+         torch.cuda.current_stream(cuda).cuda_stream)
+    status = int(st.status.item())
+    dens = O.density_canonical(X, excluded=E)
+    sc = lut_h[votes_h[special]] * dens[special]
+    sc = np.where(np.isnan(sc), -np.inf, sc)
+    order = np.lexsort((special, -sc))[:k]
+    return out_i.cpu().numpy(), out_s.cpu().numpy(), status, np.asarray(special)[order], \
+        (lut_h[votes_h] * dens)[np.asarray(special)[order]]
+
+
+@pytest.mark.parametrize("layout,extra", [("per_group", 0), ("per_group", -1), ("one_region", 0),
+                                          ("one_region", -1), ("local_sort_edge", 0)])
+def test_fast_level1_region_and_capacity_boundaries(cuda, layout, extra):
+    """The aperture-violation boundary shapes (DESIGN K3): 4,096 row groups
+    of 64 rows, so summary_select_kernel runs its maximum of 128 blocks /
+    candidate regions, with the candidate count exactly at ``cap`` (selection
+    exact, no flag) and one past it (DAL_FLAG_SAMPLE_MISS, nothing read
+    outside its region): one candidate in every group (every region 32), all
+    candidates in one region (region count == cap), and regions of 256 / 257
+    candidates (the local rank sort's limit)."""
+    from dal import _lib
+
+    n, d, gr = 4096 * 64, 16, 64
+    if layout == "per_group":
+        special = np.arange(4096) * gr + 17  # one per group: 128 regions x 32
+        k = 100
+    elif layout == "one_region":
+        special = np.arange(10, 32 * gr)  # every row of block 0's 32 groups but E
+        k = 10
+    else:
+        special = np.concatenate([np.arange(10, 10 + 256), 32 * gr + np.arange(257),
+                                  np.arange(64, 4096) * gr + 5])  # block 0: 256, block 1: 257, then 32 each
+        k = 300
+    cap = len(special) + extra
+    if cap > _lib.DAL_SORT_CAP_PAYLOAD:
+        pytest.skip("capacity above the fast level 1's one-block sort")
+    idx, sc, status, ref_idx, ref_sc = _crafted_select(cuda, n, d, special, 1 << 40, k, cap)
+    if extra < 0:
+        assert status & _lib.DAL_FLAG_SAMPLE_MISS
+        return
+    assert status == 0
+    assert np.array_equal(idx, ref_idx)
+    assert np.array_equal(sc.view(np.int64), ref_sc.view(np.int64))
