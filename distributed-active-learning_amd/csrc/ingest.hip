@@ -19,6 +19,7 @@
 
 #include <cerrno>
 #include <cstdlib>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -72,24 +73,33 @@ locale_t c_numeric_locale() {
   return loc;
 }
 
-// Copy token [a, b) into buf (NUL-terminated) without its PEP 515 digit-group
-// underscores, as Python's float() / int() read them ("1_000.5" = 1000.5):
-// an underscore must sit between two digits, anything else rejects the token.
-bool copy_token(const char* t, size_t a, size_t b, char* buf, size_t cap) {
+// Copy token [a, b) into a NUL-terminated buffer without its PEP 515
+// digit-group underscores, as Python's float() / int() read them ("1_000.5" =
+// 1000.5): an underscore must sit between two digits, anything else rejects
+// the token, and so does a NUL byte (not a field delimiter; float('1\x00')
+// raises).  Tokens that do not fit the caller's stack buffer go to ``big``
+// (float() takes any length: a 200-digit field is inf after the fp32 narrowing).
+const char* copy_token(const char* t, size_t a, size_t b, char* buf, size_t cap, std::string& big) {
   const size_t n = b - a;
-  if (n == 0 || n >= cap) return false;
+  if (n == 0) return nullptr;
+  char* dst = buf;
+  if (n >= cap) {
+    big.assign(n + 1, '\0');
+    dst = &big[0];
+  }
   size_t m = 0;
   for (size_t i = 0; i < n; ++i) {
     const char c = t[a + i];
+    if (c == 0) return nullptr;  // an embedded NUL would end strtod early: float() rejects the token
     if (c == '_') {
       const bool ok = i > 0 && i + 1 < n && is_digit(t[a + i - 1]) && is_digit(t[a + i + 1]);
-      if (!ok) return false;
+      if (!ok) return nullptr;
       continue;
     }
-    buf[m++] = c;
+    dst[m++] = c;
   }
-  buf[m] = 0;
-  return true;
+  dst[m] = 0;
+  return dst;
 }
 
 // Parse one field [a, b) as fp64 (the token must be consumed entirely).
@@ -100,24 +110,32 @@ bool copy_token(const char* t, size_t a, size_t b, char* buf, size_t cap) {
 // carries the surrounding whitespace float() would strip.
 bool parse_double(const char* t, size_t a, size_t b, double& v) {
   char buf[128];
+  std::string big;
   for (size_t i = a; i < b; ++i)
     if (t[i] == 'x' || t[i] == 'X' || t[i] == '(') return false;
-  if (!copy_token(t, a, b, buf, sizeof(buf))) return false;
+  const char* s = copy_token(t, a, b, buf, sizeof(buf), big);
+  if (!s) return false;
   const locale_t loc = c_numeric_locale();
   if (!loc) return false;
   char* end = nullptr;
   errno = 0;
-  v = strtod_l(buf, &end, loc);
-  return end != buf && *end == 0;
+  v = strtod_l(s, &end, loc);
+  return end != s && *end == 0;
 }
 
-bool parse_int(const char* t, size_t a, size_t b, long long& v) {
+// An integer field as Python's int() reads it (sign, digits, underscores).
+// Out of the int64 range: ``huge`` is set and v is unusable (int() still
+// reads it, so the reference map -- -1 or not -- can be applied).
+bool parse_int(const char* t, size_t a, size_t b, long long& v, bool& huge) {
   char buf[64];
-  if (!copy_token(t, a, b, buf, sizeof(buf))) return false;
+  std::string big;
+  const char* s = copy_token(t, a, b, buf, sizeof(buf), big);
+  if (!s) return false;
   char* end = nullptr;
   errno = 0;
-  v = std::strtoll(buf, &end, 10);
-  return end != buf && *end == 0 && errno == 0;
+  v = std::strtoll(s, &end, 10);
+  huge = errno == ERANGE;
+  return end != s && *end == 0 && (errno == 0 || huge);
 }
 
 // Parse the rows of [a, b) into x[row0..], labels[row0..]; stops after
@@ -144,8 +162,10 @@ int parse_range(const char* t, size_t a, size_t b, int64_t row0, int64_t max_row
         x[r * (cols - 1) + f] = static_cast<float>(v);
       } else {
         long long lab;
-        if (!parse_int(t, p, q, lab)) return DAL_ERR_ARG;
-        labels[r] = label_map == 0 ? (lab == -1 ? 0 : 1) : lab;
+        bool huge = false;
+        if (!parse_int(t, p, q, lab, huge)) return DAL_ERR_ARG;
+        if (huge && label_map != 0) return DAL_ERR_ARG;  // an as-is label must fit int64
+        labels[r] = label_map == 0 ? (!huge && lab == -1 ? 0 : 1) : lab;
       }
       ++f;
       p = q;

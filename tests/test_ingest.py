@@ -200,3 +200,22 @@ def test_load_pool_pinned_upload_and_select(cuda, tmp_path):
     sel = us.select(x_dev, unl, F, 50, device=cuda)
     _, ref_idx, _ = O.uncertainty_select(ref_x, unl, of, 50)
     assert np.array_equal(sel.indices.cpu().numpy(), ref_idx)
+
+
+def test_parse_long_tokens_huge_labels_and_nul(tmp_path):
+    """Tokens longer than the parser's stack buffer, labels beyond int64 and
+    embedded NUL bytes read as the reference's float() / int() read them
+    (NUL: rejected; a huge label is not -1 -> 1)."""
+    from dal import _lib
+    from dal.ingest import parse_labeled_text
+
+    p = tmp_path / "long.txt"
+    p.write_text("1 " + "9" * 200 + " 1\n" + "1_" * 150 + "1 2 " + "9" * 80 + "\n3 4 -" + "0" * 70 + "1\n")
+    got_x, got_y = parse_labeled_text(str(p))
+    ref_x, ref_y = _ref_parse(str(p))
+    assert np.array_equal(got_x.view(np.int32), ref_x.view(np.int32))
+    assert np.array_equal(got_y, ref_y)
+    for text in ("1 2\x00abc 1\n", "1 2 1\x00\n"):
+        p.write_bytes(text.encode())
+        with pytest.raises(_lib.DalError):
+            parse_labeled_text(str(p))
