@@ -225,15 +225,21 @@ class ShardedSelector:
             ev = self._event_start("all_gather")
             parts_full, pwork = comm.all_gather_start(parts) if parts is not None else (None, None)
             u_full, work = comm.all_gather_start(u_local)
-            if ev is not None and work is None and pwork is None:  # staged (gloo): already complete
-                self._event_end(ev)
+            if ev is not None:
+                if work is None and pwork is None:  # staged (gloo): already complete
+                    self._event_end(ev)
+                else:  # the end on a side stream that waits for the collectives only (not the Gram below)
+                    side = _side_stream(st.device)
+                    side.wait_stream(torch.cuda.current_stream(st.device))
+                    with torch.cuda.stream(side):
+                        comm.wait(work)
+                        comm.wait(pwork)
+                        self._event_end(ev)
                 ev = None
             if st.n:
                 st.gram_accumulate(acc, u_local, self.shard, col_row0=self.lo)
             comm.wait(work)
             comm.wait(pwork)
-            if ev is not None:
-                self._event_end(ev)
         if st.n and self.world > 1:
             if st.gram == "sym":  # one launch over every other column
                 st.gram_accumulate(acc, u_full, self.world * self.shard, col_row0=0,

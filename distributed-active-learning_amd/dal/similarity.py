@@ -160,7 +160,7 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
     _lib.call("dal_max_cosine_unit", _ptr(x), n, d, _ptr(lab.unit16), lab.m_pad, _ptr(mx), _ptr(status),
               _stream(dev))
     bound = float(lib.dal_maxcos_unit_error_bound(d))
-    tight = d not in (64, 128, 256)  # the bf16 kernel's shapes; elsewhere the unit values are final
+    tight = False  # the values are the folded kernel's until a candidate overflow asks for the tighter ones
     in_range = None  # device count of the candidates inside this shard (read with the status)
     if candidates is None:
         flags = torch.full((n,), DAL_ROW_CANDIDATE, dtype=torch.uint8, device=dev)
@@ -214,9 +214,15 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
             passes = LEVEL1_PASSES if cap <= _lib.DAL_SORT_CAP_PAYLOAD else 0
             status.zero_()
             continue
-        if not tight and st & (DAL_FLAG_SAMPLE_MISS | DAL_FLAG_CAND_OVERFLOW):
-            # too many rows within the folded kernel's bound of the boundary:
-            # the bf16 kernel's values (bound ~1000x tighter) and their keys
+        if st & DAL_FLAG_SAMPLE_MISS and passes > 0:  # the fast level 1 overflowed: exact level 1 first
+            passes = 0
+            status.zero_()
+            continue
+        if not tight and st & DAL_FLAG_CAND_OVERFLOW:
+            # the exact level 1 also holds too many rows within the folded
+            # kernel's bound of the boundary: the bf16 kernel's values (bound
+            # ~1000x tighter) and their keys -- not for a fast-level-1 miss alone
+            # (identical rows: a tighter bound cannot separate them)
             tight = True
             status.zero_()
             _lib.call("dal_max_cosine", _ptr(x), n, d, _ptr(lab.rows), lab.m_pad, _ptr(lab.inv), 0, _ptr(mx), 0,
@@ -224,10 +230,6 @@ def diversity_select(pool, labeled_idx, k: int, candidates=None, device=None, ro
             bound = float(lib.dal_maxcos_error_bound(d))
             _lib.call("dal_interval_keys_f32", _ptr(mx), n, bound, _ptr(flags), DAL_ASCENDING, _ptr(lo), _ptr(hi),
                       _stream(dev))
-            continue
-        if st & DAL_FLAG_SAMPLE_MISS:  # the fast level 1 overflowed: exact level 1
-            passes = 0
-            status.zero_()
             continue
         if cap >= n or not (st & DAL_FLAG_CAND_OVERFLOW):
             break
