@@ -6,7 +6,7 @@ One step = one cold query-selection iteration of density_weighting.py
 pool already resident in HBM: row L2-normalise -> fused symmetric MFMA Gram
 row-sum (density) -> forest votes + score -> exact top-k with fp64 re-rank.
 Nothing is cached across timed steps.  With N > 1 the pool is row-sharded
-(strong scaling: the same pool on every N) and the two exchanges run over RCCL.
+(strong scaling: the same pool on every N) and the two all-gathers run over RCCL.
 
 Default workload (N = 1 and N > 1): BASELINE config 4, the north-star pool
 (2,000,000 x 256 U[0,1) fp32 from numpy default_rng(0), the BASELINE.md pool),
@@ -478,11 +478,9 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
     if world > 1:  # the density exchange's collectives, per step, and their max over ranks
         xev, sel.exchange_events = sel.exchange_events, None
         ag_ms = sum(a.elapsed_time(b) for nm, a, b in xev if nm == "all_gather") / max(steps, 1)
-        rs_ms = sum(a.elapsed_time(b) for nm, a, b in xev if nm == "reduce_scatter") / max(steps, 1)
         gram_min = -_max_over_ranks([-gram_ms], world, dist, tdev)[0]
-        g_max, ag_max, rs_max = _max_over_ranks([gram_ms, ag_ms, rs_ms], world, dist, tdev)
-        ranks = {"gram_ms_max": g_max, "gram_ms_min": gram_min, "all_gather_ms_max": ag_max,
-                 "reduce_scatter_ms_max": rs_max}
+        g_max, ag_max = _max_over_ranks([gram_ms, ag_ms], world, dist, tdev)
+        ranks = {"gram_ms_max": g_max, "gram_ms_min": gram_min, "all_gather_ms_max": ag_max}
     elapsed, gram_ms_max = _max_over_ranks([elapsed, gram_ms], world, dist, tdev)
 
     # accuracy (outside the timed region): the timed step's

@@ -12,37 +12,41 @@
 // units of 2^-24.  Layout [n_pad][d_pad / KS][KS H | KS L].
 //
 // Symmetry.  Rows are grouped in 512-row super blocks.  Each unordered pair
-// {P, Q} is multiplied once: P takes Q iff Q == P (diagonal: row sums only),
-// Q > P with P+Q even, or Q < P with P+Q odd (global indices, so the bits do
-// not depend on the sharding).  The taker's rows are the A operand (register
-// resident), Q's the B operand (LDS-staged); the tile's row sums go to P's rows
-// and its column sums to Q's rows.
+// {P, Q} is multiplied once: P takes Q iff Q == P (diagonal), Q > P with P+Q
+// even, or Q < P with P+Q odd (global indices, so the bits do not depend on
+// the sharding).  The taker's rows are the A operand (register resident), Q's
+// the B operand (LDS-staged); the kernel keeps the tile's ROW sums (-> P's
+// rows).  The tile's column sums (-> Q's rows) are linear in P's rows,
+// sum_{i in P} <H_i, u~_j> = <sigma^H_P, u~_j>, so they are added in closed
+// form with the residual below (round 5; before, as sigma_P MFMAs and int64
+// column flushes per pair).
 //
-// Compensation.  The A side holds H only: the MFMAs form T_ij = <H_i, u~_j>
-// (two products per feature pair, H.H and H.L), and the exact remainder
-// <L_i, u~_j> of every taken pair is added afterwards in closed form -- for a
-// row r of super block B (dal_gram_sym_residual):
-//   row role (B takes Q):         sum_Q <L_r, sigma~_Q>       = <L_r, R_B>
-//   column role (P takes B, P!=B): sum_P <u~_r, sigma^L_P>     = <u~_r, C_B>
-// with sigma~_Q / sigma^L_Q the sums of u~ / L over Q's rows (exact int64 in
-// units of 2^-24) and R_B, C_B their sums over B's partners (parity-class
-// prefix sums).  d_i is then sum_j <u~_i, u~_j> with nothing dropped: the MFMA
-// work per algorithmic product is 2 fp16 products on half the pairs.
+// Compensation and column sums.  The A side holds H only: the MFMAs form
+// T_ij = <H_i, u~_j> (two products per feature pair, H.H and H.L).  For a row
+// r of super block B, dal_gram_sym_residual adds in closed form
+//   row role (B takes Q):          sum_Q <L_r, sigma~_Q>   = <L_r, R_B>
+//   column role (P takes B, P!=B): sum_P <u~_r, sigma~_P>  = <u~_r, C_B>
+// (the column role: the pair's column sums <sigma^H_P, u~_r> plus the
+// remainder <sigma^L_P, u~_r>) with sigma~_Q the sum of u~ over Q's rows
+// (exact int64 in units of 2^-24) and R_B, C_B its sums over B's partners
+// (parity-class prefix sums).  d_i is then sum_j <u~_i, u~_j> with nothing
+// dropped; the MFMA work per algorithmic product is 2 fp16 products on half
+// the pairs, and each row's density is written only by its own rows' launches
+// (no cross-GPU sum).
 //
 // Exactness of the row sums (as the earlier kernels): chains are folded to
 // multiples of 2^-32 and added as integers (LDS fp64 below 2^53, int64
 // atomics); the residual is an fp64 dot in a fixed order rounded to 2^-32.
 // The density bits are identical for any grid, column split or GPU count.
 //
-// MI355X design: block = 4 waves x 128 rows (one super block), A fragments
-// (8 row tiles x KS features of H) in registers; 32 KiB B stages in a 2-deep
-// LDS ring filled by global_load_lds_dwordx4 (source-side XOR swizzle ->
-// conflict-free ds_read_b128); two blocks per CU (two waves per SIMD).  Per
-// 16x16 output tile two accumulator chains per row tile (even / odd column
-// tiles) carry the row sums through the MFMAs; a tile's column sums are the
-// growth of its chain's lane total.  KS = 128 for d_pad % 128 == 0 (the H-only
-// A side frees the registers the L fragments held), else 64, or 32 with the
-// column sums from sigma_P MFMAs.
+// MI355X design: block = 4 waves x 128 rows (one super block; at KS 128 with
+// the round-robin schedule 8 waves, two super blocks P and P + 2 sharing each
+// B stage), A fragments (8 row tiles x KS features of H) in registers; B
+// stages in a 2-deep LDS ring filled by global_load_lds_dwordx4 (source-side
+// XOR swizzle -> conflict-free ds_read_b128).  One accumulator chain per 16-row
+// tile carries its row sums through the MFMAs and is folded to the LDS row
+// accumulator every FOLD columns.  KS = 128 for d_pad % 128 == 0 (the H-only A
+// side frees the registers the L fragments held), else 64, or 32.
 #include <stdlib.h>
 
 #include <utility>
@@ -114,9 +118,6 @@ __device__ __forceinline__ unsigned fresh_lane() {
   return v;
 }
 
-#ifndef DAL_GRAM_SIGMA_COLS
-#define DAL_GRAM_SIGMA_COLS 1  // KS 64 / 128: column sums from sigma_P MFMAs
-#endif
 #ifndef DAL_GRAM_PRIO8
 #define DAL_GRAM_PRIO8 1  // 8-wave kernel: s_setprio 1 for waves 4-7 (> 0) or 0-3 (< 0)
 #endif
@@ -124,7 +125,7 @@ __device__ __forceinline__ unsigned fresh_lane() {
 #define DAL_GRAM_KS64_OCC3 1  // KS 64: three 4-wave blocks per CU (16 KiB stages; 100k x 64 -3.2 %, 200k x 64 -3.9 %, 1M x 64 +0.6 %)
 #endif
 #ifndef DAL_GRAM_KS32_OCC
-#define DAL_GRAM_KS32_OCC 4  // KS 32: 4-wave blocks per CU (3: 16 KiB stages; 4: 8 KiB stages. Config 3: 2 -> 3 -> 4 blocks 3.944 -> 3.827 -> 3.745 ms)
+#define DAL_GRAM_KS32_OCC 5  // KS 32: 4-wave blocks per CU (3: 16 KiB stages; >= 4: 8 KiB stages. Config 3: 2 -> 3 -> 4 blocks 3.944 -> 3.827 -> 3.745 ms; row sums only (94 VGPRs): 4 -> 5 blocks 3.430 -> 3.391 ms)
 #endif
 template <int KS, int W = 4>
 struct Cfg {
@@ -141,7 +142,7 @@ struct Cfg {
   static constexpr int STAGE = OCC >= 4 ? 8192 : OCC == 3 ? 16384 : 32768;  // bytes per LDS stage
   static constexpr int SC = STAGE / ROWB;           // columns per stage: 64 / 128 / 256
   static constexpr int SPP = 256 / SC;              // stages per 512 x 256 pair: 4 / 2 / 1
-  static constexpr int FOLD = KS == 128 ? 128 : 256;  // columns per row fold (chains <= 1024 products)
+  static constexpr int FOLD = KS == 128 ? 128 : 256;  // columns per row fold
   static constexpr int SPF = FOLD / SC;             // stages per fold group
   static constexpr int F4 = STAGE / 16;
   static constexpr int SWZ = (SLOTS < 16 ? SLOTS : 16) - 1;
@@ -150,26 +151,20 @@ struct Cfg {
   static constexpr int LG = 4;
   static constexpr int NKS = KS / 32;               // k-steps of v_mfma_f32_16x16x32_f16
   static constexpr int NCT = SC / 16;               // column tiles per stage
-  // column sums from sigma_P MFMAs (sigma_P = the sum of the super block's H
-  // rows): KS 32 always, KS 64 / 128 unless DAL_GRAM_SIGMA_COLS = 0 (then the
-  // growth of the row chains' lane totals, one epilogue per 16-column tile)
-  static constexpr bool SIG = KS == 32 || DAL_GRAM_SIGMA_COLS != 0;
-  // KS >= 64: sigma_P's two fp16 terms packed as rows 0-7 / 8-15 of one A
-  // fragment, two MFMAs per k-step (KS 32 keeps its three-MFMA form)
-  static constexpr bool PACK = SIG && KS >= 64;
-  static constexpr int NCH = SIG ? 1 : 2;           // row-sum chains per row tile
-  // products summed by one row-chain element between two folds (the FOLD
-  // columns' tiles dealt over NCH chains, 2 KS products per tile): the length
-  // dal_density_error_bound_sym_d charges the row side with
-  static constexpr int CHAIN = FOLD / 16 / NCH * 2 * KS;
+  // products summed by one row-chain element between two folds (one chain
+  // per row tile over the FOLD columns' tiles, 2 KS products per tile): the
+  // length dal_density_error_bound_sym_d charges the row side with
+  static constexpr int CHAIN = FOLD / 16 * 2 * KS;
   static_assert(SPF >= 1 && SPP % SPF == 0 && PIECES >= 1 && NKS >= 1, "bad slice");
   static_assert(W == 4 || (W == 8 && KS >= 64), "two super blocks per block: KS >= 64 only");
-  static_assert(!SIG || KS <= 128, "sigma partials: <= 32 values per lane");
   static_assert(CHAIN <= 2048, "row chain longer than the density bound's worst case");
 };
 // the 8-wave form folds like the 4-wave one (one bound per KS)
 static_assert(Cfg<128, 8>::CHAIN == Cfg<128, 4>::CHAIN, "block forms must share the chain length");
 
+// Row sums of the taken pairs (the column sums of every pair are added in
+// closed form by dal_gram_sym_residual, see the header): for each pair (P,
+// J) the taker's rows accumulate <H_i, u~_j> over J's 256 columns.
 template <int KS, int W>
 __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
     const uint16_t* __restrict__ urows, int srow0, int n_srb,
@@ -177,16 +172,9 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
     int ns_active, int64_t ldh, int slice_off, int chunk_j, int n_chunks,
     unsigned long long* __restrict__ acc_out, int contig) {
   using C = Cfg<KS, W>;
-  constexpr bool SIG = C::SIG;
-  constexpr int NCH = C::NCH;
   constexpr int HV = C::HALVES;
   __shared__ __attribute__((aligned(16))) float4 lds[2 * C::F4];
-  __shared__ double colacc[2][256];
   __shared__ double rowacc[HV * kSB];
-  // sigma_P (KS 32): per-wave partial sums of the H rows, then the sum split in
-  // two fp16 terms (at 2^-6 of the operand's scale), read as an A fragment
-  __shared__ float sig_part[SIG ? W : 1][SIG ? KS : 1];
-  __shared__ f16x8 sig_row[SIG ? HV : 1][SIG ? 2 * C::HI : 1];
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -202,18 +190,7 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
   }
   const int li = lane & 15, lq = lane >> 4;
   const int G = gridDim.x, g = blockIdx.x;
-  if constexpr (HV == 1) {
-    colacc[0][tid] = 0.0;
-    colacc[1][tid] = 0.0;
-    rowacc[tid] = 0.0;
-    rowacc[tid + 256] = 0.0;
-  } else {
-    if (tid < 256) {
-      colacc[0][tid] = 0.0;
-      colacc[1][tid] = 0.0;
-    }
-    for (int e = tid; e < HV * kSB; e += C::NT) rowacc[e] = 0.0;
-  }
+  for (int e = tid; e < HV * kSB; e += C::NT) rowacc[e] = 0.0;
 
   // Work = the pairs (P, J) over row super blocks P and 256-column blocks J in
   // [j_lo, j_hi) minus [skip_lo, skip_hi), as segments (row unit, raw column
@@ -323,54 +300,6 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
 #pragma unroll
       for (int c = 0; c < C::NKS; ++c)  // read once per unit: keep the column stages resident in L2
         ah[rt][c] = __builtin_nontemporal_load(reinterpret_cast<const f16x8*>(pb + lrow + rt * tstep + c * C::LG * 8));
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    if constexpr (SIG) {
-      // this wave's 128 H rows summed per feature (lane order over the row
-      // tiles, then over the 16 lanes of the DPP row)
-      constexpr int V = C::NKS * 8;
-      float sp[V];
-#pragma unroll
-      for (int c = 0; c < C::NKS; ++c)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float t = 0.0f;
-#pragma unroll
-          for (int rt = 0; rt < C::RT; ++rt) t += static_cast<float>(ah[rt][c][e]);
-          sp[c * 8 + e] = t;
-        }
-      const int fl2 = static_cast<int>(fresh_lane()), fli = fl2 & 15, flq = fl2 >> 4;
-      if constexpr (V == 32) {
-        // 16-lane reduce-scatter of 32 values: lane li keeps values 2 li, 2 li + 1
-        rs_step<16, 0x140, 32>(sp, fli & 8);
-        rs_step<8, 0x141, 32>(sp, fli & 4);
-        rs_step<4, 0x4E, 32>(sp, fli & 2);
-        rs_step<2, 0xB1, 32>(sp, fli & 1);
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const int idx = 2 * fli + q;
-          sig_part[wave][(idx >> 3) * 32 + flq * 8 + (idx & 7)] = sp[q];
-        }
-      } else {
-        row_sum_scatter<V>(sp, fli);
-        if (fli < V) sig_part[wave][(fli >> 3) * 32 + flq * 8 + (fli & 7)] = sp[0];
-      }
-    }
-  };
-  // after a block_sync that follows load_a: sigma_P = the four waves' partials
-  // (fixed order), scaled by 2^-6 (exact) and split into two fp16 terms
-  auto build_sigma = [&]() {
-    if constexpr (SIG) {
-      if (tid < HV * KS) {  // super block hh of the block: its four waves' partials
-        const int hh = tid / KS, f = tid % KS;
-        const float sg = ((sig_part[4 * hh][f] + sig_part[4 * hh + 1][f]) + sig_part[4 * hh + 2][f]) +
-                         sig_part[4 * hh + 3][f];
-        const float s6 = sg * 0x1p-6f;
-        const _Float16 h = static_cast<_Float16>(s6);
-        const _Float16 l = static_cast<_Float16>(s6 - static_cast<float>(h));
-        reinterpret_cast<_Float16*>(sig_row[hh])[f] = h;
-        reinterpret_cast<_Float16*>(sig_row[hh])[KS + f] = l;
-      }
-    }
   };
   constexpr float kFold = 0x1p8f;  // units of 2^-24 -> multiples of 2^-32
 
@@ -382,19 +311,11 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
   const int b_swz = li & C::SWZ & ~3;
   auto b_off = [&](int c, bool lo_half) { return b_base + ((c * C::LG + (lo_half ? C::HI : 0)) ^ b_swz); };
 
-  f32x4 mc[NCH][C::RT];
-  float tprev[2];
-  // KS 32: sigma_P's high and low terms as two A fragments (every row the
-  // same), three MFMAs per k-step; KS >= 64 (PACK): one A fragment, rows 0-7
-  // the high term and rows 8-15 the low one (output row 0 + row 8 = the
-  // column sum), two MFMAs per k-step -- the same for 4- and 8-wave blocks,
-  // so the density bits do not depend on the block form
-  f16x8 sgh[SIG ? C::NKS : 1], sgl[SIG && !C::PACK ? C::NKS : 1];
-  // one stage of SC columns (col0 = its first column within the pair);
-  // fresh = first stage of a fold group (chains restart).  B fragments go
-  // through two register sets: k-step i+1's are read while k-step i's MFMAs
-  // issue (16 MFMAs of latency cover).
-  auto compute = [&](int buf, float cmul, int cbuf, int col0, bool fresh_stage) {
+  f32x4 mc[C::RT];
+  // one stage of SC columns; fresh = first stage of a fold group (the chains
+  // restart).  B fragments go through two register sets: k-step i+1's are
+  // read while k-step i's 16 MFMAs issue.
+  auto compute = [&](int buf, bool fresh_stage) {
     f16x8 bh[2], bl[2];
     auto load_b = [&](int set, int c, int ct) {
       bh[set] = __builtin_bit_cast(f16x8, lds[buf * C::F4 + ct * 16 * C::SLOTS + b_off(c, false)]);
@@ -402,71 +323,27 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
     };
     load_b(0, 0, 0);
 #pragma unroll
-    for (int ct = 0; ct <= C::NCT; ++ct) {
+    for (int ct = 0; ct < C::NCT; ++ct) {
       __builtin_amdgcn_sched_barrier(0);
-      if (ct < C::NCT) {
-        const int ch = ct % NCH;
-        const bool fresh = fresh_stage && ct < NCH;
-        const bool sig = SIG && (ct & 3) == wave4;  // column tile ct's sums: this wave's turn (per super block)
-        f32x4 sg = {};
+      const bool fresh = fresh_stage && ct == 0;
 #pragma unroll
-        for (int c = 0; c < C::NKS; ++c) {
-          const int i = ct * C::NKS + c, cur = i & 1;
-          if (c + 1 < C::NKS)
-            load_b(cur ^ 1, c + 1, ct);
-          else if (ct + 1 < C::NCT)
-            load_b(cur ^ 1, 0, ct + 1);
-          const f32x4 zero = {};
+      for (int c = 0; c < C::NKS; ++c) {
+        const int i = ct * C::NKS + c, cur = i & 1;
+        if (c + 1 < C::NKS)
+          load_b(cur ^ 1, c + 1, ct);
+        else if (ct + 1 < C::NCT)
+          load_b(cur ^ 1, 0, ct + 1);
+        const f32x4 zero = {};
 #pragma unroll
-          for (int rt = 0; rt < C::RT; ++rt)
-            mc[ch][rt] = mfma16(ah[rt][c], bh[cur], (c == 0 && fresh) ? zero : mc[ch][rt]);
+        for (int rt = 0; rt < C::RT; ++rt) mc[rt] = mfma16(ah[rt][c], bh[cur], (c == 0 && fresh) ? zero : mc[rt]);
 #pragma unroll
-          for (int rt = 0; rt < C::RT; ++rt) mc[ch][rt] = mfma16(ah[rt][c], bl[cur], mc[ch][rt]);
-          if (sig) {
-            sg = mfma16(sgh[c], bh[cur], sg);
-            sg = mfma16(sgh[c], bl[cur], sg);
-            if constexpr (!C::PACK) sg = mfma16(sgl[c], bh[cur], sg);
-          }
-        }
-        // every output row of the sigma tile is the column sum (units 2^-18);
-        // PACK: rows 0 (lane group 0) and 8 (lane group 2) its two terms, each
-        // rounded to 2^-32 and added exactly (both super blocks of an 8-wave
-        // block add theirs)
-        if constexpr (!C::PACK) {
-          if (sig && lq == 0)
-            colacc[cbuf][col0 + ct * 16 + li] = static_cast<double>(__builtin_rintf(sg[0] * cmul * 64.0f));
-        } else {
-          if (sig && (lq & 1) == 0)
-            atomicAdd(&colacc[cbuf][col0 + ct * 16 + li], static_cast<double>(__builtin_rintf(sg[0] * cmul * 64.0f)));
-        }
+        for (int rt = 0; rt < C::RT; ++rt) mc[rt] = mfma16(ah[rt][c], bl[cur], mc[rt]);
       }
-      if (!SIG && ct > 0 && !(kAbl & 1)) {
-        // tile ct-1's column sums: growth of its chain's lane total
-        // (even, odd) register sums as one packed pair: v_pk_add_f32, the
-        // same two sequential chains as separate adds, half the instructions
-        const int ch = (ct - 1) & 1;
-        f32x2 t = mc[ch % NCH][0].xy;
+      constexpr int NM = 2 * C::RT;  // MFMAs per k-step
 #pragma unroll
-        for (int rt = 0; rt < C::RT; ++rt) {
-          if (rt > 0) t += mc[ch % NCH][rt].xy;
-          t += mc[ch % NCH][rt].zw;
-        }
-        const float T = t.x + t.y;
-        const float cp = (fresh_stage && ct - 1 < 2) ? T : T - tprev[ch];
-        tprev[ch] = T;
-        atomicAdd(&colacc[cbuf][col0 + (ct - 1) * 16 + li], static_cast<double>(__builtin_rintf(cp * cmul)));
-      }
-      if (ct < C::NCT) {
-        constexpr int NM = 2 * C::RT;  // MFMAs per k-step
-#pragma unroll
-        for (int c = 0; c < C::NKS; ++c) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // next k-step's B
-#pragma unroll
-          for (int i = 0; i < NM; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);    // MFMA
-            if constexpr (!SIG) __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // VALU (epilogue)
-          }
-        }
+      for (int c = 0; c < C::NKS; ++c) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // next k-step's B
+        __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);  // MFMA
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -477,16 +354,14 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
   auto fold_rows = [&]() {
     if constexpr ((kAbl & 2) != 0) {  // keep the chains live (their MFMAs stay)
 #pragma unroll
-      for (int rt = 0; rt < C::RT; ++rt)
-#pragma unroll
-        for (int ch = 0; ch < NCH; ++ch) asm volatile("" ::"v"(mc[ch][rt]));
+      for (int rt = 0; rt < C::RT; ++rt) asm volatile("" ::"v"(mc[rt]));
       return;
     }
     float v[32];
 #pragma unroll
     for (int rt = 0; rt < C::RT; ++rt)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[rt * 4 + q] = NCH == 1 ? mc[0][rt][q] : mc[0][rt][q] + mc[NCH - 1][rt][q];
+      for (int q = 0; q < 4; ++q) v[rt * 4 + q] = mc[rt][q];
     rs_step<16, 0x140>(v, li & 8);  // row_mirror: lane i <-> 15 - i
     rs_step<8, 0x141>(v, li & 4);   // row_half_mirror: i <-> i ^ 7
     rs_step<4, 0x4E>(v, li & 2);    // quad_perm [2,3,0,1]
@@ -502,19 +377,10 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
     if (v != 0.0) atomicAdd(acc_out + out_row, static_cast<unsigned long long>(static_cast<long long>(v)));
     slot = 0.0;
   };
-  auto flush_cols = [&](int cbuf, int Jf) {
-    if (tid < 256) flush_one(colacc[cbuf][tid], static_cast<int64_t>(Jf) * 256 + tid);
-  };
   auto flush_rows = [&](int ru) {  // rowacc[h * 512 + r] -> row r of the unit's super block h
-    if constexpr (HV == 1) {
-      const int P = srow0 + ru;
-      flush_one(rowacc[tid], static_cast<int64_t>(P) * kSB + tid);
-      flush_one(rowacc[tid + 256], static_cast<int64_t>(P) * kSB + tid + 256);
-    } else {
-      for (int e = tid; e < HV * kSB; e += C::NT) {
-        const int P = rowP(ru, e / kSB);
-        if (live(P)) flush_one(rowacc[e], static_cast<int64_t>(P) * kSB + e % kSB);
-      }
+    for (int e = tid; e < HV * kSB; e += C::NT) {
+      const int P = rowP(ru, e / kSB);
+      if (live(P)) flush_one(rowacc[e], static_cast<int64_t>(P) * kSB + e % kSB);
     }
   };
   // every barrier waits for this wave's LDS adds and DMA first (hipcc may
@@ -535,10 +401,7 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
   int J = jmap(r);
   issue(0, J, 0);
   load_a(ru);
-  bool sig_fresh = true;
-  int cb = 0;        // colacc buffer of the current pair
   int buf = 0;       // LDS stage buffer of the next stage to compute
-  int flushJ = -1;   // column block whose sums wait in colacc[cb ^ 1]
   int flushRU = -1;  // row unit whose sums wait in rowacc
 
   while (true) {
@@ -548,40 +411,15 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
     const int nru = has_next ? seg_ru(n_unit) : -1;
     const bool new_rows = nru != ru;
     const int nJ = has_next ? jmap(nr) : -1;
-    // this wave's super block: takes J?  diagonal (row sums only)?  The
-    // column block gets column sums when any half takes it off the diagonal.
-    const int Pw = rowP(ru, half);
+    // this wave's super block takes J?  (a half whose super block does not idles)
     const bool act = HV == 1 || takes_h(ru, half, J);
-    const float cmul = (J >> 1) == Pw ? 0.0f : kFold;
-    bool colsums = (J >> 1) != Pw;  // (W = 4: every visited J is taken)
-    if constexpr (HV > 1) {
-      colsums = false;
-#pragma unroll
-      for (int h = 0; h < HV; ++h) colsums |= takes_h(ru, h, J) && (J >> 1) != rowP(ru, h);
-    }
 
 #pragma unroll
     for (int s = 0; s < C::SPP; ++s) {
       stage_sync();
-      if (s == 0) {
-        if (flushJ >= 0) flush_cols(cb ^ 1, flushJ);
-        if (flushRU >= 0) flush_rows(flushRU);
+      if (s == 0 && flushRU >= 0) {
+        flush_rows(flushRU);
         flushRU = -1;
-        if (SIG && sig_fresh) {
-          build_sigma();
-          block_sync();
-          sig_fresh = false;
-#pragma unroll
-          for (int c = 0; c < (SIG ? C::NKS : 0); ++c) {
-            const int fl = static_cast<int>(fresh_lane()), flq = fl >> 4;
-            if constexpr (!C::PACK) {
-              sgh[c] = sig_row[0][c * C::LG + flq];
-              sgl[c] = sig_row[0][C::HI + c * C::LG + flq];
-            } else {
-              sgh[c] = sig_row[SIG ? half : 0][((fl & 8) ? C::HI : 0) + c * C::LG + flq];
-            }
-          }
-        }
       }
       if ((kAbl & 8) != 0) {
       } else if (s + 1 < C::SPP) {
@@ -589,15 +427,13 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
       } else if (has_next) {
         issue(buf ^ 1, nJ, 0);
       }
-      if (act) {  // (wave-uniform: a half whose super block does not take J idles)
-        compute(buf, cmul, cb, s * C::SC, s % C::SPF == 0);
+      if (act) {  // (wave-uniform)
+        compute(buf, s % C::SPF == 0);
         if (s % C::SPF == C::SPF - 1) fold_rows();
       }
       buf ^= 1;
     }
 
-    flushJ = colsums ? J : -1;
-    cb ^= 1;
     if (new_rows) flushRU = ru;
     if (!has_next) break;
     unit = n_unit;
@@ -605,16 +441,13 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
     if (new_rows) {
       ru = nru;
       load_a(ru);
-      sig_fresh = true;
     }
     r = nr;
     J = nJ;
   }
   block_sync();
-  if (flushJ >= 0) flush_cols(cb ^ 1, flushJ);
   if (flushRU >= 0) flush_rows(flushRU);
 }
-
 // ---------------------------------------------------------------------------
 // Residual of the compensation (see the header).  Three launches:
 //  1. per super block Q: sigma~_Q and sigma^L_Q, exact int64 in units of 2^-24
@@ -640,8 +473,7 @@ __device__ __forceinline__ long long half_units(uint16_t bits) {  // fp16 value 
 // CPR, ... -- independent 16-B loads, 8 in flight -- summed exactly in int64,
 // then reduced over the threads of the same column in LDS.
 __global__ __launch_bounds__(256) void csym_sigma_kernel(const uint16_t* __restrict__ ops, int64_t ldh, int ks,
-                                                         int d_pad, long long* __restrict__ sig_u,
-                                                         long long* __restrict__ sig_l) {
+                                                         int d_pad, long long* __restrict__ sig_u) {
   __shared__ long long red[256][9];  // [thread][8 halves] (+1: bank spread)
   const int Q = blockIdx.x;
   const int cpr = static_cast<int>(ldh / 8);      // chunks per row
@@ -679,17 +511,11 @@ __global__ __launch_bounds__(256) void csym_sigma_kernel(const uint16_t* __restr
     // chunk column -> (slice, half, first feature): the row is [slice][H KS | L KS]
     const int hpc = ks / 8;                        // chunks per half of a slice
     const int slice = col / (2 * hpc), within = col % (2 * hpc);
-    const bool lo = within >= hpc;
     const int f0 = slice * ks + (within % hpc) * 8;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int64_t o = static_cast<int64_t>(Q) * d_pad + f0 + e;
-      if (lo) {
-        sig_l[o] = v[e];
-        atomicAdd(reinterpret_cast<unsigned long long*>(sig_u + o), static_cast<unsigned long long>(v[e]));
-      } else {
-        atomicAdd(reinterpret_cast<unsigned long long*>(sig_u + o), static_cast<unsigned long long>(v[e]));
-      }
+      atomicAdd(reinterpret_cast<unsigned long long*>(sig_u + o), static_cast<unsigned long long>(v[e]));
     }
   }
 }
@@ -701,51 +527,41 @@ __global__ __launch_bounds__(256) void csym_sigma_kernel(const uint16_t* __restr
 #define DAL_CSYM_SCAN_WAVES 16
 #endif
 constexpr int kScanWaves = DAL_CSYM_SCAN_WAVES;  // super-block ranges per feature (one wave each)
-__global__ __launch_bounds__(64 * kScanWaves) void csym_scan_kernel(const long long* __restrict__ sig_u,
-                                                         const long long* __restrict__ sig_l, int ns, int d_pad,
-                                                         int b0, int b1, double* __restrict__ rb,
-                                                         double* __restrict__ cb) {
+__global__ __launch_bounds__(64 * kScanWaves) void csym_scan_kernel(const long long* __restrict__ sig_u, int ns,
+                                                                    int d_pad, int b0, int b1,
+                                                                    double* __restrict__ rb, double* __restrict__ cb) {
   constexpr int kW = kScanWaves;
-  __shared__ long long part[kW][4][64];
+  __shared__ long long part[kW][2][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int f = blockIdx.x * 64 + lane;
   const bool live = f < d_pad;
   const int q0 = static_cast<int>(static_cast<int64_t>(ns) * w / kW);
   const int q1 = static_cast<int>(static_cast<int64_t>(ns) * (w + 1) / kW);
-  // (u~, L) sums per parity class of the super block (even, odd); named
+  // u~ sums per parity class of the super block (even, odd); named
   // registers, not arrays indexed by q & 1 (those would live in scratch)
-  long long ue = 0, uo = 0, le = 0, lo = 0;
+  long long ue = 0, uo = 0;
   if (live) {
 #pragma unroll 8
     for (int q = q0; q < q1; ++q) {
       const long long su = sig_u[static_cast<int64_t>(q) * d_pad + f];
-      const long long sl = sig_l[static_cast<int64_t>(q) * d_pad + f];
       const bool odd = q & 1;
       ue += odd ? 0 : su;
       uo += odd ? su : 0;
-      le += odd ? 0 : sl;
-      lo += odd ? sl : 0;
     }
   }
   part[w][0][lane] = ue;
   part[w][1][lane] = uo;
-  part[w][2][lane] = le;
-  part[w][3][lane] = lo;
   __syncthreads();
   // exclusive prefix over the earlier waves' ranges, and the totals
-  long long eue = 0, euo = 0, ele = 0, elo = 0, tue = 0, tuo = 0, tle = 0, tlo = 0;
+  long long eue = 0, euo = 0, tue = 0, tuo = 0;
   for (int v = 0; v < kW; ++v) {
-    const long long a0 = part[v][0][lane], a1 = part[v][1][lane], a2 = part[v][2][lane], a3 = part[v][3][lane];
+    const long long a0 = part[v][0][lane], a1 = part[v][1][lane];
     if (v < w) {
       eue += a0;
       euo += a1;
-      ele += a2;
-      elo += a3;
     }
     tue += a0;
     tuo += a1;
-    tle += a2;
-    tlo += a3;
   }
   if (!live) return;
 #pragma unroll 4
@@ -753,19 +569,18 @@ __global__ __launch_bounds__(64 * kScanWaves) void csym_scan_kernel(const long l
     // e* = exclusive prefix (super blocks < q) per class; b = q's class
     const bool odd = q & 1;
     if (q >= b0 && q < b1) {
-      // R_B = sum_{Q >= B, same class} + sum_{Q < B, other class} of sigma~;
-      // C_B = sum_{P < B, same class} + sum_{P > B, other class} of sigma^L
+      // R_B = sum_{Q >= B, same class} + sum_{Q < B, other class} of sigma~
+      // (the super blocks B takes); C_B = sum_{P < B, same class} + sum_{P >
+      // B, other class} of sigma~ (the other super blocks that take B: their
+      // pairs' column sums for B's rows)
       const long long R = odd ? (tuo - euo + eue) : (tue - eue + euo);
-      const long long Cc = odd ? (elo + tle - ele) : (ele + tlo - elo);
+      const long long Cc = odd ? (euo + tue - eue) : (eue + tuo - euo);
       rb[static_cast<int64_t>(q - b0) * d_pad + f] = static_cast<double>(R);
       cb[static_cast<int64_t>(q - b0) * d_pad + f] = static_cast<double>(Cc);
     }
     const long long su = sig_u[static_cast<int64_t>(q) * d_pad + f];
-    const long long sl = sig_l[static_cast<int64_t>(q) * d_pad + f];
     eue += odd ? 0 : su;
     euo += odd ? su : 0;
-    ele += odd ? 0 : sl;
-    elo += odd ? sl : 0;
   }
 }
 
@@ -961,7 +776,7 @@ int launch_csym(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint16
 }
 
 struct ResidualLayout {
-  size_t sig_u, sig_l, rb, cb, total;
+  size_t sig_u, sig_l, rb, cb, total;  // (sig_l: kept in the layout, unused since the closed-form column sums)
 };
 ResidualLayout residual_layout(int64_t ns_active, int64_t n_srb, int64_t d_pad) {
   ResidualLayout L{};
@@ -1007,33 +822,22 @@ extern "C" double dal_density_error_bound_sym_d(int64_t n_cols, int64_t d_pad) {
   // conservative unit roundoff for the MFMA's internal fp32 adds, counted as
   // sequential adds), products exact (f16 x f16), c = 1 + 2^-8 >= sum_d |h_i
   // h_j| + |h_i l_j| over sum_d |u_i u_j| <= 1 (Cauchy-Schwarz on unit rows):
-  //   row side   one chain per row tile between folds: Cfg<KS>::CHAIN
-  //              products (FOLD / 16 / NCH tiles x 2 KS: 1,024 at KS 32,
-  //              2,048 at KS 64 and 128 with the sigma column sums, one chain
-  //              per row tile), then 4 cross-lane adds (+1 with two chains):
-  //              gamma_(CHAIN + 5) * c
-  //   column side  sigma_P MFMAs: sigma_P = the fp32 sum of the super block's
-  //              H rows (8 row tiles, 4 DPP steps, 4 waves: <= 15 adds), split
-  //              into two fp16 terms (2^-22), then <u~_j, sigma_P> over KS
-  //              features -- KS >= 64: the two terms as rows of one A fragment,
-  //              2 x KS products, each row rounded to 2^-32: (gamma_15 +
-  //              gamma_256 + 3 * 2^-22) * c at KS 128; KS 32 (three MFMAs per
-  //              k-step): (gamma_22 + gamma_96 + 3 * 2^-22) * c.  The chain-
-  //              growth form (DAL_GRAM_SIGMA_COLS = 0): (8 gamma_128 + 15
-  //              gamma_15 + u) * c
-  //   residual   <L_i, R_B> + <u~_i, C_B> in fp64: below 2^-40 per column
+  //   row side   (the MFMA row sums of the taken pairs) one chain per row
+  //              tile between folds: Cfg<KS>::CHAIN products (FOLD / 16 tiles
+  //              x 2 KS: 1,024 at KS 32, 2,048 at KS 64 and 128), then 4
+  //              cross-lane adds: gamma_(CHAIN + 5) * c (the +1 kept from the
+  //              two-chain form)
+  //   column side  none: every taken pair's column sums are the closed form
+  //              <u~_i, C_B> of dal_gram_sym_residual (exact int64 sums, an
+  //              fp64 dot), as is the row side's remainder <L_i, R_B>: below
+  //              2^-40 per column together
   //   split + fp32 unit rows  5 * 2^-22;  fixed-point roundings <= 2^-33 each
   const double u = 1.0 / 8388608.0;  // 2^-23
   auto gamma = [u](double n) { return n * u / (1.0 - n * u); };
   const double s = 1.0 / 4194304.0;  // 2^-22
   const double row = gamma(static_cast<double>(row_chain_products(d_pad)) + 5.0);
-  const double col_growth = 8.0 * gamma(128.0) + 15.0 * gamma(15.0) + u;
-  const double col_sigma = (gamma(22.0) > gamma(15.0) ? gamma(22.0) : gamma(15.0)) + gamma(256.0) + 3.0 * s;
-  // (the chain-growth column form runs only at KS >= 64 with DAL_GRAM_SIGMA_COLS = 0)
-  const bool growth = !Cfg<128, 4>::SIG && (d_pad <= 0 || split_ks(d_pad) >= 64);
-  const double col = growth && col_growth > col_sigma ? col_growth : col_sigma;
   const double c = 1.0 + 1.0 / 256.0;
-  return ((row > col ? row : col) * c + 5.0 * s + 1e-10) * static_cast<double>(n_cols) + 1e-9;
+  return (row * c + 5.0 * s + 1e-10) * static_cast<double>(n_cols) + 1e-9;
 }
 
 // Feature-width-free form (ABI v5): the bound of the longest row chain of any
@@ -1102,7 +906,6 @@ extern "C" int dal_gram_sym_residual(const uint16_t* ops, int64_t nb_active, int
   hipStream_t st = as_stream(stream);
   unsigned char* w = static_cast<unsigned char*>(ws);
   long long* sig_u = reinterpret_cast<long long*>(w + L.sig_u);
-  long long* sig_l = reinterpret_cast<long long*>(w + L.sig_l);
   double* rb = reinterpret_cast<double*>(w + L.rb);
   double* cb = reinterpret_cast<double*>(w + L.cb);
   const int ks = split_ks(d_pad);
@@ -1110,11 +913,11 @@ extern "C" int dal_gram_sym_residual(const uint16_t* ops, int64_t nb_active, int
   if (hipMemsetAsync(sig_u, 0, static_cast<size_t>(na * d_pad) * 8, st) != hipSuccess) return DAL_ERR_HIP;
   hipLaunchKernelGGL(csym_sigma_kernel,
                      dim3(static_cast<unsigned>(na), static_cast<unsigned>(ceil_div(ldh / 8, 256))), dim3(256), 0, st,
-                     ops, ldh, ks, static_cast<int>(d_pad), sig_u, sig_l);
+                     ops, ldh, ks, static_cast<int>(d_pad), sig_u);
   DAL_RETURN_IF_LAUNCH_FAILED();
   hipLaunchKernelGGL(csym_scan_kernel, dim3(static_cast<unsigned>(ceil_div(d_pad, 64))), dim3(64 * kScanWaves), 0, st, sig_u,
-                     sig_l, static_cast<int>(na), static_cast<int>(d_pad), static_cast<int>(s0),
-                     static_cast<int>(s0 + ns), rb, cb);
+                     static_cast<int>(na), static_cast<int>(d_pad), static_cast<int>(s0), static_cast<int>(s0 + ns),
+                     rb, cb);
   DAL_RETURN_IF_LAUNCH_FAILED();
   const int64_t n_rows = ns * kSB;
   hipLaunchKernelGGL(csym_residual_kernel, dim3(static_cast<unsigned>(ceil_div(n_rows, 4))), dim3(256), 0, st,

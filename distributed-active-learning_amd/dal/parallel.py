@@ -105,8 +105,8 @@ class ShardedSelector:
         self._plans = {}         # warm-step plans by (T, depth, k, beta, cap, level-1 passes)
         self.cap_scale = 1      # re-rank candidate capacity multiplier (grown on overflow)
         # bench: list -> (name, start, end) HIP events around the density
-        # exchange's collectives ("all_gather": operand + partials, recorded on
-        # the stream that waits for them; "reduce_scatter": the density sum)
+        # exchange's collective ("all_gather": operand + partials, recorded on
+        # the stream that waits for them)
         self.exchange_events = None
 
     def index_tensor(self, unlabeled_idx):
@@ -195,8 +195,10 @@ class ShardedSelector:
         all but ``reserve_cus`` CUs, and the collectives are enqueued behind it
         from a side stream that only waits for the operand -- the host's
         collective-issue time runs under the Gram instead of in front of it.
-        gram "sym": the accumulator spans every global row (this rank's pairs
-        also yield column sums for other ranks' rows) and is reduce-scattered."""
+        gram "sym": the accumulator is indexed by global row; this rank's
+        pairs yield row sums of its own rows only (the column sums of the pairs
+        that take its rows come from the closed-form residual), so no density
+        collective follows the all-gather."""
         torch = __import__("torch")
         st = self.state
         acc = self._new_acc()
@@ -248,13 +250,20 @@ class ShardedSelector:
                 for c0, c1 in other_column_ranges(self.rank, self.world, self.shard):
                     st.gram_accumulate(acc, u_full[c0:c1], c1 - c0, col_row0=c0)
         if st.gram == "sym":
-            if st.n:  # the compensation's closed-form remainder of this rank's rows
+            if st.n:  # the closed-form remainder and column sums of this rank's rows
                 st.gram_residual(acc, u_full)
-            ev = self._event_start("reduce_scatter")
-            acc = comm.reduce_scatter_sum(acc)
-            self._event_end(ev)
+            acc = self._own_rows(acc)
         self.set_density(acc)
         return u_full, parts_full
+
+    def _own_rows(self, acc):
+        """gram "sym": the kernel adds the row sums of the pairs this rank's
+        super blocks take and the residual adds every other part of its rows
+        (the column sums of the pairs that take them, in closed form), all at
+        GLOBAL row indices of a [world * shard] accumulator -- nothing lands on
+        another rank's rows, so the density is this rank's slice (no
+        collective)."""
+        return acc[self.rank * self.shard:(self.rank + 1) * self.shard]
 
     def _event_start(self, name):
         if self.exchange_events is None:
@@ -275,15 +284,14 @@ class ShardedSelector:
         return torch.zeros(n, dtype=torch.int64, device=self.state.device)
 
     def density_contribution(self, u_full):
-        """This rank's fixed-point density contribution against every column of
-        the gathered operand: its own rows' sums ([shard]), or for gram "sym"
-        a global-length vector that must be summed over ranks."""
+        """This rank's fixed-point density against every column of the
+        gathered operand: its own rows' sums ([shard])."""
         acc = self._new_acc()
         if self.state.n:
             self.state.gram_accumulate(acc, u_full, int(u_full.shape[0]), col_row0=0)
             if self.state.gram == "sym":
                 self.state.gram_residual(acc, u_full)
-        return acc
+        return self._own_rows(acc) if self.state.gram == "sym" else acc
 
     def set_density(self, acc_local):
         self._density = acc_local
@@ -292,8 +300,6 @@ class ShardedSelector:
     # ---- phase B: density against all columns + local exact top-k ------
     def local_density(self, u_full):
         if self._density is None:
-            if self.state.gram == "sym":
-                raise RuntimeError("gram 'sym' needs the cross-rank sum: use exchange_density / emulate")
             self.set_density(self.density_contribution(u_full))
         return self._density
 
@@ -600,14 +606,8 @@ def emulate(selectors, unlabeled_idx, forest, k: int, mode: str = "dw",
         u_full = torch.cat([p[0] for p in preps])
         parts_full = torch.cat([p[1] for p in preps])
     if mode == "dw" and density_mode == "gram" and selectors and selectors[0]._density is None:
-        contrib = [s.density_contribution(u_full) for s in selectors]
-        if selectors[0].state.gram == "sym":
-            total = torch.stack(contrib).sum(dim=0)  # the reduce-scatter
-            for s in selectors:
-                s.set_density(total[s.rank * s.shard:(s.rank + 1) * s.shard].clone())
-        else:
-            for s, c in zip(selectors, contrib):
-                s.set_density(c)
+        for s in selectors:
+            s.set_density(s.density_contribution(u_full))
     tops = [s.local_select(u_full, parts_full, unlabeled_idx, forest, k, mode, strategy, beta,
                            density_mode)
             for s in selectors]

@@ -162,26 +162,27 @@ int dal_split_f16(const float* u, int64_t n_pad, int64_t d_pad, int64_t ld, uint
 int dal_prep_split(const float* x, int64_t n, int64_t d, int64_t ldx, const uint8_t* row_flags,
                    int64_t n_pad, int64_t d_pad, uint16_t* out, double* norm64, double* partials,
                    int64_t* acc_zero, int32_t* dev_status, dal_stream_t stream);
-/* Symmetric (SYRK-style), compensated Gram row-sum (ABI v5).  S = U U^T is
- * symmetric: rows are grouped in 512-row super blocks (pairs of 256-row
- * blocks) and each unordered pair {P, Q} is multiplied once, giving the row
- * sums of S_PQ (-> acc rows of P) and its column sums (-> acc rows of Q).
- * P takes Q iff Q == P, or Q > P and P+Q even, or Q < P and P+Q odd (global
- * indices, so the bits do not depend on the sharding).  The taker's side is
- * H only: per 32 features two v_mfma_f32_16x16x32_f16 (H.H, H.L) form
- * <H_i, H_j + L_j>; the exact remainder sum <L_i, H_j + L_j> of every taken
- * pair is added in closed form by dal_gram_sym_residual -- acc holds the
- * density only after BOTH (any order; integer adds).  rows: the operand of
- * global 256-row blocks [row_block0, row_block0 + n_row_blocks) (even
- * counts); cols: the operand whose first block is global block col_block0;
- * column blocks [j_lo, j_hi) minus [skip_lo, skip_hi) are processed (j_hi <=
- * nb_active = pad512(N_total) / 256), so a caller can split the columns over
- * several calls.  acc is indexed by GLOBAL row (>= nb_active * 256 entries,
- * zeroed by the caller); on several GPUs the per-rank accs are summed
- * (reduce-scatter).  Chains are folded to multiples of 2^-32 and added
- * exactly (int64): the bits do not depend on the grid, the column split or
- * the GPU count.  Rigorous bound on |d - d_canonical| of the completed
- * density: dal_density_error_bound_sym. */
+/* Symmetric (SYRK-style), compensated Gram row-sum (ABI v5; row sums only
+ * since ABI v8).  S = U U^T is symmetric: rows are grouped in 512-row super
+ * blocks (pairs of 256-row blocks) and each unordered pair {P, Q} is
+ * multiplied once.  P takes Q iff Q == P, or Q > P and P+Q even, or Q < P and
+ * P+Q odd (global indices, so the bits do not depend on the sharding).  The
+ * taker's side is H only: per 32 features two v_mfma_f32_16x16x32_f16 (H.H,
+ * H.L) form the row sums of <H_i, H_j + L_j> over the taken pairs (-> acc
+ * rows of P).  dal_gram_sym_residual adds everything else in closed form:
+ * the taker's remainder <L_i, H_j + L_j> and the pair's column sums for Q's
+ * rows (sum over the P taking Q of <u~_j, sum_{i in P} u~_i>) -- acc holds the
+ * density only after BOTH (any order; integer adds), and each call writes
+ * only the acc rows of ITS row blocks (no cross-GPU density sum).  rows: the
+ * operand of global 256-row blocks [row_block0, row_block0 + n_row_blocks)
+ * (even counts); cols: the operand whose first block is global block
+ * col_block0; column blocks [j_lo, j_hi) minus [skip_lo, skip_hi) are
+ * processed (j_hi <= nb_active = pad512(N_total) / 256), so a caller can
+ * split the columns over several calls.  acc is indexed by GLOBAL row
+ * (>= nb_active * 256 entries, zeroed by the caller).  Chains are folded to
+ * multiples of 2^-32 and added exactly (int64): the bits do not depend on the
+ * grid, the column split or the GPU count.  Rigorous bound on |d -
+ * d_canonical| of the completed density: dal_density_error_bound_sym_d. */
 int dal_gram_rowsum_sym(const uint16_t* rows, int64_t row_block0, int64_t n_row_blocks,
                         const uint16_t* cols, int64_t col_block0, int64_t j_lo, int64_t j_hi,
                         int64_t nb_active, int64_t d_pad, int64_t* acc, int grid_blocks,
@@ -190,12 +191,14 @@ int dal_gram_rowsum_sym_skip(const uint16_t* rows, int64_t row_block0, int64_t n
                              const uint16_t* cols, int64_t col_block0, int64_t j_lo, int64_t j_hi,
                              int64_t skip_lo, int64_t skip_hi, int64_t nb_active, int64_t d_pad,
                              int64_t* acc, int grid_blocks, dal_stream_t stream);
-/* The compensation term of dal_gram_rowsum_sym for the rows of global blocks
- * [row_block0, row_block0 + n_row_blocks) (even), ADDED into acc (global
- * row index): acc[r] += rint(2^32 * (<L_r, R_B> + <H_r + L_r, C_B>)), B = r's
- * super block, R_B = sum over the super blocks B takes of their (H + L) row
- * sums, C_B = sum over the other super blocks that take B of their L row sums
- * (exact int64 sums in units of 2^-24; fp64 dots in a fixed order).  ops: the
+/* The closed-form part of dal_gram_rowsum_sym's density for the rows of
+ * global blocks [row_block0, row_block0 + n_row_blocks) (even), ADDED into acc
+ * (global row index): acc[r] += rint(2^32 * (<L_r, R_B> + <H_r + L_r, C_B>)),
+ * B = r's super block, R_B = sum over the super blocks B takes of their
+ * (H + L) row sums (the taker side's remainder), C_B = the same sum over the
+ * other super blocks that take B (their pairs' column sums for B's rows;
+ * sigma~ since ABI v8) -- exact int64 sums in units of 2^-24, fp64 dots in a
+ * fixed order.  ops: the
  * operand of EVERY active row (nb_active * 256 rows: the gathered operand on
  * several GPUs).  Three launches, O(N * D); workspace from
  * dal_gram_sym_residual_workspace_bytes (256-byte aligned). */

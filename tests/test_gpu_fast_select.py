@@ -447,7 +447,7 @@ def test_fast_level1_region_and_capacity_boundaries(cuda, layout, extra):
         k = 10
     else:
         special = np.concatenate([np.arange(10, 10 + 256), 32 * gr + np.arange(257),
-                                  np.arange(64, 4096) * gr + 5])  # block 0: 256, block 1: 257, then 32 each
+                                  np.arange(600, 4096) * gr + 5])  # block 0: 256, block 1: 257, then one per group
         k = 300
     cap = len(special) + extra
     if cap > _lib.DAL_SORT_CAP_PAYLOAD:

@@ -607,8 +607,8 @@ def test_sharded_selection_with_few_candidates(cuda, case):
 
 class _RecordingComm:
     """Single-process stand-in for TorchComm: the all-gather returns the
-    precomputed gathered operand (asynchronously: a work handle), the
-    reduce-scatter returns this rank's full contribution (summed by the test)."""
+    precomputed gathered operand (asynchronously: a work handle); no other
+    collective is used by the density exchange."""
 
     overlaps = True  # take the RCCL code path: own-shard Gram queued before the collectives
 
@@ -624,15 +624,15 @@ class _RecordingComm:
         self.waited = self.waited or work == "work"
 
     def reduce_scatter_sum(self, t):
-        return t
+        raise AssertionError("the density exchange has no reduce-scatter")
 
 
 @pytest.mark.parametrize("world,n", [(2, 5000), (3, 7000), (4, 2500), (8, 9000)])
 def test_exchange_density_column_split_bit_identical(cuda, world, n):
     """ShardedSelector.exchange_density (the RCCL path: own-shard launch with
     CUs left to the collective, then the other column ranges, then the
-    reduce-scatter of the global accumulator) sums to the single-GPU density
-    bits exactly."""
+    closed-form residual of the rank's rows) gives every rank its own rows'
+    single-GPU density bits exactly, with no density collective."""
     import torch
     from dal import parallel
     from dal.engine import PoolState
@@ -645,12 +645,12 @@ def test_exchange_density_column_split_bit_identical(cuda, world, n):
         lo, hi, _ = parallel.shard_range(n, world, r)
         sels.append(parallel.ShardedSelector(X[lo:hi], n, r, world, excluded=E, device=cuda, gram="sym"))
     u_full = torch.cat([s.prep()[0] for s in sels])
-    total = None
     for s in sels:
         comm = _RecordingComm(u_full)
         s.exchange_density(comm, s.prep()[0])
         assert comm.waited
-        total = s._density.clone() if total is None else total + s._density
+        assert s._density.shape[0] == s.shard
+    total = torch.cat([s._density for s in sels])
     st = PoolState(X, excluded=E, device=cuda, gram="sym")
     assert torch.equal(total[:n], st.density_fixed()[:n])
 
@@ -702,7 +702,7 @@ class _AsyncComm:
             work.wait()
 
     def reduce_scatter_sum(self, t):
-        return t  # the test sums the ranks' global-length contributions
+        raise AssertionError("the density exchange has no reduce-scatter")
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
@@ -727,7 +727,6 @@ def test_exchange_density_async_producer_bit_identical(cuda, world):
         sels.append(parallel.ShardedSelector(X[lo:hi], n, r, world, excluded=E, device=cuda, gram="sym"))
     preps = [s.prep() for s in sels]
     pieces = {"u": [p[0] for p in preps], "parts": [p[1] for p in preps]}
-    total = None
     for r, s in enumerate(sels):
         comm = _AsyncComm(r, pieces)
         u_full, parts_full = s.exchange_density(comm, preps[r][0], preps[r][1])
@@ -735,11 +734,9 @@ def test_exchange_density_async_producer_bit_identical(cuda, world):
         # the gathered operand and partials as the consumer sees them, after the wait
         assert torch.equal(u_full, torch.cat(pieces["u"]))
         assert torch.equal(parts_full, torch.cat(pieces["parts"]))
-        total = s._density.clone() if total is None else total + s._density
+    total = torch.cat([s._density for s in sels])
     st = PoolState(X, excluded=E, device=cuda, gram="sym")
     assert torch.equal(total[:n], st.density_fixed()[:n])
-    for s in sels:
-        s.set_density(total[s.rank * s.shard:(s.rank + 1) * s.shard].clone())
     F = Forest.synthetic(10, 4, d, seed=1)
     of = O.synthetic_forest(10, 4, d, seed=1)
     idx, sc = parallel.emulate(sels, unl, F, k)

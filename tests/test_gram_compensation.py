@@ -1,10 +1,12 @@
 """The compensated symmetric Gram's algebra (csrc/gram_sym.hip), restated in
 NumPy on exact integers (CPU only): over super-block pairs taken by the
-orientation rule, the H-only taker side gives row sums of H_P (H_Q + L_Q)^T
-and column sums of the same tile; the closed-form remainder of
-dal_gram_sym_residual -- <L_r, R_B> + <u~_r, C_B> with R_B / C_B from the
-parity-class prefix sums csym_scan_kernel forms -- completes every row to
-sum_j <u~_r, u~_j> exactly.  Reference: density_weighting.py:67-75,157-161."""
+orientation rule, the H-only taker side gives the row sums of H_P (H_Q +
+L_Q)^T (the MFMA kernel); the closed form of dal_gram_sym_residual --
+<L_r, R_B> (the taker side's remainder) + <u~_r, C_B> (the column sums of
+every pair that takes r's super block) with R_B / C_B the parity-class prefix
+sums of the super blocks' u~ sums that csym_scan_kernel forms -- completes
+every row to sum_j <u~_r, u~_j> exactly.  Reference:
+density_weighting.py:67-75,157-161."""
 import numpy as np
 import pytest
 
@@ -19,18 +21,16 @@ def residual(H, L, nsb):
     U = H + L
     D = H.shape[1]
     sig_u = np.array([U[q * SB:(q + 1) * SB].sum(0) for q in range(nsb)])
-    sig_l = np.array([L[q * SB:(q + 1) * SB].sum(0) for q in range(nsb)])
-    tot = [sig_u[0::2].sum(0), sig_u[1::2].sum(0), sig_l[0::2].sum(0), sig_l[1::2].sum(0)]
-    e = [np.zeros(D, dtype=np.int64) for _ in range(4)]
+    tot = [sig_u[0::2].sum(0), sig_u[1::2].sum(0)]
+    e = [np.zeros(D, dtype=np.int64) for _ in range(2)]
     res = np.zeros(H.shape[0], dtype=np.int64)
     for q in range(nsb):
         b = q & 1
-        R = tot[b] - e[b] + e[1 - b]            # sum of u~ over the super blocks q takes
-        C = e[2 + b] + tot[3 - b] - e[3 - b]    # sum of L over the other super blocks taking q
+        R = tot[b] - e[b] + e[1 - b]          # sum of u~ over the super blocks q takes
+        C = e[b] + tot[1 - b] - e[1 - b]      # sum of u~ over the other super blocks taking q
         rows = slice(q * SB, (q + 1) * SB)
         res[rows] = L[rows] @ R + U[rows] @ C
         e[b] = e[b] + sig_u[q]
-        e[2 + b] = e[2 + b] + sig_l[q]
     return res
 
 
@@ -48,9 +48,7 @@ def test_compensated_sym_gram_completes_every_row(nsb, D, seed):
             if not takes(P, Q):
                 continue
             T = H[P * SB:(P + 1) * SB] @ U[Q * SB:(Q + 1) * SB].T
-            acc[P * SB:(P + 1) * SB] += T.sum(axis=1)
-            if Q != P:
-                acc[Q * SB:(Q + 1) * SB] += T.sum(axis=0)
+            acc[P * SB:(P + 1) * SB] += T.sum(axis=1)  # row sums only (the kernel)
     full = U @ U.sum(axis=0)
     assert np.array_equal(acc + residual(H, L, nsb), full)
     if nsb > 1:

@@ -210,7 +210,7 @@ def _comm_worker(rank, world, port, q):
         # fp16-split Gram operands travel as uint16 bit patterns (no gloo type)
         u = (torch.arange(6, dtype=torch.int32) + 1000 * rank + 60000).to(torch.uint16).view(3, 2)
         g = comm.all_gather(u)
-        # the symmetric Gram's global-length accumulator is reduce-scattered
+        # the comm's reduce-scatter primitive (a global-length int64 vector)
         acc = torch.arange(world * 4, dtype=torch.int64) * (rank + 1)
         rs = comm.reduce_scatter_sum(acc)
         q.put((rank, g.dtype == torch.uint16, g.to(torch.int32).numpy(), rs.numpy()))
