@@ -301,14 +301,21 @@ def forest_roofline(n_rows, d, trees, forest_ms, config, world):
     return out
 
 
-def topk_roofline(n_rows, select_ms, config, world, level1_passes=0):
+def topk_roofline(n_rows, select_ms, config, world, level1_passes=0, step_select_ms=None):
     """K3 (dal_dw_select).  Exact level 1: radix select of the k-th
     pessimistic key (6 passes x 8 B per row) + ordered compaction (count and
     write: both interval keys, 2 x 16 B per row).  Fast level 1 (the engine
     default on pools whose candidates fit 4,096 slots): both interval keys read
     once for the row-group minima (16 B per row); the threshold, the scan of
     the groups that can hold candidates, the exact fp64 re-rank and the
-    one-block sort touch O(groups + candidates) bytes."""
+    one-block sort touch O(groups + candidates) bytes.
+
+    ``step_select_ms`` (one GPU, fast level 1): the selection launch of the
+    fused step alone -- what dal_dw_step and the warm plan run after the score
+    kernel has folded the row-group minima (DAL_STEP_SELECT_ONLY calls).  Its
+    bytes are O(groups + candidates), so it is reported as latency-bound
+    (``fused_step_select_ms``); ``launch_ms`` / ``frac`` stay the standalone
+    dal_dw_select call with its own minima pass."""
     if not select_ms:
         return None
     if level1_passes:
@@ -323,6 +330,10 @@ def topk_roofline(n_rows, select_ms, config, world, level1_passes=0):
     return {"bound": "hbm", "kernel": kernel,
             "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
             "traffic": _traffic(config, "dw_select_bytes_per_launch", world), "launch_ms": select_ms,
+            "fused_step_select_ms": step_select_ms,
+            "fused_step_select_note": ("summary_select_kernel as dal_dw_step / the warm plan run it (row-group "
+                                       "minima folded by the score kernel), timed alone: DAL_STEP_SELECT_ONLY "
+                                       "calls, 10 per event pair behind a GPU spin; latency-bound"),
             "algorithmic_bytes_per_launch": nbytes, "bytes_per_row": per_row,
             "note": "one C-ABI call (all its launches), HIP events on the launch stream, warm steps, each call queued behind a GPU spin and issued 10x back to back between the events (device time per call incl. its launch gaps; no host submission gaps, event cost amortised)"}
 
@@ -513,23 +524,26 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
                          f"({idx_g[:8].tolist()} vs {idx_s[:8].tolist()})")
 
     # warm path: density cached (the reference's density is constant per pool)
-    warm_ms = forest_ms = select_ms = None
+    warm_ms = forest_ms = select_ms = step_select_ms = None
     warm_same = None
     if warm_steps > 0:
         step()
         # per-kernel HIP-event timing of K2 / K3 (eager launches, events on the launch stream)
         state.forest_events, state.select_events = [], []
+        state.step_select_events = [] if world == 1 else None
         state.event_lead_cycles, state.event_repeat = EVENT_LEAD_CYCLES, EVENT_REPEAT
         for _ in range(min(warm_steps, 20)):
             step(cold=False)
         torch.cuda.synchronize()
-        fev, sev = state.forest_events, state.select_events
-        state.forest_events = state.select_events = None
+        fev, sev, ssev = state.forest_events, state.select_events, state.step_select_events
+        state.forest_events = state.select_events = state.step_select_events = None
         state.event_lead_cycles, state.event_repeat = 0, 1
         if fev:
             forest_ms = sum(a.elapsed_time(b) for a, b in fev) / len(fev) / EVENT_REPEAT
         if sev:
             select_ms = sum(a.elapsed_time(b) for a, b in sev) / len(sev) / EVENT_REPEAT
+        if ssev:
+            step_select_ms = sum(a.elapsed_time(b) for a, b in ssev) / len(ssev) / EVENT_REPEAT
         # warm latency: the step as a user runs it (one GPU: the hipGraph replay)
         step(cold=False)
         tw, (idx_w, sc_w) = _timed(lambda: step(cold=False), warm_steps, barrier)
@@ -614,7 +628,7 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
                                        engine.gram_products(state)), residual_ms=resid_ms),
         "roofline_forest": forest_roofline(state.n, d, cfg["trees"], forest_ms, config, world),
         "roofline_topk": topk_roofline(state.n, select_ms, config, world,
-                                       engine.LEVEL1_PASSES if state.level1_fast else 0),
+                                       engine.LEVEL1_PASSES if state.level1_fast else 0, step_select_ms),
         "cpu_baseline": None,
         "ranks": ranks,
     }
@@ -808,10 +822,12 @@ def _r(v, nd=4):
     return float(f"{float(v):.{nd}g}")
 
 
-def _roof_short(r, keys=("bound", "achieved", "peak", "unit", "frac", "traffic", "launch_ms")):
+def _roof_short(r, keys=("bound", "achieved", "peak", "unit", "frac", "traffic", "launch_ms",
+                         "fused_step_select_ms")):
     if not r:
         return None
-    return {k: _r(r.get(k), 5 if k in ("frac", "launch_ms") else 4) for k in keys if k in r}
+    return {k: _r(r.get(k), 5 if k in ("frac", "launch_ms", "fused_step_select_ms") else 4) for k in keys
+            if k in r}
 
 
 def _checks(sc):
@@ -872,6 +888,8 @@ def extra_line(label: str, r: dict) -> dict:
         ro = r.get(key)
         if ro:
             e[short] = {"frac": _r(ro.get("frac")), "ms": _r(ro.get("launch_ms")), "bound": ro.get("bound")}
+            if ro.get("fused_step_select_ms"):
+                e[short]["fused_ms"] = _r(ro["fused_step_select_ms"])
     if "gram" in e and str(r["roofline"].get("kernel", "")).startswith("dal_max_cosine"):
         e["maxcos"] = e.pop("gram")
     cb = r.get("cpu_baseline")

@@ -121,8 +121,17 @@ __device__ __forceinline__ unsigned fresh_lane() {
 #ifndef DAL_GRAM_PRIO8
 #define DAL_GRAM_PRIO8 1  // 8-wave kernel: s_setprio 1 for waves 4-7 (> 0) or 0-3 (< 0)
 #endif
-#ifndef DAL_GRAM_KS64_OCC3
-#define DAL_GRAM_KS64_OCC3 1  // KS 64: three 4-wave blocks per CU (16 KiB stages; 100k x 64 -3.2 %, 200k x 64 -3.9 %, 1M x 64 +0.6 %)
+#ifndef DAL_GRAM_KS64_OCC
+#define DAL_GRAM_KS64_OCC 3  // KS 64: 4-wave blocks per CU (3: 16 KiB stages; 100k x 64 -3.2 %, 200k x 64 -3.9 %, 1M x 64 +0.6 % vs 2)
+#endif
+#ifndef DAL_GRAM_NCH128
+#define DAL_GRAM_NCH128 1  // row-sum chains per row tile at KS 128 (2: 240 VGPRs, no spill; KS <= 64 keep 1)
+#endif
+#ifndef DAL_GRAM_FOLD64
+#define DAL_GRAM_FOLD64 256  // columns per row fold at KS <= 64
+#endif
+#ifndef DAL_GRAM_W8_KS64
+#define DAL_GRAM_W8_KS64 0  // KS 64 in the 8-wave two-super-block form (round robin schedule only)
 #endif
 #ifndef DAL_GRAM_KS32_OCC
 #define DAL_GRAM_KS32_OCC 5  // KS 32: 4-wave blocks per CU (3: 16 KiB stages; >= 4: 8 KiB stages. Config 3: 2 -> 3 -> 4 blocks 3.944 -> 3.827 -> 3.745 ms; row sums only (94 VGPRs): 4 -> 5 blocks 3.430 -> 3.391 ms)
@@ -136,13 +145,11 @@ struct Cfg {
   static constexpr int SLOTS = ROWB / 16;           // 16-B slots per row
   static constexpr int HI = KS / 8;                 // slots of the H part
   // three 4-wave blocks per CU at KS 64 (OCC3): 16 KiB stages so three fit the LDS
-  static constexpr int OCC = (W == 4 && KS == 32 && DAL_GRAM_KS32_OCC > 3) ? DAL_GRAM_KS32_OCC
-                             : (W == 4 && ((KS == 64 && DAL_GRAM_KS64_OCC3 != 0) || (KS == 32 && DAL_GRAM_KS32_OCC != 0)))
-                                 ? 3 : 8 / W;
+  static constexpr int OCC = W == 8 ? 1 : KS == 32 ? DAL_GRAM_KS32_OCC : KS == 64 ? DAL_GRAM_KS64_OCC : 2;
   static constexpr int STAGE = OCC >= 4 ? 8192 : OCC == 3 ? 16384 : 32768;  // bytes per LDS stage
   static constexpr int SC = STAGE / ROWB;           // columns per stage: 64 / 128 / 256
   static constexpr int SPP = 256 / SC;              // stages per 512 x 256 pair: 4 / 2 / 1
-  static constexpr int FOLD = KS == 128 ? 128 : 256;  // columns per row fold
+  static constexpr int FOLD = KS == 128 ? 128 : DAL_GRAM_FOLD64;  // columns per row fold
   static constexpr int SPF = FOLD / SC;             // stages per fold group
   static constexpr int F4 = STAGE / 16;
   static constexpr int SWZ = (SLOTS < 16 ? SLOTS : 16) - 1;
@@ -151,10 +158,13 @@ struct Cfg {
   static constexpr int LG = 4;
   static constexpr int NKS = KS / 32;               // k-steps of v_mfma_f32_16x16x32_f16
   static constexpr int NCT = SC / 16;               // column tiles per stage
-  // products summed by one row-chain element between two folds (one chain
-  // per row tile over the FOLD columns' tiles, 2 KS products per tile): the
-  // length dal_density_error_bound_sym_d charges the row side with
-  static constexpr int CHAIN = FOLD / 16 * 2 * KS;
+  // row-sum chains per row tile (column tiles dealt round-robin; 2 halve the
+  // chain length -- a tighter density bound -- for 32 more VGPRs)
+  static constexpr int NCH = KS == 128 ? DAL_GRAM_NCH128 : 1;
+  // products summed by one row-chain element between two folds (the FOLD
+  // columns' tiles over NCH chains, 2 KS products per tile): the length
+  // dal_density_error_bound_sym_d charges the row side with
+  static constexpr int CHAIN = FOLD / 16 / NCH * 2 * KS;
   static_assert(SPF >= 1 && SPP % SPF == 0 && PIECES >= 1 && NKS >= 1, "bad slice");
   static_assert(W == 4 || (W == 8 && KS >= 64), "two super blocks per block: KS >= 64 only");
   static_assert(CHAIN <= 2048, "row chain longer than the density bound's worst case");
@@ -311,7 +321,7 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
   const int b_swz = li & C::SWZ & ~3;
   auto b_off = [&](int c, bool lo_half) { return b_base + ((c * C::LG + (lo_half ? C::HI : 0)) ^ b_swz); };
 
-  f32x4 mc[C::RT];
+  f32x4 mc[C::NCH][C::RT];
   // one stage of SC columns; fresh = first stage of a fold group (the chains
   // restart).  B fragments go through two register sets: k-step i+1's are
   // read while k-step i's 16 MFMAs issue.
@@ -325,7 +335,8 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
 #pragma unroll
     for (int ct = 0; ct < C::NCT; ++ct) {
       __builtin_amdgcn_sched_barrier(0);
-      const bool fresh = fresh_stage && ct == 0;
+      const bool fresh = fresh_stage && ct < C::NCH;
+      const int ch = ct % C::NCH;
 #pragma unroll
       for (int c = 0; c < C::NKS; ++c) {
         const int i = ct * C::NKS + c, cur = i & 1;
@@ -335,9 +346,10 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
           load_b(cur ^ 1, 0, ct + 1);
         const f32x4 zero = {};
 #pragma unroll
-        for (int rt = 0; rt < C::RT; ++rt) mc[rt] = mfma16(ah[rt][c], bh[cur], (c == 0 && fresh) ? zero : mc[rt]);
+        for (int rt = 0; rt < C::RT; ++rt)
+          mc[ch][rt] = mfma16(ah[rt][c], bh[cur], (c == 0 && fresh) ? zero : mc[ch][rt]);
 #pragma unroll
-        for (int rt = 0; rt < C::RT; ++rt) mc[rt] = mfma16(ah[rt][c], bl[cur], mc[rt]);
+        for (int rt = 0; rt < C::RT; ++rt) mc[ch][rt] = mfma16(ah[rt][c], bl[cur], mc[ch][rt]);
       }
       constexpr int NM = 2 * C::RT;  // MFMAs per k-step
 #pragma unroll
@@ -354,14 +366,16 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
   auto fold_rows = [&]() {
     if constexpr ((kAbl & 2) != 0) {  // keep the chains live (their MFMAs stay)
 #pragma unroll
-      for (int rt = 0; rt < C::RT; ++rt) asm volatile("" ::"v"(mc[rt]));
+      for (int rt = 0; rt < C::RT; ++rt)
+#pragma unroll
+        for (int ch = 0; ch < C::NCH; ++ch) asm volatile("" ::"v"(mc[ch][rt]));
       return;
     }
     float v[32];
 #pragma unroll
     for (int rt = 0; rt < C::RT; ++rt)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[rt * 4 + q] = mc[rt][q];
+      for (int q = 0; q < 4; ++q) v[rt * 4 + q] = C::NCH == 1 ? mc[0][rt][q] : mc[0][rt][q] + mc[C::NCH - 1][rt][q];
     rs_step<16, 0x140>(v, li & 8);  // row_mirror: lane i <-> 15 - i
     rs_step<8, 0x141>(v, li & 4);   // row_half_mirror: i <-> i ^ 7
     rs_step<4, 0x4E>(v, li & 2);    // quad_perm [2,3,0,1]
@@ -767,7 +781,7 @@ int launch_csym(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint16
   // chunks whose blocks sweep the same column stages together.  Exact integer
   // accumulation: the schedule never changes the bits.
   const int contig = (j_hi - j_lo) * 256 * ldh * 2 <= (int64_t{32} << 20);
-  if constexpr (KS == 128 && DAL_GRAM_WAVES8)
+  if constexpr ((KS == 128 && DAL_GRAM_WAVES8) || (KS == 64 && DAL_GRAM_W8_KS64))
     if (!contig)
       return launch_csym_w<KS, 8>(rows, srow0, n_srb, cols, jcol0, j_lo, j_hi, skip_lo, skip_hi, ns_active, ldh,
                                   slice_off, acc, grid_blocks, contig, stream);

@@ -1803,14 +1803,19 @@ GroupSummary make_groups(const uint64_t* ginv, int64_t n, int64_t unit) {
   return GroupSummary{ginv, ceil_div(units, per), per * unit};
 }
 
+// The group layout of launch_group_min: at most kMaxGroups groups; groups
+// below a wave are a power of two of rows (lane segments).
+GroupSummary group_min_layout(const uint64_t* ginv, int64_t n) {
+  int64_t rows = ceil_div(n, kMaxGroups), unit = 1;
+  while (unit < rows && unit < 64) unit <<= 1;
+  return make_groups(ginv, n, unit);
+}
+
 // The minima of both keys over kMaxGroups (or n) groups, by group_min_kernel
 // (which also zeroes `zero_words` words at `zero`).
 GroupSummary launch_group_min(const uint64_t* keys_lo, const uint64_t* keys_hi, int64_t n, uint64_t* ginv,
                               uint32_t* zero, int64_t zero_words, hipStream_t st) {
-  // groups below a wave are a power of two of rows (lane segments)
-  int64_t rows = ceil_div(n, kMaxGroups), unit = 1;
-  while (unit < rows && unit < 64) unit <<= 1;
-  const GroupSummary S = make_groups(ginv, n, unit);
+  const GroupSummary S = group_min_layout(ginv, n);
   const int64_t blocks = S.group_rows < 64 ? ceil_div(n, 256) : ceil_div(S.ng, 4);
   hipLaunchKernelGGL(group_min_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, keys_lo, keys_hi, n,
                      S.group_rows, S.ng, ginv, zero, zero_words);
@@ -2121,12 +2126,20 @@ int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_
   if (!x || !inner || !leaf || !lut || !density_fixed || !norm64 || !colsum || !ws || !votes || !scores ||
       !keys_lo || !keys_hi || !out_idx || !out_scores || !dev_status)
     return DAL_ERR_ARG;
-  if (step_flags & ~static_cast<uint32_t>(DAL_STEP_RESET_STATUS | DAL_STEP_WS_CLEAN)) return DAL_ERR_ARG;
+  if (step_flags & ~static_cast<uint32_t>(DAL_STEP_RESET_STATUS | DAL_STEP_WS_CLEAN | DAL_STEP_KEEP_GROUPS |
+                                         DAL_STEP_SELECT_ONLY))
+    return DAL_ERR_ARG;
   if (d < 1 || ldx < d) return DAL_ERR_SHAPE;
   int rc = check_rerank_args(n, k, cap, level1_passes, ws, ws_bytes);
   if (rc) return rc;
   hipStream_t st = as_stream(stream);
   const bool clean = step_flags & DAL_STEP_WS_CLEAN;
+  const bool keep = step_flags & DAL_STEP_KEEP_GROUPS;
+  const bool select_only = step_flags & DAL_STEP_SELECT_ONLY;
+  // the selection launch alone re-reads the keys and group minima a previous
+  // call left (KEEP_GROUPS): fast level 1, clean header, status owned by the caller
+  if (select_only && (level1_passes == 0 || !clean || (step_flags & DAL_STEP_RESET_STATUS))) return DAL_ERR_ARG;
+  if (keep && level1_passes == 0) return DAL_ERR_ARG;
   ForestStepHooks hooks;
   if (plan_hooks) hooks = *plan_hooks;
   if (step_flags & DAL_STEP_RESET_STATUS) hooks.status_reset = dev_status;
@@ -2166,10 +2179,15 @@ int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_
     zero_words(reinterpret_cast<uint32_t*>(h1), kFastHdrWords, st);
     if (folded) zero_words(reinterpret_cast<uint32_t*>(gmin), 2 * S.ng * 2, st);
   }
-  rc = forest_score_launch(x, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, DAL_DENSITY_FIXED,
-                           density_err, row_flags, beta, DAL_DESCENDING, votes, scores, keys_lo, keys_hi, hooks, st);
-  if (rc) return rc;
-  if (!in_score) S = launch_group_min(keys_lo, keys_hi, n, gmin, nullptr, 0, st);
+  if (!select_only) {
+    rc = forest_score_launch(x, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, DAL_DENSITY_FIXED,
+                             density_err, row_flags, beta, DAL_DESCENDING, votes, scores, keys_lo, keys_hi, hooks,
+                             st);
+    if (rc) return rc;
+    if (!in_score) S = launch_group_min(keys_lo, keys_hi, n, gmin, nullptr, 0, st);
+  } else if (!in_score) {
+    S = group_min_layout(gmin, n);  // the minima the previous call's group_min_kernel wrote
+  }
   if (colsum_ready && hipStreamWaitEvent(st, reinterpret_cast<hipEvent_t>(colsum_ready), 0) != hipSuccess)
     return DAL_ERR_HIP;
   const DwRerank R{x, static_cast<int>(d), ldx, norm64, colsum, lut, votes, row_flags, beta,
@@ -2181,7 +2199,7 @@ int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_
   tail.status = dev_status;
   tail.clear = reinterpret_cast<uint32_t*>(h1);
   tail.clear_words = kFastHdrWords;
-  if (folded) {
+  if (folded && !keep) {
     tail.clear2 = reinterpret_cast<uint32_t*>(gmin);
     tail.clear2_words = 2 * S.ng * 2;
   }

@@ -36,6 +36,8 @@ DAL_SORT_CAP = 8192
 DAL_SORT_CAP_PAYLOAD = 4096
 DAL_STEP_RESET_STATUS = 1
 DAL_STEP_WS_CLEAN = 2
+DAL_STEP_KEEP_GROUPS = 4
+DAL_STEP_SELECT_ONLY = 8
 DAL_RF_MAX_SPLITS = 255
 DAL_RF_MAX_SPLIT_SAMPLE = 16384
 DAL_RF_MAX_DEPTH = 10

@@ -20,7 +20,8 @@ from . import _lib
 from ._lib import (DAL_ASCENDING, DAL_CANON_CHUNK, DAL_DENSITY_EXACT, DAL_DENSITY_FIXED,
                    DAL_DENSITY_NONE, DAL_DESCENDING, DAL_FIXED_SCALE, DAL_FLAG_CAND_OVERFLOW,
                    DAL_FLAG_SAMPLE_MISS, DAL_FLAG_ZERO_NORM, DAL_ROW_CANDIDATE, DAL_ROW_EXCLUDED,
-                   DAL_SORT_CAP_PAYLOAD, DAL_STEP_RESET_STATUS, DAL_STEP_WS_CLEAN, call)
+                   DAL_SORT_CAP_PAYLOAD, DAL_STEP_KEEP_GROUPS, DAL_STEP_RESET_STATUS, DAL_STEP_SELECT_ONLY,
+                   DAL_STEP_WS_CLEAN, call)
 from .forest import Forest
 from .luts import ASCENDING, lut as make_lut
 
@@ -161,6 +162,9 @@ class PoolState:
         self.residual_events = []  # (start, end) HIP events around each residual call (with gram_events)
         self.forest_events = None  # list -> (start, end) HIP events around each forest-score call
         self.select_events = None  # list -> (start, end) HIP events around each dal_dw_select call
+        # list -> (start, end) around event_repeat selection-only launches of the
+        # fused step (bench; single GPU, fast level 1)
+        self.step_select_events = None
         # bench: a GPU spin (torch.cuda._sleep cycles) queued before each timed
         # call's start event, so the call's launches are all submitted before
         # the GPU reaches them -- the events then bracket the device span, not
@@ -809,7 +813,54 @@ def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: 
     idx, sel_scores, _ = dw_select_local(state, flags, votes, keys_lo, keys_hi, lut_dev, kk, beta,
                                          state.colsum(), colsum_ready=colsum_ready)
     state.check_status(state.last_status)  # the word dw_select_local read (no second sync)
+    if state.select_events is not None and state.step_select_events is not None and state.level1_fast:
+        _time_step_select(state, forest, flags, dens, lut_dev, kk, beta)
     return Selection(scores=(scores, loc), indices=idx, selected_scores=sel_scores, votes=(votes, loc))
+
+
+def _time_step_select(state: PoolState, forest: Forest, flags, dens, lut_dev, k: int, beta: float):
+    """bench: the selection launch of the fused step (what dal_dw_step and the
+    warm plan run after the score kernel folded the row-group minima) timed on
+    its own: one full dal_dw_step that keeps the minima, then event_repeat
+    DAL_STEP_SELECT_ONLY calls between two events (behind a GPU spin), then one
+    more that clears them.  The selections must equal the step's."""
+    torch = _torch()
+    lib = _lib.load()
+    n, dev = state.n, state.device
+    inner, leaf = forest.device(dev)
+    norm64, colsum = state.norms(), state.colsum()
+    base = candidate_cap(n, k) if state.cap_base is None else max(int(k), int(state.cap_base))
+    cap = int(min(n, base * state.cap_scale))
+    passes = level1_passes(state, n, k, cap)
+    if passes == 0:
+        return
+    wsb = int(lib.dal_dw_step_workspace_bytes(n, k, cap))
+    ws, wsp = workspace(wsb, dev)
+    ws.zero_()
+    bufs = [torch.empty(n, dtype=t, device=dev) for t in (torch.int32, torch.float64, torch.int64, torch.int64)]
+    outs = [(torch.empty(k, dtype=torch.int64, device=dev), torch.empty(k, dtype=torch.float64, device=dev))
+            for _ in range(2)]
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def step(flags_bits, out):
+        call("dal_dw_step", _ptr(state.x), n, state.d, state.d, _ptr(inner), _ptr(leaf), forest.n_trees,
+             forest.depth, _ptr(lut_dev), _ptr(dens), float(density_error(state)), _ptr(flags), float(beta),
+             state.row_base, _ptr(norm64), _ptr(colsum), k, cap, passes, flags_bits, wsp, wsb,
+             *[_ptr(b) for b in bufs], _ptr(out[0]), _ptr(out[1]), 0, _ptr(status), 0, _stream(dev))
+
+    step(DAL_STEP_WS_CLEAN | DAL_STEP_KEEP_GROUPS, outs[0])
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    if state.event_lead_cycles:
+        torch.cuda._sleep(state.event_lead_cycles)
+    ev[0].record()
+    for _ in range(state.event_repeat):
+        step(DAL_STEP_WS_CLEAN | DAL_STEP_KEEP_GROUPS | DAL_STEP_SELECT_ONLY, outs[1])
+    ev[1].record()
+    step(DAL_STEP_WS_CLEAN | DAL_STEP_SELECT_ONLY, outs[1])  # the last one clears the minima
+    if int(status.item()) != 0 or not (torch.equal(outs[0][0], outs[1][0]) and
+                                      torch.equal(outs[0][1].view(torch.int64), outs[1][1].view(torch.int64))):
+        return  # (an overflow or a mismatch: no timing recorded)
+    state.step_select_events.append(ev)
 
 
 class WarmStepGraph:

@@ -297,9 +297,22 @@ int dal_dw_select(const uint64_t* keys_lo, const uint64_t* keys_hi, const int32_
  *                          dal_dw_step left it so, or the caller zeroed the
  *                          workspace once): no zeroing launch.  The header is
  *                          left zero on exit whenever this flag is given.
+ *   DAL_STEP_KEEP_GROUPS   (ABI v8; fast level 1) the row-group minima the step
+ *                          folded are left in the workspace instead of cleared,
+ *                          so that DAL_STEP_SELECT_ONLY calls can re-run the
+ *                          selection; a later call without this flag clears them.
+ *   DAL_STEP_SELECT_ONLY   (ABI v8; with DAL_STEP_WS_CLEAN, fast level 1, no
+ *                          DAL_STEP_RESET_STATUS) only the selection launch: it
+ *                          re-reads the votes, keys and group minima that the
+ *                          previous call with DAL_STEP_KEEP_GROUPS left on the
+ *                          same buffers and workspace (the same arguments),
+ *                          and gives the same outputs.  Used to time the
+ *                          selection launch of the fused step on its own.
  * Workspace: dal_dw_step_workspace_bytes (== dal_dw_select's). */
 #define DAL_STEP_RESET_STATUS 1u
 #define DAL_STEP_WS_CLEAN 2u
+#define DAL_STEP_KEEP_GROUPS 4u
+#define DAL_STEP_SELECT_ONLY 8u
 size_t dal_dw_step_workspace_bytes(int64_t n, int64_t k, int64_t cap);
 int dal_dw_step(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner, const uint8_t* leaf,
                 int32_t n_trees, int32_t depth, const double* lut, const int64_t* density_fixed,

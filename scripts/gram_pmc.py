@@ -1,6 +1,7 @@
 """The density Gram (dal_gram_rowsum_sym + dal_gram_sym_residual) at one
 shape, a few launches, for rocprofv3 --pmc / --kernel-trace (one counter
-group per run).  usage: python scripts/gram_pmc.py NxD [reps]"""
+group per run).  usage: python scripts/gram_pmc.py NxD [reps] [LIB.so]
+(LIB.so: an A/B build, scripts/ab_build.sh, instead of the product library)"""
 import os
 import sys
 
@@ -11,7 +12,18 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import bench  # noqa: E402
+from dal import _lib  # noqa: E402
 from dal.engine import PoolState  # noqa: E402
+
+if len(sys.argv) > 3:  # bind an A/B build in place of the product library
+    import ctypes
+
+    lib = ctypes.CDLL(os.path.abspath(sys.argv[3]))
+    for name, (res, args) in _lib.SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib._lib = lib
 
 dev = torch.device("cuda:0")
 n, d = (int(v) for v in sys.argv[1].split("x"))

@@ -459,3 +459,62 @@ def test_fast_level1_region_and_capacity_boundaries(cuda, layout, extra):
     assert status == 0
     assert np.array_equal(idx, ref_idx)
     assert np.array_equal(sc.view(np.int64), ref_sc.view(np.int64))
+
+
+@pytest.mark.parametrize("n,d,trees", [(100_000, 64, 10), (300_000, 64, 10), (20_000, 32, 10)])
+def test_dw_step_select_only_repeats_the_selection(cuda, n, d, trees):
+    """DAL_STEP_KEEP_GROUPS leaves the folded row-group minima in the
+    workspace and DAL_STEP_SELECT_ONLY re-runs only the selection launch on
+    them (the bench times the fused step's selection this way): every repeat
+    gives the full step's bits, and the last call without KEEP_GROUPS leaves
+    the workspace as clean as a normal step (300,000 x 64: several score
+    blocks per group, atomic-max minima; 20,000 x 32: the minima from the
+    group_min pass)."""
+    import torch
+
+    from dal import _lib, engine
+    from dal._lib import DAL_STEP_KEEP_GROUPS, DAL_STEP_SELECT_ONLY, DAL_STEP_WS_CLEAN, call
+    from dal.forest import Forest
+
+    X = O.synthetic_pool(n, d, seed=8)
+    st = engine.PoolState(X, excluded=np.arange(10), device=cuda)
+    dens, colsum, norm64 = st.density_fixed(), st.colsum(), st.norms()
+    flags, _, _ = st.row_flags(np.arange(10, n))
+    F = Forest.synthetic(trees, 4, d, seed=3)
+    inner, leaf = F.device(cuda)
+    lut = engine.device_lut("entropy", trees, cuda)
+    lib = _lib.load()
+    k = 100
+    cap = engine.candidate_cap(n, k)
+    wsb = int(lib.dal_dw_step_workspace_bytes(n, k, cap))
+    ws, wsp = engine.workspace(wsb, cuda)
+    ws.zero_()
+    P = lambda t: t.data_ptr()  # noqa: E731
+    bufs = [torch.empty(n, dtype=t, device=cuda) for t in (torch.int32, torch.float64, torch.int64, torch.int64)]
+    S = torch.cuda.current_stream(cuda).cuda_stream
+
+    def step(bits):
+        i = torch.empty(k, dtype=torch.int64, device=cuda)
+        c = torch.empty(k, dtype=torch.float64, device=cuda)
+        st.status.zero_()
+        call("dal_dw_step", P(st.x), n, d, d, P(inner), P(leaf), trees, 4, P(lut), P(dens),
+             float(engine.density_error(st)), P(flags), 1.0, 0, P(norm64), P(colsum), k, cap, 1, bits, wsp, wsb,
+             *[P(b) for b in bufs], P(i), P(c), 0, P(st.status), 0, S)
+        assert int(st.status.item()) == 0
+        return i, c
+
+    i0, c0 = step(DAL_STEP_WS_CLEAN | DAL_STEP_KEEP_GROUPS)
+    for _ in range(3):
+        i1, c1 = step(DAL_STEP_WS_CLEAN | DAL_STEP_KEEP_GROUPS | DAL_STEP_SELECT_ONLY)
+        assert torch.equal(i1, i0) and torch.equal(c1.view(torch.int64), c0.view(torch.int64))
+    i1, c1 = step(DAL_STEP_WS_CLEAN | DAL_STEP_SELECT_ONLY)
+    assert torch.equal(i1, i0)
+    _, ref_idx, ref_ss = O.density_select(X, np.arange(10, n), O.synthetic_forest(trees, 4, d, seed=3), k, 1.0,
+                                          np.arange(10))
+    assert np.array_equal(i0.cpu().numpy(), ref_idx)
+    # a normal step on the same workspace after the sequence: the minima were cleared
+    i2, c2 = step(DAL_STEP_WS_CLEAN)
+    assert torch.equal(i2, i0) and torch.equal(c2.view(torch.int64), c0.view(torch.int64))
+    # flag combinations outside the contract are refused before any launch
+    with pytest.raises(_lib.DalError):
+        step(DAL_STEP_SELECT_ONLY)  # without WS_CLEAN
