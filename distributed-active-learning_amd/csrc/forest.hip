@@ -34,6 +34,14 @@ constexpr int kForestThreads = DAL_FOREST_THREADS;
 #define DAL_FOREST_ILP 4
 #endif
 constexpr int kTreeIlp = DAL_FOREST_ILP;  // independent tree walks in flight per lane
+// Timing-only A/B (scripts/ab_build.sh -DDAL_FOREST_BITMASK=1; verdict r4 item
+// 5): depth-4 trees evaluated whole -- every wave walks one tree at a time for
+// 64 rows, reads the tree's 15 nodes at wave-uniform LDS addresses, gathers
+// and compares all 15 predicates (no dependent node-then-feature round trips),
+// then resolves the leaf from the 15-bit mask.  0 in the product.
+#ifndef DAL_FOREST_BITMASK
+#define DAL_FOREST_BITMASK 0
+#endif
 
 struct ForestArgs {
   const float* x;
@@ -126,14 +134,38 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
   const int n_leaf = 1 << A.depth;
   const int tid = threadIdx.x;
   const int64_t row0 = tile * R;
-  const int r = tid / tpr, sub = tid - r * tpr;
+  // bitmask form: wave w holds rows (w / tpr) * 64 + lane and trees w % tpr, +tpr, ...
+  const bool bm = DAL_FOREST_BITMASK && X_LDS && A.depth == 4 && R * tpr == kForestThreads && R % 64 == 0;
+  const int r = bm ? (tid >> 6) / tpr * 64 + (tid & 63) : tid / tpr;
+  const int sub = bm ? (tid >> 6) % tpr : tid - r * tpr;
   const int64_t row = row0 + r;
   const bool live = r < R && row < A.n;
 
   const float* xrow = X_LDS ? xs + r * xstride : A.x + (live ? row : 0) * A.ldx;
 
   int v = 0;
-  if (live) {
+  if (DAL_FOREST_BITMASK && bm) {
+    if (live) {
+      for (int t = sub; t < A.n_trees; t += tpr) {  // (wave-uniform tree)
+        const int2* nd = inner + t * 15;
+        unsigned m = 0;
+#pragma unroll
+        for (int h = 0; h < 15; ++h) {
+          const int2 q = nd[h];  // the same address in every lane: an LDS broadcast
+          m |= (xrow[q.x] <= __int_as_float(q.y) ? 1u : 0u) << h;
+        }
+        int h = 0;
+#pragma unroll
+        for (int l = 0; l < 4; ++l) h = 2 * h + 2 - static_cast<int>((m >> h) & 1u);
+        v += leaf[t * 16 + (h - 15)];
+      }
+    }
+    __shared__ int s_vote[kForestThreads];
+    s_vote[sub * R + r] = v;
+    __syncthreads();
+    if (sub == 0)
+      for (int q = 1; q < tpr; ++q) v += s_vote[q * R + r];
+  } else if (live) {
     int t = sub;
     for (; t + (kTreeIlp - 1) * tpr < A.n_trees; t += kTreeIlp * tpr) {
       int h[kTreeIlp];
@@ -160,7 +192,8 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
     }
   }
   // row's TPR threads are consecutive lanes
-  for (int o = 1; o < tpr; o <<= 1) v += __shfl_xor(v, o);
+  if (!bm)
+    for (int o = 1; o < tpr; o <<= 1) v += __shfl_xor(v, o);
   unsigned long long klo = DAL_KEY_NONE, khi = DAL_KEY_NONE;
   if (live && sub == 0) {
     const uint8_t fl = pre ? fl_pre : A.flags ? row_flag(A, row) : DAL_ROW_CANDIDATE;

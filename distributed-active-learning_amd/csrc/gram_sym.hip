@@ -122,7 +122,7 @@ __device__ __forceinline__ unsigned fresh_lane() {
 #define DAL_GRAM_PRIO8 1  // 8-wave kernel: s_setprio 1 for waves 4-7 (> 0) or 0-3 (< 0)
 #endif
 #ifndef DAL_GRAM_KS64_OCC
-#define DAL_GRAM_KS64_OCC 3  // KS 64: 4-wave blocks per CU (3: 16 KiB stages; 100k x 64 -3.2 %, 200k x 64 -3.9 %, 1M x 64 +0.6 % vs 2)
+#define DAL_GRAM_KS64_OCC 4  // KS 64: 4-wave blocks per CU (3: 16 KiB stages, 100k x 64 -3.2 % vs 2; row sums only, 128 VGPRs: 4 blocks on 8 KiB stages 100k x 64 -0.7 %, 200k x 64 -0.5 % vs 3)
 #endif
 #ifndef DAL_GRAM_NCH128
 #define DAL_GRAM_NCH128 1  // row-sum chains per row tile at KS 128 (2: 240 VGPRs, no spill; KS <= 64 keep 1)

@@ -1,5 +1,6 @@
 """dal_forest_score at one BASELINE shape, a few launches, for rocprofv3 --pmc
-(FETCH_SIZE / WRITE_SIZE in separate passes).  usage: python scripts/forest_pmc.py NxDxT [reps]"""
+(FETCH_SIZE / WRITE_SIZE in separate passes).  usage: python scripts/forest_pmc.py NxDxT [reps] [LIB.so]
+(LIB.so: an A/B build, scripts/ab_build.sh, instead of the product library)"""
 import os
 import sys
 
@@ -10,7 +11,17 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import bench  # noqa: E402
-from dal import engine  # noqa: E402
+from dal import _lib, engine  # noqa: E402
+
+if len(sys.argv) > 3:  # bind an A/B build in place of the product library
+    import ctypes
+
+    lib = ctypes.CDLL(os.path.abspath(sys.argv[3]))
+    for name, (res, args) in _lib.SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib._lib = lib
 from dal._lib import DAL_DESCENDING  # noqa: E402
 from dal.forest import Forest  # noqa: E402
 
