@@ -300,7 +300,10 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
   // d + 4 (rows stay 16-B aligned, one ds_write_b128 per load, consecutive
   // lanes on consecutive banks; rows of a wave start 4 banks apart)
   const int xstride = A.d + (pad4 ? 4 : 1);
-  const int r = tid / tpr, sub = tid - r * tpr;
+  // (the row / tree-phase mapping of score_tile: the bitmask form's row leaders differ)
+  const bool bm = DAL_FOREST_BITMASK && X_LDS && A.depth == 4 && R * tpr == kForestThreads && R % 64 == 0;
+  const int r = bm ? (tid >> 6) / tpr * 64 + (tid & 63) : tid / tpr;
+  const int sub = bm ? (tid >> 6) % tpr : tid - r * tpr;
   GroupFold fold;  // the previous tile's group fold, not yet issued (persistent kernel)
   __shared__ unsigned long long wmin[2][2][kForestWaves];
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {  // block-uniform

@@ -471,11 +471,6 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
 //  3. per row r of the requested super blocks: acc[r] += rint(2^8 *
 //     (<L_r, R_B> + <u~_r, C_B>)) with the dots in fp64 in a fixed order.
 
-// operand element (H or L half) of feature f of a row
-__device__ __forceinline__ const uint16_t* half_ptr(const uint16_t* row, int f, int ks, bool lo) {
-  return row + (f / ks) * (2 * ks) + (lo ? ks : 0) + (f % ks);
-}
-
 __device__ __forceinline__ long long half_units(uint16_t bits) {  // fp16 value * 2^24, exact
   return static_cast<long long>(static_cast<float>(__builtin_bit_cast(_Float16, bits)) * 16777216.0f);
 }
@@ -495,13 +490,16 @@ __global__ __launch_bounds__(256) void csym_sigma_kernel(const uint16_t* __restr
   const int col = blockIdx.y * 256 + threadIdx.x % cols;
   const int rstep = 256 / cols;                    // rows advanced per round
   const int r0 = threadIdx.x / cols;
+  // this block's rows of the super block: [rb, re) (gridDim.z row slices)
+  const int rb = kSB * static_cast<int>(blockIdx.z) / static_cast<int>(gridDim.z);
+  const int re = kSB * (static_cast<int>(blockIdx.z) + 1) / static_cast<int>(gridDim.z);
   long long acc[8] = {};
   if (col < cpr && r0 < rstep) {
     const uint4* base = reinterpret_cast<const uint4*>(ops + static_cast<int64_t>(Q) * kSB * ldh) + col;
-    for (int r = r0; r < kSB; r += 8 * rstep) {
+    for (int r = rb + r0; r < re; r += 8 * rstep) {
       uint4 q[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) q[j] = r + j * rstep < kSB ? base[static_cast<int64_t>(r + j * rstep) * cpr] : uint4{};
+      for (int j = 0; j < 8; ++j) q[j] = r + j * rstep < re ? base[static_cast<int64_t>(r + j * rstep) * cpr] : uint4{};
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const uint32_t w[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
@@ -598,33 +596,52 @@ __global__ __launch_bounds__(64 * kScanWaves) void csym_scan_kernel(const long l
   }
 }
 
-// one wave per row: lane l takes features l, l+64, ... (sequential fp64 per
-// lane, then a fixed butterfly) -- a fixed order, so the bits are the same on
-// every GPU count.  rows: the operand of the requested super blocks.
-__global__ __launch_bounds__(256) void csym_residual_kernel(const uint16_t* __restrict__ rows, int64_t ldh, int ks,
-                                                            int d_pad, int b0, int n_rows,
-                                                            const double* __restrict__ rb,
-                                                            const double* __restrict__ cb,
-                                                            long long* __restrict__ acc) {
-  const int lane = threadIdx.x & 63;
-  const int64_t rr = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  if (rr >= n_rows) return;
-  const uint16_t* row = rows + rr * ldh;
-  const int64_t B = rr / kSB;  // relative to b0
-  const double* R = rb + B * d_pad;
-  const double* Cc = cb + B * d_pad;
-  double t = 0.0;
-  for (int f = lane; f < d_pad; f += 64) {
-    const double h = static_cast<double>(static_cast<float>(__builtin_bit_cast(_Float16, *half_ptr(row, f, ks, false))));
-    const double l = static_cast<double>(static_cast<float>(__builtin_bit_cast(_Float16, *half_ptr(row, f, ks, true))));
-    t = t + l * R[f];
-    t = t + (h + l) * Cc[f];
+// One thread per row: a block's 256 rows lie in one super block B, whose R_B
+// and C_B are staged in LDS once; each thread sums its row's features in
+// order, t = t + l_f R_f, t = t + (h_f + l_f) C_f for f = 0, 1, ... (fp64, no
+// FMA) -- a fixed order, so the bits are the same on every GPU count.  The
+// row's operand is read 16 B (8 halves) at a time.  rows: the operand of the
+// requested super blocks.  (Round 4: one wave per row, lanes over features and
+// a butterfly -- 2-byte loads, 57 us of the 0.81 ms config-2 Gram.)
+constexpr int kResRows = 256;
+__global__ __launch_bounds__(kResRows) void csym_residual_kernel(const uint16_t* __restrict__ rows, int64_t ldh, int ks,
+                                                                 int d_pad, int b0, int n_rows,
+                                                                 const double* __restrict__ rb,
+                                                                 const double* __restrict__ cb,
+                                                                 long long* __restrict__ acc) {
+  extern __shared__ double rc[];  // [d_pad] R_B | [d_pad] C_B
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kResRows;  // (a multiple of 256: one super block)
+  const int64_t B = r0 / kSB;                                       // relative to b0
+  for (int f = threadIdx.x; f < d_pad; f += kResRows) {
+    rc[f] = rb[B * d_pad + f];
+    rc[d_pad + f] = cb[B * d_pad + f];
   }
+  __syncthreads();
+  const int64_t rr = r0 + threadIdx.x;
+  if (rr >= n_rows) return;
+  const uint4* row = reinterpret_cast<const uint4*>(rows + rr * ldh);
+  const int hs = ks / 8;  // 16-B chunks per half of a slice
+  double t = 0.0;
+  for (int s0 = 0; s0 < d_pad; s0 += ks) {
+    const uint4* sl = row + (s0 / ks) * 2 * hs;
+    for (int c = 0; c < hs; ++c) {
+      const uint4 hq = sl[c], lq = sl[hs + c];
+      const uint32_t hw[4] = {hq.x, hq.y, hq.z, hq.w}, lw[4] = {lq.x, lq.y, lq.z, lq.w};
 #pragma unroll
-  for (int sh = 32; sh >= 1; sh >>= 1) t += __shfl_xor(t, sh);
+      for (int e = 0; e < 8; ++e) {
+        const int f = s0 + c * 8 + e;
+        const uint16_t hb = static_cast<uint16_t>(e & 1 ? hw[e >> 1] >> 16 : hw[e >> 1] & 0xFFFFu);
+        const uint16_t lb = static_cast<uint16_t>(e & 1 ? lw[e >> 1] >> 16 : lw[e >> 1] & 0xFFFFu);
+        const double h = static_cast<double>(static_cast<float>(__builtin_bit_cast(_Float16, hb)));
+        const double l = static_cast<double>(static_cast<float>(__builtin_bit_cast(_Float16, lb)));
+        t = t + l * rc[f];
+        t = t + (h + l) * rc[d_pad + f];
+      }
+    }
+  }
   // R, C in units of 2^-24 x (split units); value = t * 2^-24 * 2^-24 ... in
   // fixed point (2^32): t * 2^-24 (operand units^2 = 2^24 x value) * 2^8
-  if (lane == 0 && t != 0.0) acc[static_cast<int64_t>(b0) * kSB + rr] += static_cast<long long>(__builtin_rint(t * 0x1p-16));
+  if (t != 0.0) acc[static_cast<int64_t>(b0) * kSB + rr] += static_cast<long long>(__builtin_rint(t * 0x1p-16));
 }
 
 // ---------------------------------------------------------------------------
@@ -925,18 +942,19 @@ extern "C" int dal_gram_sym_residual(const uint16_t* ops, int64_t nb_active, int
   const int ks = split_ks(d_pad);
   const int64_t ldh = 2 * d_pad;
   if (hipMemsetAsync(sig_u, 0, static_cast<size_t>(na * d_pad) * 8, st) != hipSuccess) return DAL_ERR_HIP;
+  // rows of a super block over 4 blocks (more loads in flight: 196 super blocks at config 2)
   hipLaunchKernelGGL(csym_sigma_kernel,
-                     dim3(static_cast<unsigned>(na), static_cast<unsigned>(ceil_div(ldh / 8, 256))), dim3(256), 0, st,
-                     ops, ldh, ks, static_cast<int>(d_pad), sig_u);
+                     dim3(static_cast<unsigned>(na), static_cast<unsigned>(ceil_div(ldh / 8, 256)), 4), dim3(256), 0,
+                     st, ops, ldh, ks, static_cast<int>(d_pad), sig_u);
   DAL_RETURN_IF_LAUNCH_FAILED();
   hipLaunchKernelGGL(csym_scan_kernel, dim3(static_cast<unsigned>(ceil_div(d_pad, 64))), dim3(64 * kScanWaves), 0, st, sig_u,
                      static_cast<int>(na), static_cast<int>(d_pad), static_cast<int>(s0), static_cast<int>(s0 + ns),
                      rb, cb);
   DAL_RETURN_IF_LAUNCH_FAILED();
   const int64_t n_rows = ns * kSB;
-  hipLaunchKernelGGL(csym_residual_kernel, dim3(static_cast<unsigned>(ceil_div(n_rows, 4))), dim3(256), 0, st,
-                     ops + s0 * kSB * ldh, ldh, ks, static_cast<int>(d_pad), static_cast<int>(s0),
-                     static_cast<int>(n_rows), rb, cb, reinterpret_cast<long long*>(acc));
+  hipLaunchKernelGGL(csym_residual_kernel, dim3(static_cast<unsigned>(ceil_div(n_rows, kResRows))), dim3(kResRows),
+                     static_cast<size_t>(2 * d_pad) * 8, st, ops + s0 * kSB * ldh, ldh, ks, static_cast<int>(d_pad),
+                     static_cast<int>(s0), static_cast<int>(n_rows), rb, cb, reinterpret_cast<long long*>(acc));
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
 }
