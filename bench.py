@@ -274,30 +274,45 @@ def _traffic(config, key, world):
         return None
 
 
-def forest_roofline(n_rows, d, trees, forest_ms, config, world):
+def forest_roofline(n_rows, d, trees, forest_ms, config, world, used_features=None):
     """K2 (dal_forest_score, density mode).  Algorithmic bytes per launch =
     every row's features once (n*d*4) + row flag (1) + fixed-point density in
     (8) + votes (4) + fp64 score (8) + the two interval keys (16).  At T = 10
     the kernel streams HBM; at T = 100 (config 3) the LDS traversal (4 levels
     x T trees per row: a node read + a feature gather per level) and its
     instruction issue bound it, so the HBM fraction is reported with bound
-    "lds-issue" (counters: profiles/r02/forest_config3_pmc.csv)."""
+    "lds-issue" (counters: profiles/r02/forest_config3_pmc.csv).
+    used_features: the warm steps ran the blocked kernel (ABI v9,
+    dal_forest_score_blocked), which reads only the forest's distinct tested
+    features: those count instead of d (the row-major kernel's bytes are
+    reported beside)."""
     if not forest_ms:
         return None
-    per_row = d * 4 + 1 + 8 + 4 + 8 + 16
+    tail = 1 + 8 + 4 + 8 + 16
+    feats = d if used_features is None else used_features
+    per_row = feats * 4 + tail
     nbytes = float(n_rows) * per_row
     gbs = nbytes / (forest_ms * 1e-3) / 1e9
+    kernel = (f"dal_forest_score (T={trees} depth-4 trees, LDS-resident SoA; "
+              "votes -> LUT -> density-weighted interval keys)")
+    if used_features is not None:
+        kernel = (f"dal_forest_score_blocked (T={trees} depth-4 trees over the pool's blocked feature-major copy: "
+                  f"the {used_features} of {d} features the forest tests, 256-B runs per 64-row tile by LDS-DMA; "
+                  "votes -> LUT -> density-weighted interval keys)")
     out = {"bound": "hbm" if trees <= 32 else "lds-issue",
-           "kernel": f"dal_forest_score (T={trees} depth-4 trees, LDS-resident SoA; "
-                     "votes -> LUT -> density-weighted interval keys)",
+           "kernel": kernel,
            "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
-           "traffic": _traffic(config, "forest_score_bytes_per_launch", world), "launch_ms": forest_ms,
+           "traffic": _traffic(config, "forest_blocked_bytes_per_launch" if used_features is not None
+                               else "forest_score_bytes_per_launch", world), "launch_ms": forest_ms,
            "algorithmic_bytes_per_launch": nbytes, "bytes_per_row": per_row,
            "note": "timed with HIP events on the launch stream over the warm steps (density cached), each call queued behind a GPU spin and issued 10x back to back between the events (device time per call incl. its launch gaps; no host submission gaps, event cost amortised)"}
     if trees > 32:
         out["counters"] = ("PMC per launch at config 3 (profiles/r02/forest_config3_pmc.csv): LDS array busy "
                            "SQ_LDS_IDX_ACTIVE, 42% of it bank-conflict cycles (lane-divergent feature gathers); "
                            "waves parked on s_waitcnt 51% / issue-stalled 22% / issuing 27% of their cycles")
+    if used_features is not None:
+        out["used_features"] = used_features
+        out["row_major_bytes_per_row"] = d * 4 + tail
     return out
 
 
@@ -524,7 +539,7 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
                          f"({idx_g[:8].tolist()} vs {idx_s[:8].tolist()})")
 
     # warm path: density cached (the reference's density is constant per pool)
-    warm_ms = forest_ms = select_ms = step_select_ms = None
+    warm_ms = forest_ms = select_ms = step_select_ms = forest_used = None
     warm_same = None
     if warm_steps > 0:
         step()
@@ -540,6 +555,9 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
         state.event_lead_cycles, state.event_repeat = 0, 1
         if fev:
             forest_ms = sum(a.elapsed_time(b) for a, b in fev) / len(fev) / EVENT_REPEAT
+            # the warm steps' K2 read the blocked copy: the forest's distinct tested features
+            if state._xb is not None:
+                forest_used = int(np.unique(forest.inner[..., 0]).size)
         if sev:
             select_ms = sum(a.elapsed_time(b) for a, b in sev) / len(sev) / EVENT_REPEAT
         if ssev:
@@ -626,7 +644,8 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
                       if sep_ms else None),
         "roofline": dict(gram_roofline(state.gram, achieved, traffic, gram_ms, gram_ms_max, flops,
                                        engine.gram_products(state)), residual_ms=resid_ms),
-        "roofline_forest": forest_roofline(state.n, d, cfg["trees"], forest_ms, config, world),
+        "roofline_forest": forest_roofline(state.n, d, cfg["trees"], forest_ms, config, world,
+                                           used_features=forest_used),
         "roofline_topk": topk_roofline(state.n, select_ms, config, world,
                                        engine.LEVEL1_PASSES if state.level1_fast else 0, step_select_ms),
         "cpu_baseline": None,
@@ -823,7 +842,7 @@ def _r(v, nd=4):
 
 
 def _roof_short(r, keys=("bound", "achieved", "peak", "unit", "frac", "traffic", "launch_ms",
-                         "fused_step_select_ms")):
+                         "fused_step_select_ms", "used_features")):
     if not r:
         return None
     return {k: _r(r.get(k), 5 if k in ("frac", "launch_ms", "fused_step_select_ms") else 4) for k in keys

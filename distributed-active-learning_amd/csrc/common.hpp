@@ -120,9 +120,12 @@ struct ForestStepHooks {
 
 // Rows per block of dal_forest_score's kernel for this shape (the row
 // groups of ForestStepHooks::gmin are whole blocks).
-int forest_rows_per_block(const float* x, int64_t d, int64_t ldx, int32_t n_trees);
+// xb: the pool's blocked feature-major copy (dal_pool_blocked) or null; the
+// blocked path (64-row tiles) runs when the forest is small enough.
+int forest_rows_per_block(const float* x, const float* xb, int64_t d, int64_t ldx, int32_t n_trees,
+                          int32_t depth);
 
-int forest_score_launch(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
+int forest_score_launch(const float* x, const float* xb, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
                         const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
                         const void* density, int density_kind, double density_err, const uint8_t* row_flags,
                         double beta, int order, int32_t* votes, double* scores, uint64_t* keys,
@@ -131,7 +134,8 @@ int forest_score_launch(const float* x, int64_t n, int64_t d, int64_t ldx, const
 // dal_dw_step with the plan's publishing hooks (topk.hip, SortTail): the
 // selection is also written to *out_slot (a host-mapped word holding a device
 // address; nullable) and the final status word to *status_mirror (host-mapped).
-int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner, const uint8_t* leaf,
+int dw_step_impl(const float* x, const float* xb, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
+                 const uint8_t* leaf,
                  int32_t n_trees, int32_t depth, const double* lut, const int64_t* density_fixed, double density_err,
                  const uint8_t* row_flags, double beta, int64_t idx_base, const double* norm64, const double* colsum,
                  int64_t k, int64_t cap, int32_t level1_passes, uint32_t step_flags, void* ws, size_t ws_bytes,

@@ -125,7 +125,10 @@ __device__ __forceinline__ void issue_fold(const ForestArgs& A, GroupFold& f,
 // and the tile's minimum keys folded into its row group (hooks.gmin).  With
 // several blocks per group in the persistent kernel (wmin non-null) the
 // fold is left pending (GroupFold, issue_fold).
-template <bool X_LDS>
+// WROWS (the blocked feature-major path): wave w holds rows (w / tpr) * 64 +
+// lane and walks trees w % tpr, + tpr, ...; the waves' partial votes of a row
+// are summed through LDS.
+template <bool X_LDS, bool WROWS = false>
 __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs, int xstride, int64_t tile, int R,
                                            int tpr, const int2* inner, const uint8_t* leaf, bool pre,
                                            uint8_t fl_pre, long long dens_pre, GroupFold& fold,
@@ -136,8 +139,9 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
   const int64_t row0 = tile * R;
   // bitmask form: wave w holds rows (w / tpr) * 64 + lane and trees w % tpr, +tpr, ...
   const bool bm = DAL_FOREST_BITMASK && X_LDS && A.depth == 4 && R * tpr == kForestThreads && R % 64 == 0;
-  const int r = bm ? (tid >> 6) / tpr * 64 + (tid & 63) : tid / tpr;
-  const int sub = bm ? (tid >> 6) % tpr : tid - r * tpr;
+  const bool wr = WROWS || bm;  // rows by wave lanes, trees by waves
+  const int r = wr ? (tid >> 6) / tpr * 64 + (tid & 63) : tid / tpr;
+  const int sub = wr ? (tid >> 6) % tpr : tid - r * tpr;
   const int64_t row = row0 + r;
   const bool live = r < R && row < A.n;
 
@@ -160,11 +164,6 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
         v += leaf[t * 16 + (h - 15)];
       }
     }
-    __shared__ int s_vote[kForestThreads];
-    s_vote[sub * R + r] = v;
-    __syncthreads();
-    if (sub == 0)
-      for (int q = 1; q < tpr; ++q) v += s_vote[q * R + r];
   } else if (live) {
     int t = sub;
     for (; t + (kTreeIlp - 1) * tpr < A.n_trees; t += kTreeIlp * tpr) {
@@ -191,9 +190,15 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
       v += leaf[t * n_leaf + (h - n_inner)];
     }
   }
-  // row's TPR threads are consecutive lanes
-  if (!bm)
+  if (wr) {  // a row's tree phases are in different waves
+    __shared__ int s_vote[kForestThreads];
+    s_vote[sub * R + r] = v;
+    __syncthreads();
+    if (sub == 0)
+      for (int q = 1; q < tpr; ++q) v += s_vote[q * R + r];
+  } else {  // a row's TPR threads are consecutive lanes
     for (int o = 1; o < tpr; o <<= 1) v += __shfl_xor(v, o);
+  }
   unsigned long long klo = DAL_KEY_NONE, khi = DAL_KEY_NONE;
   if (live && sub == 0) {
     const uint8_t fl = pre ? fl_pre : A.flags ? row_flag(A, row) : DAL_ROW_CANDIDATE;
@@ -396,12 +401,136 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
   if (PERSIST && tid == 0) issue_fold(A, fold, wmin);  // the last tile's (its waves passed the loop barrier)
 }
 
+// ---------------------------------------------- blocked feature-major path --
+// dal_pool_blocked: the pool as tiles of kBlk rows, feature-major inside a
+// tile: xb[(tile * d + f) * kBlk + r] = x[tile * kBlk + r][f] (rows past n are
+// zero).  A tile's feature f is one contiguous 256-B run, so a kernel that
+// needs only some features of a tile reads only those runs.
+constexpr int kBlk = 64;
+
+__global__ __launch_bounds__(256) void pool_blocked_kernel(const float* __restrict__ x, int64_t n, int d,
+                                                           int64_t ldx, float* __restrict__ xb) {
+  __shared__ float t[kBlk][kBlk + 1];
+  const int64_t tile = blockIdx.x;
+  const int tid = threadIdx.x;
+  for (int f0 = 0; f0 < d; f0 += kBlk) {
+    for (int e = tid; e < kBlk * kBlk; e += 256) {  // row-major reads (coalesced along f)
+      const int r = e / kBlk, c = e % kBlk;
+      const int64_t row = tile * kBlk + r;
+      t[r][c] = row < n && f0 + c < d ? x[row * ldx + f0 + c] : 0.0f;
+    }
+    __syncthreads();
+    for (int e = tid; e < kBlk * kBlk; e += 256) {  // feature-major writes (coalesced along r)
+      const int c = e / kBlk, r = e % kBlk;
+      if (f0 + c < d) xb[(tile * d + f0 + c) * kBlk + r] = t[r][c];
+    }
+    __syncthreads();
+  }
+}
+
+// Forest votes + score over the blocked copy, reading only the features the
+// forest tests.  Each block (persistent grid) first lists the forest's
+// distinct features (a bitmap over d, prefix popcounts) and rewrites every
+// LDS node's feature as its slot in that list (times kBlk); a 64-row tile is
+// then staged by LDS-DMA as the listed features' 256-B runs only (four runs
+// per global_load_lds_dwordx4: lane l loads 16 B of run 4i + l / 16), and
+// scored with the rows on the lanes of every wave and the trees dealt over
+// the waves (x of row r, slot s at xs[s * kBlk + r]: a wave's 64 lanes read
+// 64 consecutive words of a run whatever slot each lane's tree asks for --
+// no bank conflicts).  Bytes per row: 4 F_used + the epilogue's, against
+// 4 d for the row-major tile (config 4, T = 10: ~113 of 256 features).
+__global__ __launch_bounds__(kForestThreads) void forest_blocked_kernel(ForestArgs A, const float* __restrict__ xb,
+                                                                        int fu_max, int64_t n_tiles) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int tpr = kForestWaves;  // one tree phase per wave, 64 rows per tile
+  const int n_inner = (1 << A.depth) - 1, n_leaf = 1 << A.depth;
+  const int nn = A.n_trees * n_inner, nw = (A.d + 31) >> 5;
+  float* xs = reinterpret_cast<float*>(smem);
+  int2* fs = reinterpret_cast<int2*>(smem + static_cast<size_t>(fu_max) * kBlk * 4);
+  uint8_t* ls = reinterpret_cast<uint8_t*>(fs + nn);
+  int* used = reinterpret_cast<int*>(ls + round_up(static_cast<int64_t>(A.n_trees) * n_leaf, 4));
+  unsigned* bits = reinterpret_cast<unsigned*>(used + fu_max);
+  int* pre = reinterpret_cast<int*>(bits + nw);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (A.hooks.status_reset && blockIdx.x == 0 && tid == 0) *A.hooks.status_reset = 0;
+  for (int w = tid; w < nw; w += kForestThreads) bits[w] = 0u;
+  for (int e = tid; e < A.n_trees * n_leaf; e += kForestThreads) ls[e] = A.leaf[e];
+  __syncthreads();
+  for (int e = tid; e < nn; e += kForestThreads) {
+    int2 q = A.inner[e];
+    q.x = q.x < 0 ? 0 : q.x >= A.d ? A.d - 1 : q.x;  // (a valid forest tests features < d)
+    fs[e] = q;
+    atomicOr(&bits[q.x >> 5], 1u << (q.x & 31));
+  }
+  __syncthreads();
+  for (int w = tid; w < nw; w += kForestThreads) {
+    int c = 0;
+    for (int j = 0; j < w; ++j) c += __popc(bits[j]);
+    pre[w] = c;
+  }
+  __syncthreads();
+  auto slot = [&](int f) { return pre[f >> 5] + __popc(bits[f >> 5] & ((1u << (f & 31)) - 1u)); };
+  for (int f = tid; f < A.d; f += kForestThreads)
+    if ((bits[f >> 5] >> (f & 31)) & 1u) used[slot(f)] = f;
+  for (int e = tid; e < nn; e += kForestThreads) fs[e].x = slot(fs[e].x) * kBlk;
+  const int fu = pre[nw - 1] + __popc(bits[nw - 1]);  // <= fu_max
+  __syncthreads();
+  const int n_ins = (fu + 3) >> 2;  // DMA instructions per tile (4 runs each)
+  typedef __attribute__((address_space(3))) float lds_float;
+  GroupFold fold;
+  __shared__ unsigned long long wmin[2][2][kForestWaves];
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {  // block-uniform
+    const int64_t row = tile * kBlk + lane;
+    const bool lead = wave == 0 && row < A.n;  // the rows' epilogue: wave 0
+    uint8_t fl_pre = DAL_ROW_CANDIDATE;
+    long long dens_pre = 0;
+    if (lead) {
+      if (A.flags) fl_pre = row_flag(A, row);
+      if (A.dkind) dens_pre = static_cast<const long long*>(A.density)[row];
+    }
+    const char* src = reinterpret_cast<const char*>(xb + tile * A.d * kBlk);
+    for (int i = wave; i < n_ins; i += kForestWaves) {
+      const int sl = 4 * i + (lane >> 4);
+      const unsigned dst = __builtin_amdgcn_readfirstlane(
+          static_cast<unsigned>(reinterpret_cast<uintptr_t>((lds_float*)(xs + 4 * i * kBlk))));
+      if (sl < fu) {
+        const unsigned voff = static_cast<unsigned>(used[sl]) * (kBlk * 4u) + static_cast<unsigned>(lane & 15) * 16u;
+        unsigned keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+            "global_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(voff), "s"(dst), "s"(src)
+            : "memory");
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) issue_fold(A, fold, wmin);  // after this tile's DMA wait
+    score_tile<true, true>(A, xs, 1, tile, kBlk, tpr, fs, ls, true, fl_pre, dens_pre, fold, wmin);
+    __syncthreads();  // every wave done with the tile before the next one is staged
+  }
+  if (tid == 0) issue_fold(A, fold, wmin);
+}
+
 }  // namespace
 }  // namespace dal
 
 namespace dal {
 
 namespace {
+// The blocked path's LDS bound on the forest's distinct features, or 0 when
+// the path does not apply: depth-limited complete-heap trees whose node count
+// bounds the distinct features at most 3/4 of d (fewer bytes than the
+// row-major tile by at least a quarter) and at most 150 runs of 256 B (four
+// blocks per CU).
+int blocked_fu_max(int64_t d, int32_t n_trees, int32_t depth) {
+  const int64_t nodes = static_cast<int64_t>(n_trees) * ((int64_t{1} << depth) - 1);
+  const int64_t fu = nodes < d ? nodes : d;
+  return fu * 4 <= 3 * d && fu <= 150 ? static_cast<int>(fu) : 0;
+}
+
 struct ForestTiling {
   int R;        // rows per block
   bool x_lds;   // pool rows staged in LDS
@@ -440,11 +569,13 @@ ForestTiling forest_tiling(const float* x, int64_t d, int64_t ldx, int32_t n_tre
 }
 }  // namespace
 
-int forest_rows_per_block(const float* x, int64_t d, int64_t ldx, int32_t n_trees) {
+int forest_rows_per_block(const float* x, const float* xb, int64_t d, int64_t ldx, int32_t n_trees,
+                          int32_t depth) {
+  if (xb && blocked_fu_max(d, n_trees, depth)) return kBlk;
   return forest_tiling(x, d, ldx, n_trees).R;
 }
 
-int forest_score_launch(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
+int forest_score_launch(const float* x, const float* xb, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
                         const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
                         const void* density, int density_kind, double density_err, const uint8_t* row_flags,
                         double beta, int order, int32_t* votes, double* scores, uint64_t* keys,
@@ -454,7 +585,35 @@ int forest_score_launch(const float* x, int64_t n, int64_t d, int64_t ldx, const
   if (density_kind < 0 || density_kind > 2 || (density_kind && !density)) return DAL_ERR_ARG;
   if (n < 0 || d < 1 || ldx < d || n_trees < 1) return DAL_ERR_SHAPE;
   if (depth < 1 || depth > DAL_MAX_TREE_DEPTH) return DAL_ERR_UNSUPPORTED;
+  if (xb && reinterpret_cast<uintptr_t>(xb) % 16 != 0) return DAL_ERR_ARG;
   if (n == 0) return DAL_OK;
+  if (const int fu_max = xb ? blocked_fu_max(d, n_trees, depth) : 0) {
+    const int64_t tiles = ceil_div(n, kBlk);
+    if (hooks_in.gmin &&
+        (hooks_in.group_blocks < 1 || ceil_div(tiles, hooks_in.group_blocks) != hooks_in.n_groups))
+      return DAL_ERR_ARG;
+    ForestArgs A{x, n, static_cast<int>(d), ldx, reinterpret_cast<const int2*>(inner), leaf, n_trees,
+                 depth, lut, density_kind ? density : nullptr, density_kind, density_err, row_flags, beta,
+                 order, votes, scores, keys, keys_hi, hooks_in};
+    const int64_t nn = static_cast<int64_t>(n_trees) * ((int64_t{1} << depth) - 1);
+    const int64_t nw = (d + 31) / 32;
+    const size_t smem = static_cast<size_t>(fu_max) * kBlk * 4 + static_cast<size_t>(nn) * 8 +
+                        static_cast<size_t>(round_up(static_cast<int64_t>(n_trees) << depth, 4)) +
+                        static_cast<size_t>(fu_max) * 4 + static_cast<size_t>(nw) * 8;
+    const void* fn = reinterpret_cast<const void*>(forest_blocked_kernel);
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1 ||
+        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(smem)) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kForestThreads, smem) != hipSuccess)
+      return DAL_ERR_HIP;
+    if (per_cu < 1) per_cu = 1;
+    const int64_t grid = tiles < static_cast<int64_t>(cus) * per_cu ? tiles : static_cast<int64_t>(cus) * per_cu;
+    hipLaunchKernelGGL(forest_blocked_kernel, dim3(static_cast<unsigned>(grid)), dim3(kForestThreads), smem, st, A,
+                       xb, fu_max, tiles);
+    DAL_RETURN_IF_LAUNCH_FAILED();
+    return DAL_OK;
+  }
   const ForestTiling T = forest_tiling(x, d, ldx, n_trees);
   const int R = T.R, tpr = kForestThreads / R;
   const int64_t blocks = ceil_div(n, R);
@@ -525,7 +684,37 @@ extern "C" int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ld
                                 const uint8_t* row_flags,
                                 double beta, int order, int32_t* votes, double* scores, uint64_t* keys,
                                 uint64_t* keys_hi, dal_stream_t stream) {
-  return forest_score_launch(x, n, d, ldx, inner, leaf, n_trees, depth, lut, density, density_kind, density_err,
-                             row_flags, beta, order, votes, scores, keys, keys_hi, ForestStepHooks{},
+  return forest_score_launch(x, nullptr, n, d, ldx, inner, leaf, n_trees, depth, lut, density, density_kind,
+                             density_err, row_flags, beta, order, votes, scores, keys, keys_hi, ForestStepHooks{},
+                             as_stream(stream));
+}
+
+extern "C" int dal_forest_blocked_rows(int64_t d, int32_t n_trees, int32_t depth) {
+  if (d < 1 || n_trees < 1 || depth < 1 || depth > DAL_MAX_TREE_DEPTH) return 0;
+  return blocked_fu_max(d, n_trees, depth) ? kBlk : 0;
+}
+
+extern "C" int64_t dal_pool_blocked_floats(int64_t n, int64_t d) {
+  return n < 0 || d < 1 ? -1 : ceil_div(n, kBlk) * kBlk * d;
+}
+
+extern "C" int dal_pool_blocked(const float* x, int64_t n, int64_t d, int64_t ldx, float* xb, dal_stream_t stream) {
+  if (!x || !xb) return DAL_ERR_ARG;
+  if (n < 0 || d < 1 || ldx < d || d > (int64_t{1} << 24)) return DAL_ERR_SHAPE;
+  if (n == 0) return DAL_OK;
+  hipLaunchKernelGGL(pool_blocked_kernel, dim3(static_cast<unsigned>(ceil_div(n, kBlk))), dim3(256), 0,
+                     as_stream(stream), x, n, static_cast<int>(d), ldx, xb);
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}
+
+extern "C" int dal_forest_score_blocked(const float* x, const float* xb, int64_t n, int64_t d, int64_t ldx,
+                                        const int32_t* inner, const uint8_t* leaf, int32_t n_trees, int32_t depth,
+                                        const double* lut, const void* density, int density_kind,
+                                        double density_err, const uint8_t* row_flags, double beta, int order,
+                                        int32_t* votes, double* scores, uint64_t* keys, uint64_t* keys_hi,
+                                        dal_stream_t stream) {
+  return forest_score_launch(x, xb, n, d, ldx, inner, leaf, n_trees, depth, lut, density, density_kind,
+                             density_err, row_flags, beta, order, votes, scores, keys, keys_hi, ForestStepHooks{},
                              as_stream(stream));
 }

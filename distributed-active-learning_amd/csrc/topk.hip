@@ -898,6 +898,9 @@ __device__ bool select_compact(const uint64_t* __restrict__ keys, const int64_t*
     s_mn[tid >> 6] = mn;
     s_mx[tid >> 6] = mx;
   }
+  // the radix histogram is zeroed here and then by the scanning wave as it
+  // reads each pass's bins: two barriers per pass instead of four
+  if (tid < 256) hist[tid] = 0u;
   __syncthreads();
 #pragma unroll
   for (int q = 0; q < kSortThreads / 64; ++q) {
@@ -911,8 +914,6 @@ __device__ bool select_compact(const uint64_t* __restrict__ keys, const int64_t*
   while (neq > static_cast<unsigned int>(kSelSmall) && top > 0) {  // (block-uniform)
     const int width = top < 8 ? top : 8, shift = top - width;
     const unsigned long long dmask = (1ull << width) - 1ull;
-    if (tid < 256) hist[tid] = 0u;
-    __syncthreads();
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       const bool valid = tid + j * kSortThreads < m && (key[j] & mask) == prefix;
@@ -928,11 +929,12 @@ __device__ bool select_compact(const uint64_t* __restrict__ keys, const int64_t*
       }
     }
     __syncthreads();
-    if (tid < 64) {  // one wave: 4 bins per lane, inclusive scan, locate krem
+    if (tid < 64) {  // one wave: 4 bins per lane (read, then zeroed for the next pass), inclusive scan, locate krem
       unsigned c[4], tot = 0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         c[q] = hist[lane * 4 + q];
+        hist[lane * 4 + q] = 0u;
         tot += c[q];
       }
       unsigned x = tot;
@@ -959,7 +961,6 @@ __device__ bool select_compact(const uint64_t* __restrict__ keys, const int64_t*
     neq = s_neq;
     mask |= dmask << shift;
     top = shift;
-    __syncthreads();
   }
   if (neq > static_cast<unsigned int>(kSelSmall)) return false;
   // the k - krem keys below the prefix and the neq keys in its bucket
@@ -1459,6 +1460,10 @@ __device__ unsigned long long group_threshold(const GroupSummary& S, int64_t k) 
     s_mx[w] = mx;
     s_nv[w] = nv;
   }
+  // the radix histogram is zeroed here (this barrier orders it before the
+  // first pass) and then by the scanning wave as it reads each pass's bins:
+  // two barriers per pass instead of three
+  if (tid < 256) hist[tid] = 0u;
   __syncthreads();
   nv = 0;
 #pragma unroll
@@ -1476,8 +1481,6 @@ __device__ unsigned long long group_threshold(const GroupSummary& S, int64_t k) 
   while (cnt > 64 && top > 0) {
     const int width = top < 8 ? top : 8, shift = top - width;
     const unsigned dmask = (1u << width) - 1u;
-    if (tid < 256) hist[tid] = 0u;
-    __syncthreads();
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const bool valid = val[j] && (key[j] & mask) == prefix;
@@ -1492,11 +1495,12 @@ __device__ unsigned long long group_threshold(const GroupSummary& S, int64_t k) 
       }
     }
     __syncthreads();
-    if (tid < 64) {  // one wave: 4 bins per lane, inclusive scan, locate krem
+    if (tid < 64) {  // one wave: 4 bins per lane (read, then zeroed for the next pass), inclusive scan, locate krem
       unsigned c[4], tot = 0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         c[q] = hist[lane * 4 + q];
+        hist[lane * 4 + q] = 0u;
         tot += c[q];
       }
       unsigned x = tot;
@@ -2115,7 +2119,8 @@ extern "C" size_t dal_dw_step_workspace_bytes(int64_t n, int64_t k, int64_t cap)
 // with DAL_STEP_RESET_STATUS.  Same bits as the two calls.
 namespace dal {
 
-int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner, const uint8_t* leaf,
+int dw_step_impl(const float* x, const float* xb, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
+                 const uint8_t* leaf,
                  int32_t n_trees, int32_t depth, const double* lut, const int64_t* density_fixed, double density_err,
                  const uint8_t* row_flags, double beta, int64_t idx_base, const double* norm64, const double* colsum,
                  int64_t k, int64_t cap, int32_t level1_passes, uint32_t step_flags, void* ws, size_t ws_bytes,
@@ -2147,7 +2152,7 @@ int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_
   char* base = static_cast<char*>(ws);
   TopkHdr* h1 = reinterpret_cast<TopkHdr*>(base + W.L1.hdr);
   if (level1_passes == 0) {  // exact level 1: the two calls as they are
-    rc = forest_score_launch(x, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, DAL_DENSITY_FIXED,
+    rc = forest_score_launch(x, xb, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, DAL_DENSITY_FIXED,
                              density_err, row_flags, beta, DAL_DESCENDING, votes, scores, keys_lo, keys_hi, hooks,
                              st);
     if (rc) return rc;
@@ -2165,7 +2170,7 @@ int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_
   // (tau then lies within a few ranks of K); smaller pools take one
   // group_min_kernel pass over finer groups after the score kernel
   uint64_t* gmin = reinterpret_cast<uint64_t*>(base + W.gmin);
-  const int rows_per_block = forest_rows_per_block(x, d, ldx, n_trees);
+  const int rows_per_block = forest_rows_per_block(x, xb, d, ldx, n_trees, depth);
   GroupSummary S = make_groups(gmin, n, rows_per_block);
   const bool in_score = S.ng >= 2 * k;
   if (in_score) {
@@ -2180,7 +2185,7 @@ int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_
     if (folded) zero_words(reinterpret_cast<uint32_t*>(gmin), 2 * S.ng * 2, st);
   }
   if (!select_only) {
-    rc = forest_score_launch(x, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, DAL_DENSITY_FIXED,
+    rc = forest_score_launch(x, xb, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, DAL_DENSITY_FIXED,
                              density_err, row_flags, beta, DAL_DESCENDING, votes, scores, keys_lo, keys_hi, hooks,
                              st);
     if (rc) return rc;
@@ -2218,7 +2223,7 @@ int dw_step_impl(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_
 
 }  // namespace dal
 
-extern "C" int dal_dw_step(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
+extern "C" int dal_dw_step(const float* x, const float* xb, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
                            const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
                            const int64_t* density_fixed, double density_err, const uint8_t* row_flags, double beta,
                            int64_t idx_base, const double* norm64, const double* colsum, int64_t k, int64_t cap,
@@ -2226,7 +2231,7 @@ extern "C" int dal_dw_step(const float* x, int64_t n, int64_t d, int64_t ldx, co
                            double* scores, uint64_t* keys_lo, uint64_t* keys_hi, int64_t* out_idx,
                            double* out_scores, uint64_t* out_keys, int32_t* dev_status, dal_event_t colsum_ready,
                            dal_stream_t stream) {
-  return dw_step_impl(x, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, density_err, row_flags, beta,
+  return dw_step_impl(x, xb, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, density_err, row_flags, beta,
                       idx_base, norm64, colsum, k, cap, level1_passes, step_flags, ws, ws_bytes, votes, scores,
                       keys_lo, keys_hi, out_idx, out_scores, out_keys, dev_status, colsum_ready, stream, nullptr,
                       nullptr, nullptr);

@@ -75,6 +75,12 @@ SIGNATURES = {
     "dal_forest_score": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32,
                                  c_int32, c_void_p, c_void_p, c_int, c_double, c_void_p, c_double,
                                  c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "dal_forest_blocked_rows": (c_int, [c_int64, c_int32, c_int32]),
+    "dal_pool_blocked_floats": (c_int64, [c_int64, c_int64]),
+    "dal_pool_blocked": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p]),
+    "dal_forest_score_blocked": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32,
+                                         c_int32, c_void_p, c_void_p, c_int, c_double, c_void_p, c_double,
+                                         c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "dal_density_separable": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_void_p]),
     "dal_topk_workspace_bytes": (c_size_t, [c_int64, c_int64]),
@@ -86,11 +92,11 @@ SIGNATURES = {
                               c_int64, c_int32, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_void_p]),
     "dal_dw_step_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
-    "dal_dw_step": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32, c_int32, c_void_p,
+    "dal_dw_step": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32, c_int32, c_void_p,
                             c_void_p, c_double, c_void_p, c_double, c_int64, c_void_p, c_void_p, c_int64, c_int64,
                             c_int32, ctypes.c_uint32, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "dal_dw_plan_create": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32, c_int32,
+    "dal_dw_plan_create": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32, c_int32,
                                    c_void_p, c_void_p, c_double, c_void_p, c_void_p, c_double, c_int64, c_void_p,
                                    c_void_p, c_int64, c_int64, c_int32, c_void_p, c_size_t, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

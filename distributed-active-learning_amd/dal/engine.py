@@ -157,6 +157,7 @@ class PoolState:
         self._colsum = None
         self._density_exact = None
         self._acc_pre = None  # density accumulator already zeroed by the prep kernel
+        self._xb = None  # blocked feature-major copy of x (dal_pool_blocked), built by the first warm step
         self._ws_clean = {}   # (n, k, cap) -> workspace whose top-k header is zero (dal_dw_step)
         self.gram_events = None  # list -> (start, end) HIP events around each Gram call
         self.residual_events = []  # (start, end) HIP events around each residual call (with gram_events)
@@ -182,10 +183,30 @@ class PoolState:
         self.last_status = 0     # status word read by the last synchronising select
 
     def clear_caches(self):
-        """Drop normalised rows, density and column sums (forces a cold step)."""
+        """Drop normalised rows, density, column sums and the blocked copy
+        (forces a cold step)."""
         self._u = self._norm64 = self._density = self._colsum = self._colsum_partials = None
-        self._split = self._density_exact = None
+        self._split = self._density_exact = self._xb = None
         self._graphs = {}
+
+    def blocked_pool(self, forest, build: bool = True):
+        """The pool's blocked feature-major copy (dal_pool_blocked) when the
+        forest is one the blocked score kernel applies to (it then reads only
+        the features the forest tests), else None.  Built on first use
+        (``build``) on the current stream and kept with the pool's caches:
+        the warm steps build it, the cold step keeps the row-major kernel."""
+        if self.n == 0:
+            return None
+        lib = _lib.load()
+        if not lib.dal_forest_blocked_rows(self.d, forest.n_trees, forest.depth):
+            return None
+        if self._xb is None and build:
+            torch = _torch()
+            xb = torch.empty(int(lib.dal_pool_blocked_floats(self.n, self.d)), dtype=torch.float32,
+                             device=self.device)
+            call("dal_pool_blocked", _ptr(self.x), self.n, self.d, self.d, _ptr(xb), _stream(self.device))
+            self._xb = xb
+        return self._xb
 
     # ------------------------------------------------------------- caches
     def set_excluded(self, excluded):
@@ -522,8 +543,9 @@ def device_lut(strategy: str, n_trees: int, device):
 
 def forest_score(state: PoolState, forest: Forest, lut_dev, flags, order: int, density=None,
                  density_err: float = 0.0, beta: float = 1.0, want_hi: bool = False,
-                 density_kind=None):
-    """Launch dal_forest_score over the shard; returns (votes, scores, keys, keys_hi)."""
+                 density_kind=None, xb=None):
+    """Launch dal_forest_score (dal_forest_score_blocked over ``xb``, the
+    pool's blocked copy) over the shard; returns (votes, scores, keys, keys_hi)."""
     torch = _torch()
     inner, leaf = forest.device(state.device)
     n = state.n
@@ -543,11 +565,14 @@ def forest_score(state: PoolState, forest: Forest, lut_dev, flags, order: int, d
         if state.event_lead_cycles:
             torch.cuda._sleep(state.event_lead_cycles)
         ev[0].record()
+    args = (n, state.d, state.d, _ptr(inner), _ptr(leaf), forest.n_trees, forest.depth, _ptr(lut_dev),
+            0 if density is None else _ptr(density), kind, float(density_err), _ptr(flags), float(beta), int(order),
+            _ptr(votes), _ptr(scores), _ptr(keys), 0 if keys_hi is None else _ptr(keys_hi), _stream(state.device))
     for _ in range(state.event_repeat if ev is not None else 1):
-        call("dal_forest_score", _ptr(state.x), n, state.d, state.d, _ptr(inner), _ptr(leaf),
-             forest.n_trees, forest.depth, _ptr(lut_dev), 0 if density is None else _ptr(density), kind,
-             float(density_err), _ptr(flags), float(beta), int(order), _ptr(votes), _ptr(scores),
-             _ptr(keys), 0 if keys_hi is None else _ptr(keys_hi), _stream(state.device))
+        if xb is None:
+            call("dal_forest_score", _ptr(state.x), *args)
+        else:
+            call("dal_forest_score_blocked", _ptr(state.x), _ptr(xb), *args)
     if ev is not None:
         ev[1].record()
         state.forest_events.append(ev)
@@ -660,10 +685,11 @@ def dw_select_local(state: PoolState, flags, votes, keys_lo, keys_hi, lut_dev, k
 
 
 def dw_step_local(state: PoolState, forest: Forest, flags, dens, lut_dev, k: int, beta: float, colsum,
-                  colsum_ready=None, cap_scale: int = None, sync: bool = True):
+                  colsum_ready=None, cap_scale: int = None, sync: bool = True, xb=None):
     """dal_dw_step on this pool or shard: votes, scores and interval keys
     of every row, then the exact canonical top-k -- one C call with fused
-    launches (the fast level 1).  Same retries as dw_select_local.
+    launches (the fast level 1; ``xb``: the pool's blocked copy for the score
+    kernel).  Same retries as dw_select_local.
     Returns (votes, scores, indices, selected scores); sync=False (the
     multi-GPU path: the caller reads the status word after the merge and
     re-runs with a larger ``cap_scale``) also returns the selected keys."""
@@ -695,8 +721,9 @@ def dw_step_local(state: PoolState, forest: Forest, flags, dens, lut_dev, k: int
         out_scores = torch.empty(k, dtype=torch.float64, device=dev)
         out_keys = None if sync else torch.empty(k, dtype=torch.int64, device=dev)
         try:
-            call("dal_dw_step", _ptr(state.x), n, state.d, state.d, _ptr(inner), _ptr(leaf), forest.n_trees,
-                 forest.depth, _ptr(lut_dev), _ptr(dens), derr, _ptr(flags), float(beta), state.row_base,
+            call("dal_dw_step", _ptr(state.x), 0 if xb is None else _ptr(xb), n, state.d, state.d, _ptr(inner),
+                 _ptr(leaf), forest.n_trees, forest.depth, _ptr(lut_dev), _ptr(dens), derr, _ptr(flags),
+                 float(beta), state.row_base,
                  _ptr(norm64), _ptr(colsum), k, cap, passes, DAL_STEP_WS_CLEAN, wsp, wsb, _ptr(votes),
                  _ptr(scores), _ptr(keys_lo), _ptr(keys_hi), _ptr(out_idx), _ptr(out_scores),
                  0 if out_keys is None else _ptr(out_keys), _ptr(state.status),
@@ -773,6 +800,9 @@ def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: 
         return _density_step_graph(state, unl, forest, min(int(k), int(unl.shape[0])), beta)
     # the density GEMM goes to the GPU first; the host prepares the rest while it runs
     colsum_ready = None
+    # warm (density cached): the score kernel reads the pool's blocked copy
+    # (built by the first warm step); the cold step keeps the row-major kernel
+    xb = state.blocked_pool(forest) if state._density is not None or density_fixed is not None else None
     if density_fixed is None and state._density is None and state._colsum is None and state.n:
         # cold step: the canonical column sum (only the exact re-rank needs it)
         # runs on a side stream AFTER the Gram, beside the vote / score chain
@@ -803,22 +833,22 @@ def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: 
             and state.n == state.n_total):
         # one C call, fused launches (the per-kernel timing path below keeps K2 / K3 apart)
         votes, scores, idx, sel_scores = dw_step_local(state, forest, flags, dens, lut_dev, kk, beta,
-                                                       state.colsum(), colsum_ready)
+                                                       state.colsum(), colsum_ready, xb=xb)
         state.check_status(state.last_status)
         return Selection(scores=(scores, loc), indices=idx, selected_scores=sel_scores, votes=(votes, loc))
     votes, scores, keys_lo, keys_hi = forest_score(
         state, forest, lut_dev, flags, DAL_DESCENDING, density=dens,
-        density_err=density_error(state), beta=beta, want_hi=True)
+        density_err=density_error(state), beta=beta, want_hi=True, xb=xb)
     # the main stream joins the column sum inside the call, just before the re-rank
     idx, sel_scores, _ = dw_select_local(state, flags, votes, keys_lo, keys_hi, lut_dev, kk, beta,
                                          state.colsum(), colsum_ready=colsum_ready)
     state.check_status(state.last_status)  # the word dw_select_local read (no second sync)
     if state.select_events is not None and state.step_select_events is not None and state.level1_fast:
-        _time_step_select(state, forest, flags, dens, lut_dev, kk, beta)
+        _time_step_select(state, forest, flags, dens, lut_dev, kk, beta, xb)
     return Selection(scores=(scores, loc), indices=idx, selected_scores=sel_scores, votes=(votes, loc))
 
 
-def _time_step_select(state: PoolState, forest: Forest, flags, dens, lut_dev, k: int, beta: float):
+def _time_step_select(state: PoolState, forest: Forest, flags, dens, lut_dev, k: int, beta: float, xb=None):
     """bench: the selection launch of the fused step (what dal_dw_step and the
     warm plan run after the score kernel folded the row-group minima) timed on
     its own: one full dal_dw_step that keeps the minima, then event_repeat
@@ -843,8 +873,9 @@ def _time_step_select(state: PoolState, forest: Forest, flags, dens, lut_dev, k:
     status = torch.zeros(1, dtype=torch.int32, device=dev)
 
     def step(flags_bits, out):
-        call("dal_dw_step", _ptr(state.x), n, state.d, state.d, _ptr(inner), _ptr(leaf), forest.n_trees,
-             forest.depth, _ptr(lut_dev), _ptr(dens), float(density_error(state)), _ptr(flags), float(beta),
+        call("dal_dw_step", _ptr(state.x), 0 if xb is None else _ptr(xb), n, state.d, state.d, _ptr(inner),
+             _ptr(leaf), forest.n_trees, forest.depth, _ptr(lut_dev), _ptr(dens), float(density_error(state)),
+             _ptr(flags), float(beta),
              state.row_base, _ptr(norm64), _ptr(colsum), k, cap, passes, flags_bits, wsp, wsb,
              *[_ptr(b) for b in bufs], _ptr(out[0]), _ptr(out[1]), 0, _ptr(status), 0, _stream(dev))
 
@@ -913,11 +944,13 @@ class WarmStepGraph:
         lib = _lib.load()
         self.wsb = int(lib.dal_dw_step_workspace_bytes(n, k, cap))
         self.ws, self.wsp = workspace(self.wsb, dev)
+        xb = state.blocked_pool(forest)  # the score kernel reads the pool's blocked copy when it applies
         self._keep = (state.density_fixed(), state.colsum() if colsum is None else colsum, state.norms(),
-                      state.flags, state.x)
+                      state.flags, state.x, xb)
         dens, colsum, norm64 = self._keep[:3]
         plan = ctypes.c_void_p()
-        call("dal_dw_plan_create", _ptr(state.x), n, state.d, state.d, _ptr(self.inner), _ptr(self.leaf),
+        call("dal_dw_plan_create", _ptr(state.x), 0 if xb is None else _ptr(xb), n, state.d, state.d,
+             _ptr(self.inner), _ptr(self.leaf),
              self.n_trees, self.depth, _ptr(self.lut), _ptr(dens), float(density_error(state)), _ptr(state.flags),
              _ptr(self.flags), float(beta), state.row_base, _ptr(norm64), _ptr(colsum), k, cap, passes, self.wsp,
              self.wsb, _ptr(self.votes), _ptr(self.scores), _ptr(self.keys_lo), _ptr(self.keys_hi),

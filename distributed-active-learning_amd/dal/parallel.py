@@ -333,15 +333,18 @@ class ShardedSelector:
             i, kk_keys = topk_keys(kys, kk, st.row_base)
             s = sc[i - st.row_base]
         elif mode == "dw":
+            # warm (density cached): the score kernel reads the shard's blocked copy, as on one GPU
+            xb = st.blocked_pool(forest) if self._density is not None else None
             dens = self.local_density(u_full)
             colsum = self.global_colsum(partials_full)
             lut_dev = device_lut("entropy", forest.n_trees, st.device)
             if st.events_off():  # one fused call (dal_dw_step), as the single-GPU step
                 _, _, i, s, kk_keys = dw_step_local(st, forest, flags, dens, lut_dev, kk, beta, colsum,
-                                                    cap_scale=self.cap_scale, sync=False)
+                                                    cap_scale=self.cap_scale, sync=False, xb=xb)
             else:  # bench per-kernel timing: K2 and K3 as separate calls
                 votes, sc, klo, khi = forest_score(st, forest, lut_dev, flags, DAL_DESCENDING, density=dens,
-                                                   density_err=density_error(st), beta=beta, want_hi=True)
+                                                   density_err=density_error(st), beta=beta, want_hi=True,
+                                                   xb=xb)
                 i, s, kk_keys = dw_select_local(st, flags, votes, klo, khi, lut_dev, kk, beta, colsum,
                                                 cap_scale=self.cap_scale, sync=False)
         else:

@@ -238,6 +238,26 @@ int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ldx,
                      int32_t* votes, double* scores, uint64_t* keys, uint64_t* keys_hi,
                      dal_stream_t stream);
 
+/* ---- (a5-a10) the same over the pool's blocked feature-major copy (ABI v9)
+ * dal_pool_blocked writes the pool as tiles of 64 rows, feature-major inside
+ * a tile: xb[(t * d + f) * 64 + r] = x[t * 64 + r][f], rows past n zero
+ * (dal_pool_blocked_floats(n, d) floats; a per-pool copy, built once -- the
+ * pool is constant across AL iterations).  dal_forest_score_blocked gives
+ * dal_forest_score's outputs bit for bit; when dal_forest_blocked_rows(d,
+ * n_trees, depth) is non-zero (a forest whose node count bounds its distinct
+ * features at <= 3/4 d and <= 150) it reads only the features the forest
+ * tests -- each tile's listed features as 256-B runs -- instead of whole rows
+ * (config 4, T = 10: ~116 of 256 features), else it runs dal_forest_score's
+ * row-major kernel on x.  xb must be 16-B aligned. */
+int dal_forest_blocked_rows(int64_t d, int32_t n_trees, int32_t depth);
+int64_t dal_pool_blocked_floats(int64_t n, int64_t d);
+int dal_pool_blocked(const float* x, int64_t n, int64_t d, int64_t ldx, float* xb, dal_stream_t stream);
+int dal_forest_score_blocked(const float* x, const float* xb, int64_t n, int64_t d, int64_t ldx,
+                             const int32_t* inner, const uint8_t* leaf, int32_t n_trees, int32_t depth,
+                             const double* lut, const void* density, int density_kind, double density_err,
+                             const uint8_t* row_flags, double beta, int order, int32_t* votes, double* scores,
+                             uint64_t* keys, uint64_t* keys_hi, dal_stream_t stream);
+
 /* ---- (a11) top-k: sortBy(score).take(k) --------------------------------
  * Replaces uncertainty_sampling.py:106,109 / density_weighting.py:168,172.
  * The k smallest keys, ties -> lower index; out_idx = idx_base + row, sorted
@@ -308,13 +328,16 @@ int dal_dw_select(const uint64_t* keys_lo, const uint64_t* keys_hi, const int32_
  *                          same buffers and workspace (the same arguments),
  *                          and gives the same outputs.  Used to time the
  *                          selection launch of the fused step on its own.
+ * xb (ABI v9; nullable): the pool's blocked copy (dal_pool_blocked) -- the
+ * score kernel is then dal_forest_score_blocked's.
  * Workspace: dal_dw_step_workspace_bytes (== dal_dw_select's). */
 #define DAL_STEP_RESET_STATUS 1u
 #define DAL_STEP_WS_CLEAN 2u
 #define DAL_STEP_KEEP_GROUPS 4u
 #define DAL_STEP_SELECT_ONLY 8u
 size_t dal_dw_step_workspace_bytes(int64_t n, int64_t k, int64_t cap);
-int dal_dw_step(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner, const uint8_t* leaf,
+int dal_dw_step(const float* x, const float* xb, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
+                const uint8_t* leaf,
                 int32_t n_trees, int32_t depth, const double* lut, const int64_t* density_fixed,
                 double density_err, const uint8_t* row_flags, double beta, int64_t idx_base,
                 const double* norm64, const double* colsum, int64_t k, int64_t cap, int32_t level1_passes,
@@ -339,9 +362,10 @@ int dal_dw_step(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t
  * wait for that word (a bounded spin, then a stream sync) and return the
  * status in *status -- the
  * density_weighting.py:133-176 iteration in one call.  Buffers must outlive
- * the plan; dal_dw_plan_destroy frees it. */
+ * the plan; dal_dw_plan_destroy frees it.  xb (ABI v9; nullable): as
+ * dal_dw_step's. */
 typedef struct dal_dw_plan dal_dw_plan_t;
-int dal_dw_plan_create(const float* x, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
+int dal_dw_plan_create(const float* x, const float* xb, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
                        const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
                        const int64_t* density_fixed, double density_err, const uint8_t* base_flags,
                        uint8_t* flags, double beta, int64_t idx_base, const double* norm64,

@@ -25,6 +25,8 @@ from dal.forest import Forest  # noqa: E402
 def bind(path):
     lib = ctypes.CDLL(path)
     for name, (res, args) in _lib.SIGNATURES.items():
+        if not hasattr(lib, name):  # an older library: entry points added since
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -36,7 +36,7 @@ def test_library_exports_every_header_symbol():
 
 def test_host_helpers():
     lib = _lib.load()
-    assert lib.dal_abi_version() == 8
+    assert lib.dal_abi_version() == 9
     assert lib.dal_pad_rows(1) == 512 and lib.dal_pad_rows(100000) == 100352
     assert [lib.dal_pad_features(d) for d in (1, 30, 33, 64, 65, 128, 129, 256, 500, 784)] == \
         [32, 32, 64, 64, 128, 128, 256, 256, 512, 1024]
@@ -89,6 +89,32 @@ def test_host_argument_validation_without_gpu():
     assert lib.dal_topk(p, 100000, 9000, 0, p, 1 << 30, p, p, None) == -5
     assert lib.dal_forest_score(p, 10, 4, 4, p, p, 3, 17, p, None, 0, 0.0, None, 1.0, 0, p, p, p,
                                 None, None) == -3
+
+
+def test_blocked_pool_rule_without_gpu():
+    """ABI v9: the blocked K2 path applies when the forest's node count
+    bounds its distinct features at <= 3/4 d and <= 150 (config 4, T = 10:
+    150 of 256); the copy's size is whole 64-row tiles; bad arguments are
+    rejected before any HIP call."""
+    lib = _lib.load()
+    assert lib.dal_forest_blocked_rows(256, 10, 4) == 64     # config 4
+    assert lib.dal_forest_blocked_rows(256, 100, 4) == 0     # config 4 at T = 100
+    assert lib.dal_forest_blocked_rows(256, 11, 4) == 0      # 165 > 150 runs
+    assert lib.dal_forest_blocked_rows(64, 10, 4) == 0       # config 2: 64 features, every one may be tested
+    assert lib.dal_forest_blocked_rows(30, 100, 4) == 0      # config 3
+    assert lib.dal_forest_blocked_rows(96, 4, 4) == 64       # 60 <= 72
+    assert lib.dal_forest_blocked_rows(80, 4, 4) == 64       # 60 <= 60
+    assert lib.dal_forest_blocked_rows(79, 4, 4) == 0        # 60 > 59.25
+    assert lib.dal_forest_blocked_rows(0, 10, 4) == 0 and lib.dal_forest_blocked_rows(256, 10, 17) == 0
+    assert lib.dal_pool_blocked_floats(1, 256) == 64 * 256 and lib.dal_pool_blocked_floats(128, 3) == 128 * 3
+    assert lib.dal_pool_blocked_floats(0, 8) == 0 and lib.dal_pool_blocked_floats(10, 0) == -1
+    p = ctypes.c_void_p(256)
+    assert lib.dal_pool_blocked(None, 10, 4, 4, p, None) == -1
+    assert lib.dal_pool_blocked(p, 10, 4, 3, p, None) == -2
+    assert lib.dal_pool_blocked(p, 0, 4, 4, p, None) == 0  # nothing to copy: no launch
+    odd = ctypes.c_void_p(264)  # xb must be 16-B aligned
+    assert lib.dal_forest_score_blocked(p, odd, 10, 256, 256, p, p, 10, 4, p, None, 0, 0.0, None, 1.0, 0,
+                                        p, p, p, None, None) == -1
 
 
 def test_merge_and_mark_count_validation_without_gpu():
