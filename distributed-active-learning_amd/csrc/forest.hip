@@ -190,9 +190,9 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
       v += leaf[t * n_leaf + (h - n_inner)];
     }
   }
-  if (wr) {  // a row's tree phases are in different waves
-    __shared__ int s_vote[kForestThreads];
-    s_vote[sub * R + r] = v;
+  if (wr) {  // a row's tree phases are in different waves (partial votes < 256: T <= 150 here)
+    __shared__ uint8_t s_vote[kForestThreads];
+    s_vote[sub * R + r] = static_cast<uint8_t>(v);
     __syncthreads();
     if (sub == 0)
       for (int q = 1; q < tpr; ++q) v += s_vote[q * R + r];
@@ -448,8 +448,8 @@ __global__ __launch_bounds__(kForestThreads) void forest_blocked_kernel(ForestAr
   float* xs = reinterpret_cast<float*>(smem);
   int2* fs = reinterpret_cast<int2*>(smem + static_cast<size_t>(fu_max) * kBlk * 4);
   uint8_t* ls = reinterpret_cast<uint8_t*>(fs + nn);
-  int* used = reinterpret_cast<int*>(ls + round_up(static_cast<int64_t>(A.n_trees) * n_leaf, 4));
-  unsigned* bits = reinterpret_cast<unsigned*>(used + fu_max);
+  uint16_t* used = reinterpret_cast<uint16_t*>(ls + round_up(static_cast<int64_t>(A.n_trees) * n_leaf, 4));
+  unsigned* bits = reinterpret_cast<unsigned*>(used + round_up(fu_max, 2));
   int* pre = reinterpret_cast<int*>(bits + nw);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(kForestThreads) void forest_blocked_kernel(ForestAr
   __syncthreads();
   auto slot = [&](int f) { return pre[f >> 5] + __popc(bits[f >> 5] & ((1u << (f & 31)) - 1u)); };
   for (int f = tid; f < A.d; f += kForestThreads)
-    if ((bits[f >> 5] >> (f & 31)) & 1u) used[slot(f)] = f;
+    if ((bits[f >> 5] >> (f & 31)) & 1u) used[slot(f)] = static_cast<uint16_t>(f);  // d <= 2^16 here
   for (int e = tid; e < nn; e += kForestThreads) fs[e].x = slot(fs[e].x) * kBlk;
   const int fu = pre[nw - 1] + __popc(bits[nw - 1]);  // <= fu_max
   __syncthreads();
@@ -524,11 +524,12 @@ namespace {
 // the path does not apply: depth-limited complete-heap trees whose node count
 // bounds the distinct features at most 3/4 of d (fewer bytes than the
 // row-major tile by at least a quarter) and at most 150 runs of 256 B (four
-// blocks per CU).
+// blocks per CU: 150 x 256 B + the forest, the feature list and the votes fit
+// a quarter of the 160 KiB LDS).
 int blocked_fu_max(int64_t d, int32_t n_trees, int32_t depth) {
   const int64_t nodes = static_cast<int64_t>(n_trees) * ((int64_t{1} << depth) - 1);
   const int64_t fu = nodes < d ? nodes : d;
-  return fu * 4 <= 3 * d && fu <= 150 ? static_cast<int>(fu) : 0;
+  return fu * 4 <= 3 * d && fu <= 150 && d <= 65536 ? static_cast<int>(fu) : 0;  // (16-bit feature list)
 }
 
 struct ForestTiling {
@@ -599,7 +600,7 @@ int forest_score_launch(const float* x, const float* xb, int64_t n, int64_t d, i
     const int64_t nw = (d + 31) / 32;
     const size_t smem = static_cast<size_t>(fu_max) * kBlk * 4 + static_cast<size_t>(nn) * 8 +
                         static_cast<size_t>(round_up(static_cast<int64_t>(n_trees) << depth, 4)) +
-                        static_cast<size_t>(fu_max) * 4 + static_cast<size_t>(nw) * 8;
+                        static_cast<size_t>(round_up(fu_max, 2)) * 2 + static_cast<size_t>(nw) * 8;
     const void* fn = reinterpret_cast<const void*>(forest_blocked_kernel);
     int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
