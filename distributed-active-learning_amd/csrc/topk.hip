@@ -871,11 +871,23 @@ __device__ bool select_compact(const uint64_t* __restrict__ keys, const int64_t*
   __shared__ unsigned int s_krem, s_neq, s_count;
   const int tid = threadIdx.x, lane = tid & 63;
   constexpr int kPer = DAL_SORT_CAP_PAYLOAD / kSortThreads;  // 4
+  // the indices and payloads are loaded with the keys (the compaction below
+  // then needs no second coherent round trip)
   unsigned long long key[kPer];
+  long long iv[kPer];
+  double pv[kPer];
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     const int64_t e = tid + static_cast<int64_t>(j) * kSortThreads;
-    key[j] = e < m ? ld_sc1(keys + M(e)) : 0ull;
+    key[j] = 0ull;
+    iv[j] = 0;
+    pv[j] = 0.0;
+    if (e < m) {
+      const int64_t q = M(e);
+      key[j] = ld_sc1(keys + q);
+      iv[j] = ld_sc1(idx + q);
+      pv[j] = ld_sc1(pay + q);
+    }
   }
   // the digits start below the keys' common high bits (for density-weighted
   // keys the sign and most of the exponent: the first 8-bit pass over them
@@ -978,8 +990,8 @@ __device__ bool select_compact(const uint64_t* __restrict__ keys, const int64_t*
     if (take) {
       const unsigned p = base + static_cast<unsigned>(__popcll(tm & ((1ull << lane) - 1ull)));
       sk[p] = key[j];
-      si[p] = ld_sc1(idx + M(e));
-      sp[p] = ld_sc1(pay + M(e));
+      si[p] = iv[j];
+      sp[p] = pv[j];
     }
   }
   __syncthreads();
