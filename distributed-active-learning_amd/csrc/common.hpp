@@ -94,7 +94,9 @@ __device__ __forceinline__ double row_sq_norm_bf16(const uint16_t* __restrict__ 
 //   status_reset (nullable) is zeroed by the first thread, before any later
 //                kernel of the step can raise a flag (a replayed step starts clean);
 //   base_flags   (nullable; the warm-step plan) the row flags are built here:
-//                base_flags[r] | (stamp[r] == *step_id ? DAL_ROW_CANDIDATE : 0),
+//                base_flags[r] | (stamp[r] == (uint8_t)*step_id ? DAL_ROW_CANDIDATE : 0)
+//                (8-bit stamps: the plan cycles its step ids through 1..255 and
+//                clears the stamps when they wrap),
 //                written to row_flags for the step's later kernels -- the
 //                unlabeled rows were stamped by the plan's mark kernel, so no
 //                per-step copy of the base flags;
@@ -107,7 +109,7 @@ __device__ __forceinline__ double row_sq_norm_bf16(const uint16_t* __restrict__ 
 struct ForestStepHooks {
   int32_t* status_reset = nullptr;
   const uint8_t* base_flags = nullptr;
-  const uint32_t* stamp = nullptr;
+  const uint8_t* stamp = nullptr;
   const uint32_t* step_id = nullptr;
   uint64_t* gmin = nullptr;
   int group_blocks = 1;

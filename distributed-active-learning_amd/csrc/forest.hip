@@ -84,7 +84,7 @@ __device__ __forceinline__ double density_pow_err(double d, double derr, double 
 // with DAL_ROW_CANDIDATE from this step's mark stamp.
 __device__ __forceinline__ uint8_t row_flag(const ForestArgs& A, int64_t row) {
   if (!A.hooks.base_flags) return A.flags[row];
-  const bool cand = A.hooks.stamp[row] == *A.hooks.step_id;
+  const bool cand = A.hooks.stamp[row] == static_cast<uint8_t>(*A.hooks.step_id);
   return static_cast<uint8_t>(A.hooks.base_flags[row] | (cand ? DAL_ROW_CANDIDATE : 0));
 }
 

@@ -38,18 +38,33 @@ constexpr int kMarkBlocks = 512;  // fixed at capture: the list length varies pe
 // step (no per-step copy of the flags).  The list's (address, length) and the
 // step id are kernel arguments, rewritten before each replay by
 // hipGraphExecKernelNodeSetParams: no host-memory reads in the graph.  Block 0
-// publishes the step id for the score kernel.
+// publishes the step id for the score kernel.  Stamps are 8-bit (a quarter of
+// the bytes to write, and to write back from L2 before the score kernel):
+// step ids cycle through 1..255 and dal_dw_plan_run clears the stamps when
+// they wrap.  Four list entries per thread are loaded before their stores.
+constexpr int kMarkPer = 4;
 __global__ __launch_bounds__(kPlanThreads) void plan_mark_direct_kernel(const int64_t* __restrict__ idx, int64_t count,
                                                                         uint32_t step, int64_t row_base, int64_t n,
-                                                                        uint32_t* __restrict__ stamp,
+                                                                        uint8_t* __restrict__ stamp,
                                                                         uint32_t* __restrict__ step_dev) {
   if (blockIdx.x == 0 && threadIdx.x == 0) *step_dev = step;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kPlanThreads;
-  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kPlanThreads + threadIdx.x; t < count; t += stride) {
-    const int64_t r = idx[t] - row_base;
-    if (r >= 0 && r < n) stamp[r] = step;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kPlanThreads * kMarkPer;
+  for (int64_t t0 = static_cast<int64_t>(blockIdx.x) * kPlanThreads * kMarkPer + threadIdx.x; t0 < count;
+       t0 += stride) {
+    int64_t r[kMarkPer];
+#pragma unroll
+    for (int j = 0; j < kMarkPer; ++j) {
+      const int64_t t = t0 + j * kPlanThreads;
+      r[j] = t < count ? idx[t] - row_base : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < kMarkPer; ++j)
+      if (r[j] >= 0 && r[j] < n) stamp[r[j]] = static_cast<uint8_t>(step);
   }
 }
+
+// The step id of the plan's n-th replay: 1..255, cycling (8-bit stamps).
+inline uint32_t stamp_step(uint32_t step) { return (step - 1u) % 255u + 1u; }
 
 }  // namespace
 
@@ -63,7 +78,8 @@ struct dal_dw_plan {
   int32_t* dev_status = nullptr;
   PlanSlot* slot = nullptr;       // host view
   PlanSlot* slot_dev = nullptr;   // the same words as the device addresses them
-  uint32_t* stamp = nullptr;      // device [n + 1]: per-row mark stamps, then the current step id
+  uint8_t* stamp = nullptr;       // device: n per-row 8-bit mark stamps, then (4-B aligned) the step id
+  uint32_t* step_dev = nullptr;   // the step id word after the stamps
   int device = 0;                 // the HIP device of the capture stream (every call runs there)
   hipGraphNode_t mark_node = nullptr;  // the mark kernel's node (its arguments change every replay)
   hipKernelNodeParams mark_params{};   // its launch shape, reused by every SetParams
@@ -127,19 +143,21 @@ extern "C" int dal_dw_plan_create(const float* x, const float* xb, int64_t n, in
     p->slot->status = 0;
   }
   // stamps start at 0 and steps at 1: no row is marked before its first step
-  if (!rc && (hipMalloc(reinterpret_cast<void**>(&p->stamp), (n + 1) * sizeof(uint32_t)) != hipSuccess ||
-              hipMemsetAsync(p->stamp, 0, (n + 1) * sizeof(uint32_t), st) != hipSuccess ||
+  const size_t stamp_bytes = static_cast<size_t>(round_up(n, 4)) + sizeof(uint32_t);
+  if (!rc && (hipMalloc(reinterpret_cast<void**>(&p->stamp), stamp_bytes) != hipSuccess ||
+              hipMemsetAsync(p->stamp, 0, stamp_bytes, st) != hipSuccess ||
               hipStreamSynchronize(st) != hipSuccess))
     rc = DAL_ERR_HIP;
+  if (!rc) p->step_dev = reinterpret_cast<uint32_t*>(p->stamp + round_up(n, 4));
   if (!rc && hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) rc = DAL_ERR_HIP;
   if (!rc && hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) != hipSuccess) rc = DAL_ERR_HIP;
   if (!rc) {
     hipLaunchKernelGGL(plan_mark_direct_kernel, dim3(kMarkBlocks), dim3(kPlanThreads), 0, cs,
-                       static_cast<const int64_t*>(nullptr), int64_t{0}, 0u, idx_base, n, p->stamp, p->stamp + n);
+                       static_cast<const int64_t*>(nullptr), int64_t{0}, 0u, idx_base, n, p->stamp, p->step_dev);
     ForestStepHooks hooks;
     hooks.base_flags = base_flags;
     hooks.stamp = p->stamp;
-    hooks.step_id = p->stamp + n;
+    hooks.step_id = p->step_dev;
     const int step_rc = dw_step_impl(x, xb, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, density_err,
                                      flags, beta, idx_base, norm64, colsum, k, cap, level1_passes,
                                      DAL_STEP_RESET_STATUS | DAL_STEP_WS_CLEAN, ws, ws_bytes, votes, scores, keys_lo,
@@ -191,12 +209,15 @@ extern "C" int dal_dw_plan_run(dal_dw_plan_t* p, const int64_t* unl, int64_t n_u
   const DeviceGuard guard(st);
   if (!guard.ok() || guard.device() != p->device) return DAL_ERR_ARG;  // a stream of another device
   volatile PlanSlot* slot = p->slot;
-  const uint32_t step = ++p->step;
+  const uint32_t step = stamp_step(++p->step);
+  // the 8-bit stamps wrapped: clear them (once per 255 replays) before this step marks its rows
+  if (step == 1u && p->step > 1u && hipMemsetAsync(p->stamp, 0, static_cast<size_t>(p->n), st) != hipSuccess)
+    return DAL_ERR_HIP;
   {
     hipKernelNodeParams np = p->mark_params;
     int64_t row_base = p->row_base, n = p->n;
-    uint32_t* stamp = p->stamp;
-    uint32_t* step_dev = p->stamp + p->n;
+    uint8_t* stamp = p->stamp;
+    uint32_t* step_dev = p->step_dev;
     void* kargs[7] = {&unl, &n_unl, const_cast<uint32_t*>(&step), &row_base, &n, &stamp, &step_dev};
     np.kernelParams = kargs;
     np.extra = nullptr;
@@ -227,11 +248,13 @@ extern "C" int dal_dw_plan_launch(dal_dw_plan_t* p, const int64_t* unl, int64_t 
   hipStream_t st = as_stream(stream);
   const DeviceGuard guard(st);
   if (!guard.ok() || guard.device() != p->device) return DAL_ERR_ARG;
-  const uint32_t step = ++p->step;
+  const uint32_t step = stamp_step(++p->step);
+  if (step == 1u && p->step > 1u && hipMemsetAsync(p->stamp, 0, static_cast<size_t>(p->n), st) != hipSuccess)
+    return DAL_ERR_HIP;  // (as dal_dw_plan_run)
   hipKernelNodeParams np = p->mark_params;
   int64_t row_base = p->row_base, n = p->n;
-  uint32_t* stamp = p->stamp;
-  uint32_t* step_dev = p->stamp + p->n;
+  uint8_t* stamp = p->stamp;
+  uint32_t* step_dev = p->step_dev;
   void* kargs[7] = {&unl, &n_unl, const_cast<uint32_t*>(&step), &row_base, &n, &stamp, &step_dev};
   np.kernelParams = kargs;
   np.extra = nullptr;

@@ -470,13 +470,13 @@ struct DwRerank {
   // a plan step (ForestStepHooks): flags = base_flags | (stamp == step ?
   // CANDIDATE : 0), derived here for the candidates instead of stored per row
   const uint8_t* base_flags = nullptr;
-  const uint32_t* stamp = nullptr;
+  const uint8_t* stamp = nullptr;
   const uint32_t* step_id = nullptr;
 };
 
 __device__ __forceinline__ uint8_t rerank_flag(const DwRerank& R, int64_t i) {
   if (R.base_flags)
-    return static_cast<uint8_t>(R.base_flags[i] | (R.stamp[i] == *R.step_id ? DAL_ROW_CANDIDATE : 0));
+    return static_cast<uint8_t>(R.base_flags[i] | (R.stamp[i] == static_cast<uint8_t>(*R.step_id) ? DAL_ROW_CANDIDATE : 0));
   return R.flags ? R.flags[i] : DAL_ROW_CANDIDATE;
 }
 
