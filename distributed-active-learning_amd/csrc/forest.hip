@@ -228,11 +228,14 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
     if (A.keys_hi) A.keys_hi[row] = khi;
   }
   if (!A.hooks.gmin) return;  // kernel-uniform
-  // the block's minimum keys -> its row group (the top-k's fast level 1)
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned long long a = __shfl_xor(klo, o), b = __shfl_xor(khi, o);
-    klo = a < klo ? a : klo;
-    khi = b < khi ? b : khi;
+  // the block's minimum keys -> its row group (the top-k's fast level 1);
+  // with rows on wave lanes (wr) only the row leaders' wave (sub 0) holds keys
+  if (!wr || sub == 0) {  // (wave-uniform)
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long a = __shfl_xor(klo, o), b = __shfl_xor(khi, o);
+      klo = a < klo ? a : klo;
+      khi = b < khi ? b : khi;
+    }
   }
   if (wmin && A.hooks.group_blocks > 1) {  // kernel-uniform
     if ((tid & 63) == 0) {
