@@ -348,7 +348,10 @@ def topk_roofline(n_rows, select_ms, config, world, level1_passes=0, step_select
             "fused_step_select_ms": step_select_ms,
             "fused_step_select_note": ("summary_select_kernel as dal_dw_step / the warm plan run it (row-group "
                                        "minima folded by the score kernel), timed alone: DAL_STEP_SELECT_ONLY "
-                                       "calls, 10 per event pair behind a GPU spin; latency-bound"),
+                                       "calls, 10 per event pair behind a GPU spin; latency-bound. The repeats "
+                                       "find the candidate rows cache-warm: in the warm plan's kernel trace, "
+                                       "right after the score kernel, the same launch took 23.7 us at config 4 "
+                                       "(profiles/r05/warm/timeline_config4_warm.txt)"),
             "algorithmic_bytes_per_launch": nbytes, "bytes_per_row": per_row,
             "note": "one C-ABI call (all its launches), HIP events on the launch stream, warm steps, each call queued behind a GPU spin and issued 10x back to back between the events (device time per call incl. its launch gaps; no host submission gaps, event cost amortised)"}
 
