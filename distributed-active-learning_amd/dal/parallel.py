@@ -307,7 +307,7 @@ class ShardedSelector:
                      strategy: str = "least_confidence", beta: float = 1.0,
                      density_mode: str = "gram") -> LocalTopk:
         from .engine import (density_error, device_lut, dw_select_local, dw_step_local, forest_score,
-                             topk_keys)
+                             topk_keys, uncertainty_blocked)
         from .luts import ASCENDING
 
         torch = __import__("torch")
@@ -350,7 +350,7 @@ class ShardedSelector:
         else:
             order = DAL_ASCENDING if ASCENDING[strategy] else DAL_DESCENDING
             lut_dev = device_lut(strategy, forest.n_trees, st.device)
-            votes, sc, kys, _ = forest_score(st, forest, lut_dev, flags, order)
+            votes, sc, kys, _ = forest_score(st, forest, lut_dev, flags, order, xb=uncertainty_blocked(st, forest))
             i, kk_keys = topk_keys(kys, kk, st.row_base)
             s = sc[i - st.row_base]
         if kk == k:  # every slot written by the selection

@@ -167,3 +167,27 @@ def test_dw_step_and_plan_with_blocked_copy(cuda):
         assert (st2._xb is not None) == (it > 0)
         assert np.array_equal(sel.indices.cpu().numpy(), ref_idx)
         assert np.array_equal(sel.selected_scores.cpu().numpy(), ref_ss)
+
+
+@pytest.mark.parametrize("strategy", ["least_confidence", "margin", "entropy"])
+def test_uncertainty_steps_with_blocked_copy(cuda, strategy):
+    """uncertainty_sampling.py:85-112 on one pool, three iterations: the first
+    scores with the row-major kernel, the later ones build and read the blocked
+    copy; every selection equals the oracle's for its shrinking unlabeled list."""
+    from dal import uncertainty_sampling as us
+    from dal.engine import PoolState
+    from dal.forest import Forest
+
+    n, d, k = 30_000, 256, 50
+    X = O.synthetic_pool(n, d, seed=17)
+    st = PoolState(X, device=cuda)
+    F = Forest.synthetic(10, 4, d, seed=9)
+    of = O.synthetic_forest(10, 4, d, seed=9)
+    unl = np.arange(n)
+    for it in range(3):
+        sel = us.select(st, unl, F, k, strategy=strategy)
+        _, ref_idx, ref_ss = O.uncertainty_select(X, unl, of, k, strategy)
+        assert np.array_equal(sel.indices.cpu().numpy(), ref_idx), it
+        assert np.array_equal(sel.selected_scores.cpu().numpy(), ref_ss), it
+        assert (st._xb is not None) == (it > 0)
+        unl = np.setdiff1d(unl, ref_idx)
