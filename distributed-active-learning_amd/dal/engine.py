@@ -548,6 +548,7 @@ def forest_score(state: PoolState, forest: Forest, lut_dev, flags, order: int, d
     """Launch dal_forest_score (dal_forest_score_blocked over ``xb``, the
     pool's blocked copy) over the shard; returns (votes, scores, keys, keys_hi)."""
     torch = _torch()
+    forest.check_features(state.d)
     inner, leaf = forest.device(state.device)
     n = state.n
     votes = torch.empty(n, dtype=torch.int32, device=state.device)
@@ -697,6 +698,7 @@ def dw_step_local(state: PoolState, forest: Forest, flags, dens, lut_dev, k: int
     torch = _torch()
     lib = _lib.load()
     n = state.n
+    forest.check_features(state.d)
     inner, leaf = forest.device(state.device)
     norm64 = state.norms()
     derr = float(density_error(state))
@@ -929,6 +931,7 @@ class WarmStepGraph:
         dev = state.device
         n = state.n
         self.state, self.k, self.cap, self.passes = state, int(k), int(cap), int(passes)
+        forest.check_features(state.d)
         inner, leaf = forest.device(dev)
         self.inner, self.leaf = inner.clone(), leaf.clone()
         self.forest_ref = forest
@@ -985,6 +988,7 @@ class WarmStepGraph:
             prev._detach()
         dev = self.state.device
         if forest is not self.forest_ref:
+            forest.check_features(self.state.d)
             inner, leaf = forest.device(dev)
             self.inner.copy_(inner)
             self.leaf.copy_(leaf)
@@ -1001,6 +1005,7 @@ class WarmStepGraph:
         """Refresh and replay on the current stream WITHOUT waiting (the
         outputs land in ``packed``); the caller reads the status later."""
         if forest is not self.forest_ref:
+            forest.check_features(self.state.d)
             inner, leaf = forest.device(self.state.device)
             self.inner.copy_(inner)
             self.leaf.copy_(leaf)

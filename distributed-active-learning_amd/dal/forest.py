@@ -55,6 +55,16 @@ class Forest:
     def n_trees(self) -> int:
         return int(self.inner.shape[0])
 
+    def check_features(self, d: int):
+        """Raise unless every inner node tests a feature in [0, d): the score
+        kernels index the pool row (or the blocked copy's feature list) with it."""
+        if "range" not in self._dev:
+            f = self.inner[..., 0]
+            self._dev["range"] = (int(f.min()), int(f.max())) if f.size else (0, 0)
+        lo, hi = self._dev["range"]
+        if lo < 0 or hi >= d:
+            raise ValueError(f"forest tests feature {lo if lo < 0 else hi}, outside the pool's {d} features")
+
     def device(self, device):
         """(inner, leaf) as device tensors, uploaded once per device."""
         import torch

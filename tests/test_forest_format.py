@@ -164,3 +164,22 @@ def test_from_mllib_saved_parquet(tmp_path):
     write_mllib_saved(of, str(tmp_path))
     F = Forest.from_mllib_saved(str(tmp_path))
     assert np.array_equal(heap_votes(F, g["X"]), O.votes(of, g["X"]))
+
+
+def test_check_features_rejects_out_of_range():
+    """Every score launch first checks that the forest's features index the
+    pool's row (the kernels gather x[f] / the blocked copy's run of f)."""
+    import numpy as np
+    import pytest
+
+    from dal.forest import Forest
+
+    F = Forest.synthetic(3, 4, 20, seed=1)
+    F.check_features(20)
+    with pytest.raises(ValueError, match="outside"):
+        F.check_features(int(F.inner[..., 0].max()))
+    bad = F.inner.copy()
+    bad[0, 0, 0] = -1
+    with pytest.raises(ValueError, match="-1"):
+        Forest(inner=bad, leaf=F.leaf.copy(), depth=F.depth).check_features(20)
+    assert np.array_equal(F.inner, Forest.synthetic(3, 4, 20, seed=1).inner)
