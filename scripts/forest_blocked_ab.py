@@ -17,7 +17,16 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import bench  # noqa: E402
-from dal import engine  # noqa: E402
+from dal import _lib, engine  # noqa: E402
+
+if os.environ.get("DAL_AB_LIB"):  # an A/B build in place of the product library
+    import ctypes
+
+    _ab = ctypes.CDLL(os.path.abspath(os.environ["DAL_AB_LIB"]))
+    for _name, (_res, _args) in _lib.SIGNATURES.items():
+        getattr(_ab, _name).restype = _res
+        getattr(_ab, _name).argtypes = _args
+    _lib._lib = _ab
 from dal._lib import DAL_DESCENDING, call, load  # noqa: E402
 from dal.engine import PoolState, _ptr, _stream  # noqa: E402
 from dal.forest import Forest  # noqa: E402
