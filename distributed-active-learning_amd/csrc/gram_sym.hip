@@ -125,10 +125,21 @@ __device__ __forceinline__ unsigned fresh_lane() {
 #define DAL_GRAM_KS64_OCC 4  // KS 64: 4-wave blocks per CU (3: 16 KiB stages, 100k x 64 -3.2 % vs 2; row sums only, 128 VGPRs: 4 blocks on 8 KiB stages 100k x 64 -0.7 %, 200k x 64 -0.5 % vs 3)
 #endif
 #ifndef DAL_GRAM_NCH128
-#define DAL_GRAM_NCH128 1  // row-sum chains per row tile at KS 128 (2: 240 VGPRs, no spill; KS <= 64 keep 1)
+// row-sum chains per row tile at KS 128 (240 VGPRs, no spill; KS <= 64 keep 1).
+// Two chains fold every 256 columns (once per pair) at the chain length one
+// chain has folding every 128: the same density bound, half the folds
+// (2M x 256 1190.7 -> 1173.4 ms, 1M x 128 -2.6 %, 200k x 256 -1.8 %; one
+// chain with the 256-column fold -- a bound twice as wide -- 1169.7 ms)
+#define DAL_GRAM_NCH128 2
 #endif
 #ifndef DAL_GRAM_FOLD64
 #define DAL_GRAM_FOLD64 256  // columns per row fold at KS <= 64
+#endif
+#ifndef DAL_GRAM_FOLD128
+#define DAL_GRAM_FOLD128 256  // columns per row fold at KS 128 (<= 256: a fold never spans two pairs)
+#endif
+#ifndef DAL_GRAM_CHAIN_MAX
+#define DAL_GRAM_CHAIN_MAX 2048  // the longest row chain dal_density_error_bound_sym_d charges
 #endif
 #ifndef DAL_GRAM_W8_KS64
 #define DAL_GRAM_W8_KS64 0  // KS 64 in the 8-wave two-super-block form (round robin schedule only)
@@ -149,7 +160,7 @@ struct Cfg {
   static constexpr int STAGE = OCC >= 4 ? 8192 : OCC == 3 ? 16384 : 32768;  // bytes per LDS stage
   static constexpr int SC = STAGE / ROWB;           // columns per stage: 64 / 128 / 256
   static constexpr int SPP = 256 / SC;              // stages per 512 x 256 pair: 4 / 2 / 1
-  static constexpr int FOLD = KS == 128 ? 128 : DAL_GRAM_FOLD64;  // columns per row fold
+  static constexpr int FOLD = KS == 128 ? DAL_GRAM_FOLD128 : DAL_GRAM_FOLD64;  // columns per row fold
   static constexpr int SPF = FOLD / SC;             // stages per fold group
   static constexpr int F4 = STAGE / 16;
   static constexpr int SWZ = (SLOTS < 16 ? SLOTS : 16) - 1;
@@ -167,7 +178,7 @@ struct Cfg {
   static constexpr int CHAIN = FOLD / 16 / NCH * 2 * KS;
   static_assert(SPF >= 1 && SPP % SPF == 0 && PIECES >= 1 && NKS >= 1, "bad slice");
   static_assert(W == 4 || (W == 8 && KS >= 64), "two super blocks per block: KS >= 64 only");
-  static_assert(CHAIN <= 2048, "row chain longer than the density bound's worst case");
+  static_assert(CHAIN <= DAL_GRAM_CHAIN_MAX, "row chain longer than the density bound's worst case");
 };
 // the 8-wave form folds like the 4-wave one (one bound per KS)
 static_assert(Cfg<128, 8>::CHAIN == Cfg<128, 4>::CHAIN, "block forms must share the chain length");
@@ -853,11 +864,11 @@ extern "C" double dal_density_error_bound_sym_d(int64_t n_cols, int64_t d_pad) {
   // conservative unit roundoff for the MFMA's internal fp32 adds, counted as
   // sequential adds), products exact (f16 x f16), c = 1 + 2^-8 >= sum_d |h_i
   // h_j| + |h_i l_j| over sum_d |u_i u_j| <= 1 (Cauchy-Schwarz on unit rows):
-  //   row side   (the MFMA row sums of the taken pairs) one chain per row
-  //              tile between folds: Cfg<KS>::CHAIN products (FOLD / 16 tiles
-  //              x 2 KS: 1,024 at KS 32, 2,048 at KS 64 and 128), then 4
-  //              cross-lane adds: gamma_(CHAIN + 5) * c (the +1 kept from the
-  //              two-chain form)
+  //   row side   (the MFMA row sums of the taken pairs) NCH chains per row
+  //              tile between folds: Cfg<KS>::CHAIN products each (FOLD / 16 /
+  //              NCH tiles x 2 KS: 1,024 at KS 32, 2,048 at KS 64 and 128), the
+  //              add combining the two chains (KS 128) and 4 cross-lane adds:
+  //              gamma_(CHAIN + 5) * c
   //   column side  none: every taken pair's column sums are the closed form
   //              <u~_i, C_B> of dal_gram_sym_residual (exact int64 sums, an
   //              fp64 dot), as is the row side's remainder <L_i, R_B>: below
