@@ -138,6 +138,9 @@ __device__ __forceinline__ unsigned fresh_lane() {
 #ifndef DAL_GRAM_FOLD128
 #define DAL_GRAM_FOLD128 256  // columns per row fold at KS 128 (<= 256: a fold never spans two pairs)
 #endif
+#ifndef DAL_GRAM_STAGE8
+#define DAL_GRAM_STAGE8 32768  // bytes per LDS stage of the 8-wave kernel (65536: 2M x 256 1149.6 -> 1378.3 ms)
+#endif
 #ifndef DAL_GRAM_CHAIN_MAX
 #define DAL_GRAM_CHAIN_MAX 2048  // the longest row chain dal_density_error_bound_sym_d charges
 #endif
@@ -157,7 +160,7 @@ struct Cfg {
   static constexpr int HI = KS / 8;                 // slots of the H part
   // three 4-wave blocks per CU at KS 64 (OCC3): 16 KiB stages so three fit the LDS
   static constexpr int OCC = W == 8 ? 1 : KS == 32 ? DAL_GRAM_KS32_OCC : KS == 64 ? DAL_GRAM_KS64_OCC : 2;
-  static constexpr int STAGE = OCC >= 4 ? 8192 : OCC == 3 ? 16384 : 32768;  // bytes per LDS stage
+  static constexpr int STAGE = W == 8 ? DAL_GRAM_STAGE8 : OCC >= 4 ? 8192 : OCC == 3 ? 16384 : 32768;  // bytes per LDS stage
   static constexpr int SC = STAGE / ROWB;           // columns per stage: 64 / 128 / 256
   static constexpr int SPP = 256 / SC;              // stages per 512 x 256 pair: 4 / 2 / 1
   static constexpr int FOLD = KS == 128 ? DAL_GRAM_FOLD128 : DAL_GRAM_FOLD64;  // columns per row fold
