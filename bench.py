@@ -306,10 +306,13 @@ def forest_roofline(n_rows, d, trees, forest_ms, config, world, used_features=No
                                else "forest_score_bytes_per_launch", world), "launch_ms": forest_ms,
            "algorithmic_bytes_per_launch": nbytes, "bytes_per_row": per_row,
            "note": "timed with HIP events on the launch stream over the warm steps (density cached), each call queued behind a GPU spin and issued 10x back to back between the events (device time per call incl. its launch gaps; no host submission gaps, event cost amortised)"}
-    if trees > 32:
+    if trees > 32 and used_features is None:
         out["counters"] = ("PMC per launch at config 3 (profiles/r02/forest_config3_pmc.csv): LDS array busy "
                            "SQ_LDS_IDX_ACTIVE, 42% of it bank-conflict cycles (lane-divergent feature gathers); "
                            "waves parked on s_waitcnt 51% / issue-stalled 22% / issuing 27% of their cycles")
+    elif trees > 32:
+        out["counters"] = ("the blocked kernel's gathers are conflict-free (rows on lanes, feature-major tile); "
+                           "at T > 32 its 4 x T dependent node-then-feature LDS visits per row bound it, not HBM")
     if used_features is not None:
         out["used_features"] = used_features
         out["row_major_bytes_per_row"] = d * 4 + tail

@@ -190,7 +190,7 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
       v += leaf[t * n_leaf + (h - n_inner)];
     }
   }
-  if (wr) {  // a row's tree phases are in different waves (partial votes < 256: T <= 150 here)
+  if (wr) {  // a row's tree phases are in different waves (partial votes < 256: T <= 1020 here)
     __shared__ uint8_t s_vote[kForestThreads];
     s_vote[sub * R + r] = static_cast<uint8_t>(v);
     __syncthreads();
@@ -524,15 +524,29 @@ namespace dal {
 
 namespace {
 // The blocked path's LDS bound on the forest's distinct features, or 0 when
-// the path does not apply: depth-limited complete-heap trees whose node count
-// bounds the distinct features at most 3/4 of d (fewer bytes than the
-// row-major tile by at least a quarter) and at most 150 runs of 256 B (four
-// blocks per CU: 150 x 256 B + the forest, the feature list and the votes fit
-// a quarter of the 160 KiB LDS).
+// the path does not apply.  The node count bounds the distinct features; a
+// tile holds that many 256-B runs (<= 256: config 4 at T = 10 stages <= 150,
+// four blocks per CU; at T = 100 all 256, two), plus the forest, the feature
+// list and the bitmap, within 96 KiB.  The blocked kernel beat the row-major
+// one in every shape measured, whole rows included (same process, bits
+// identical: 2M x 256 x 100 501 -> 468 us, 1M x 128 x 100 193 -> 155 us,
+// 100k x 64 x 10 12.7 -> 9.6 us, config 3 43.4 -> 41.9 us): conflict-free
+// gathers, LDS-DMA staging and a persistent grid for every width.
+#ifndef DAL_FOREST_BLOCKED_MAX_RUNS
+#define DAL_FOREST_BLOCKED_MAX_RUNS 256
+#endif
+size_t blocked_smem(int fu_max, int64_t d, int32_t n_trees, int32_t depth) {
+  const int64_t nn = static_cast<int64_t>(n_trees) * ((int64_t{1} << depth) - 1);
+  return static_cast<size_t>(fu_max) * kBlk * 4 + static_cast<size_t>(nn) * 8 +
+         static_cast<size_t>(round_up(static_cast<int64_t>(n_trees) << depth, 4)) +
+         static_cast<size_t>(round_up(fu_max, 2)) * 2 + static_cast<size_t>((d + 31) / 32) * 8;
+}
 int blocked_fu_max(int64_t d, int32_t n_trees, int32_t depth) {
   const int64_t nodes = static_cast<int64_t>(n_trees) * ((int64_t{1} << depth) - 1);
   const int64_t fu = nodes < d ? nodes : d;
-  return fu * 4 <= 3 * d && fu <= 150 && d <= 65536 ? static_cast<int>(fu) : 0;  // (16-bit feature list)
+  // (16-bit feature list; a wave's partial vote fits the 8-bit LDS slot)
+  if (fu > DAL_FOREST_BLOCKED_MAX_RUNS || d > 65536 || n_trees > 255 * kForestWaves) return 0;
+  return blocked_smem(static_cast<int>(fu), d, n_trees, depth) <= 96 * 1024 ? static_cast<int>(fu) : 0;
 }
 
 struct ForestTiling {
@@ -599,11 +613,7 @@ int forest_score_launch(const float* x, const float* xb, int64_t n, int64_t d, i
     ForestArgs A{x, n, static_cast<int>(d), ldx, reinterpret_cast<const int2*>(inner), leaf, n_trees,
                  depth, lut, density_kind ? density : nullptr, density_kind, density_err, row_flags, beta,
                  order, votes, scores, keys, keys_hi, hooks_in};
-    const int64_t nn = static_cast<int64_t>(n_trees) * ((int64_t{1} << depth) - 1);
-    const int64_t nw = (d + 31) / 32;
-    const size_t smem = static_cast<size_t>(fu_max) * kBlk * 4 + static_cast<size_t>(nn) * 8 +
-                        static_cast<size_t>(round_up(static_cast<int64_t>(n_trees) << depth, 4)) +
-                        static_cast<size_t>(round_up(fu_max, 2)) * 2 + static_cast<size_t>(nw) * 8;
+    const size_t smem = blocked_smem(fu_max, d, n_trees, depth);
     const void* fn = reinterpret_cast<const void*>(forest_blocked_kernel);
     int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess ||

@@ -244,11 +244,11 @@ int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ldx,
  * (dal_pool_blocked_floats(n, d) floats; a per-pool copy, built once -- the
  * pool is constant across AL iterations).  dal_forest_score_blocked gives
  * dal_forest_score's outputs bit for bit; when dal_forest_blocked_rows(d,
- * n_trees, depth) is non-zero (a forest whose node count bounds its distinct
- * features at <= 3/4 d and <= 150) it reads only the features the forest
- * tests -- each tile's listed features as 256-B runs -- instead of whole rows
- * (config 4, T = 10: ~116 of 256 features), else it runs dal_forest_score's
- * row-major kernel on x.  xb must be 16-B aligned. */
+ * n_trees, depth) is non-zero (the forest's node count bounds its distinct
+ * features at <= 256, and a tile of those plus the forest fits 96 KiB of LDS)
+ * it reads only the features the forest tests -- each tile's listed features
+ * as 256-B runs (config 4, T = 10: ~116 of 256 features) -- else it runs
+ * dal_forest_score's row-major kernel on x.  xb must be 16-B aligned. */
 int dal_forest_blocked_rows(int64_t d, int32_t n_trees, int32_t depth);
 int64_t dal_pool_blocked_floats(int64_t n, int64_t d);
 int dal_pool_blocked(const float* x, int64_t n, int64_t d, int64_t ldx, float* xb, dal_stream_t stream);

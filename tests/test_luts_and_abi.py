@@ -92,19 +92,19 @@ def test_host_argument_validation_without_gpu():
 
 
 def test_blocked_pool_rule_without_gpu():
-    """ABI v9: the blocked K2 path applies when the forest's node count
-    bounds its distinct features at <= 3/4 d and <= 150 (config 4, T = 10:
-    150 of 256); the copy's size is whole 64-row tiles; bad arguments are
-    rejected before any HIP call."""
+    """ABI v9: the blocked K2 path applies when a tile's runs -- the forest's
+    node count bounds its distinct features -- number <= 256 and fit 96 KiB of
+    LDS with the forest, and a wave's partial vote fits 8 bits; the copy's
+    size is whole 64-row tiles; bad arguments are rejected before any HIP call."""
     lib = _lib.load()
-    assert lib.dal_forest_blocked_rows(256, 10, 4) == 64     # config 4
-    assert lib.dal_forest_blocked_rows(256, 100, 4) == 0     # config 4 at T = 100
-    assert lib.dal_forest_blocked_rows(256, 11, 4) == 0      # 165 > 150 runs
-    assert lib.dal_forest_blocked_rows(64, 10, 4) == 0       # config 2: 64 features, every one may be tested
-    assert lib.dal_forest_blocked_rows(30, 100, 4) == 0      # config 3
-    assert lib.dal_forest_blocked_rows(96, 4, 4) == 64       # 60 <= 72
-    assert lib.dal_forest_blocked_rows(80, 4, 4) == 64       # 60 <= 60
-    assert lib.dal_forest_blocked_rows(79, 4, 4) == 0        # 60 > 59.25
+    assert lib.dal_forest_blocked_rows(256, 10, 4) == 64     # config 4 (150 runs)
+    assert lib.dal_forest_blocked_rows(256, 100, 4) == 64    # config 4 at T = 100 (256 runs)
+    assert lib.dal_forest_blocked_rows(64, 10, 4) == 64      # config 2
+    assert lib.dal_forest_blocked_rows(30, 100, 4) == 64     # config 3
+    assert lib.dal_forest_blocked_rows(512, 100, 4) == 0     # 512 runs
+    assert lib.dal_forest_blocked_rows(300, 100, 8) == 0     # a 204-KB forest
+    assert lib.dal_forest_blocked_rows(20, 1021, 1) == 0     # partial votes past 8 bits
+    assert lib.dal_forest_blocked_rows(20, 1020, 1) == 64
     assert lib.dal_forest_blocked_rows(0, 10, 4) == 0 and lib.dal_forest_blocked_rows(256, 10, 17) == 0
     assert lib.dal_pool_blocked_floats(1, 256) == 64 * 256 and lib.dal_pool_blocked_floats(128, 3) == 128 * 3
     assert lib.dal_pool_blocked_floats(0, 8) == 0 and lib.dal_pool_blocked_floats(10, 0) == -1
