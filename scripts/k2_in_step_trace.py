@@ -1,7 +1,8 @@
 """K2 inside a warm step vs alone, one process, for rocprofv3 --kernel-trace:
 5 standalone dal_forest_score_blocked launches (no hooks), 5 eager fused
 steps (dal_dw_step: group-minima fold, stored row flags), 5 warm-plan
-replays (hipGraph: the fold plus the stamp-derived row flags).  Analyse with
+replays (hipGraph: the fold plus the stamp-derived row flags), 5 eager steps
+with the exact level 1 (no fold).  Analyse with
 --analyse DIR: per kernel name and phase, the median duration.
 usage: python scripts/k2_in_step_trace.py [CONFIG]   |   --analyse DIR"""
 import glob
@@ -13,7 +14,8 @@ REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 
 
 def analyse(d):
-    """The blocked K2 launches in order: 5 alone, 5 in eager steps, 6 in plan replays."""
+    """The blocked K2 launches in order: 5 alone, 5 in eager steps, 6 in plan
+    replays, 5 in eager steps with the exact level 1 (no group-minima hooks)."""
     import csv
     f = sorted(glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True))[-1]
     rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
@@ -21,7 +23,9 @@ def analyse(d):
           if "forest_blocked_kernel" in r["Kernel_Name"]]
     sel = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows
            if "summary_select_kernel" in r["Kernel_Name"]]
-    for nm, a, b in (("alone", 0, 5), ("eager step", 5, 10), ("plan replay", 10, 16)):
+    for nm, a, b in (("alone", 0, 5), ("eager step", 5, 10), ("plan replay", 10, 16), ("exact L1", 16, 21)):
+        if len(k2) < b:
+            continue
         print(f"K2 {nm:12s} median {statistics.median(k2[a:b]):8.1f} us  {[round(v, 1) for v in k2[a:b]]}")
     print(f"selection launches (cold, eager x5, plan x6): {[round(v, 1) for v in sel]}")
 
@@ -68,6 +72,11 @@ def main():
     torch.cuda.synchronize()
     st.use_graphs = True
     for _ in range(6):
+        engine.density_step(st, unl, forest, cfg["k"])
+    torch.cuda.synchronize()
+    # eager steps with the exact level 1 (no group-minima hooks in the score kernel)
+    st.use_graphs, st.level1_fast = False, False
+    for _ in range(5):
         engine.density_step(st, unl, forest, cfg["k"])
     torch.cuda.synchronize()
     print("ok")
