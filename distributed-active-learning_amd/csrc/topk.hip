@@ -1438,6 +1438,9 @@ struct GroupSummary {
 // keys per thread in registers, 8-bit digits) until the k-th key's bucket
 // holds <= 64 keys; tau is that bucket's upper edge.  Every block computes it
 // (no grid sync).
+#ifndef DAL_TAU_BUCKET
+#define DAL_TAU_BUCKET 64  // radix passes stop once the k-th key's bucket holds at most this many minima (256 / 1024: neutral)
+#endif
 __device__ unsigned long long group_threshold(const GroupSummary& S, int64_t k) {
   constexpr int PER = kMaxGroups / kSumThreads;
   constexpr int W = kSumThreads / 64;
@@ -1490,7 +1493,7 @@ __device__ unsigned long long group_threshold(const GroupSummary& S, int64_t k) 
   unsigned long long mask = top == 64 ? 0ull : ~((1ull << top) - 1ull);
   unsigned long long prefix = mn & mask;
   unsigned int krem = static_cast<unsigned int>(k), cnt = nv;
-  while (cnt > 64 && top > 0) {
+  while (cnt > DAL_TAU_BUCKET && top > 0) {
     const int width = top < 8 ? top : 8, shift = top - width;
     const unsigned dmask = (1u << width) - 1u;
 #pragma unroll
