@@ -104,13 +104,14 @@ struct GroupFold {
 // minima and atomic-max them into its row group (the atomics then complete
 // during that tile's traversal: up to 16 blocks hit a group's two words at
 // once, and a contended atomic in flight would hold the next DMA wait)
+template <int NW = kForestWaves>
 __device__ __forceinline__ void issue_fold(const ForestArgs& A, GroupFold& f,
-                                           const unsigned long long (*wmin)[2][kForestWaves]) {
+                                           const unsigned long long (*wmin)[2][NW]) {
   if (f.tile < 0) return;
-  const unsigned long long(&m)[2][kForestWaves] = wmin[f.slot ^ 1];
+  const unsigned long long(&m)[2][NW] = wmin[f.slot ^ 1];
   unsigned long long lo = m[0][0], hi = m[1][0];
 #pragma unroll
-  for (int w = 1; w < kForestWaves; ++w) {
+  for (int w = 1; w < NW; ++w) {
     lo = m[0][w] < lo ? m[0][w] : lo;
     hi = m[1][w] < hi ? m[1][w] : hi;
   }
@@ -128,17 +129,18 @@ __device__ __forceinline__ void issue_fold(const ForestArgs& A, GroupFold& f,
 // WROWS (the blocked feature-major path): wave w holds rows (w / tpr) * 64 +
 // lane and walks trees w % tpr, + tpr, ...; the waves' partial votes of a row
 // are summed through LDS.
-template <bool X_LDS, bool WROWS = false>
+template <bool X_LDS, bool WROWS = false, int NW = kForestWaves>
 __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs, int xstride, int64_t tile, int R,
                                            int tpr, const int2* inner, const uint8_t* leaf, bool pre,
                                            uint8_t fl_pre, long long dens_pre, GroupFold& fold,
-                                           unsigned long long (*wmin)[2][kForestWaves]) {
+                                           unsigned long long (*wmin)[2][NW]) {
+  constexpr int NT = NW * 64;  // threads of the block
   const int n_inner = (1 << A.depth) - 1;
   const int n_leaf = 1 << A.depth;
   const int tid = threadIdx.x;
   const int64_t row0 = tile * R;
   // bitmask form: wave w holds rows (w / tpr) * 64 + lane and trees w % tpr, +tpr, ...
-  const bool bm = DAL_FOREST_BITMASK && X_LDS && A.depth == 4 && R * tpr == kForestThreads && R % 64 == 0;
+  const bool bm = DAL_FOREST_BITMASK && X_LDS && A.depth == 4 && R * tpr == NT && R % 64 == 0;
   const bool wr = WROWS || bm;  // rows by wave lanes, trees by waves
   const int r = wr ? (tid >> 6) / tpr * 64 + (tid & 63) : tid / tpr;
   const int sub = wr ? (tid >> 6) % tpr : tid - r * tpr;
@@ -191,7 +193,7 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
     }
   }
   if (wr) {  // a row's tree phases are in different waves (partial votes < 256: T <= 1020 here)
-    __shared__ uint8_t s_vote[kForestThreads];
+    __shared__ uint8_t s_vote[NT];
     s_vote[sub * R + r] = static_cast<uint8_t>(v);
     __syncthreads();
     if (sub == 0)
@@ -246,7 +248,7 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
     fold.slot ^= 1;  // issue_fold reads slot ^ 1: this tile's
     return;
   }
-  __shared__ unsigned long long s_min[2][kForestThreads / 64];
+  __shared__ unsigned long long s_min[2][NW];
   if ((tid & 63) == 0) {
     s_min[0][tid >> 6] = klo;
     s_min[1][tid >> 6] = khi;
@@ -254,7 +256,7 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
   __syncthreads();
   if (tid == 0) {
 #pragma unroll
-    for (int w = 1; w < kForestThreads / 64; ++w) {
+    for (int w = 1; w < NW; ++w) {
       klo = s_min[0][w] < klo ? s_min[0][w] : klo;
       khi = s_min[1][w] < khi ? s_min[1][w] : khi;
     }
@@ -442,10 +444,12 @@ __global__ __launch_bounds__(256) void pool_blocked_kernel(const float* __restri
 // 64 consecutive words of a run whatever slot each lane's tree asks for --
 // no bank conflicts).  Bytes per row: 4 F_used + the epilogue's, against
 // 4 d for the row-major tile (config 4, T = 10: ~113 of 256 features).
-__global__ __launch_bounds__(kForestThreads) void forest_blocked_kernel(ForestArgs A, const float* __restrict__ xb,
-                                                                        int fu_max, int64_t n_tiles) {
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void forest_blocked_kernel(ForestArgs A, const float* __restrict__ xb,
+                                                                 int fu_max, int64_t n_tiles) {
+  constexpr int NT = NW * 64;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int tpr = kForestWaves;  // one tree phase per wave, 64 rows per tile
+  constexpr int tpr = NW;  // one tree phase per wave, 64 rows per tile
   const int n_inner = (1 << A.depth) - 1, n_leaf = 1 << A.depth;
   const int nn = A.n_trees * n_inner, nw = (A.d + 31) >> 5;
   float* xs = reinterpret_cast<float*>(smem);
@@ -457,32 +461,32 @@ __global__ __launch_bounds__(kForestThreads) void forest_blocked_kernel(ForestAr
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (A.hooks.status_reset && blockIdx.x == 0 && tid == 0) *A.hooks.status_reset = 0;
-  for (int w = tid; w < nw; w += kForestThreads) bits[w] = 0u;
-  for (int e = tid; e < A.n_trees * n_leaf; e += kForestThreads) ls[e] = A.leaf[e];
+  for (int w = tid; w < nw; w += NT) bits[w] = 0u;
+  for (int e = tid; e < A.n_trees * n_leaf; e += NT) ls[e] = A.leaf[e];
   __syncthreads();
-  for (int e = tid; e < nn; e += kForestThreads) {
+  for (int e = tid; e < nn; e += NT) {
     int2 q = A.inner[e];
     q.x = q.x < 0 ? 0 : q.x >= A.d ? A.d - 1 : q.x;  // (a valid forest tests features < d)
     fs[e] = q;
     atomicOr(&bits[q.x >> 5], 1u << (q.x & 31));
   }
   __syncthreads();
-  for (int w = tid; w < nw; w += kForestThreads) {
+  for (int w = tid; w < nw; w += NT) {
     int c = 0;
     for (int j = 0; j < w; ++j) c += __popc(bits[j]);
     pre[w] = c;
   }
   __syncthreads();
   auto slot = [&](int f) { return pre[f >> 5] + __popc(bits[f >> 5] & ((1u << (f & 31)) - 1u)); };
-  for (int f = tid; f < A.d; f += kForestThreads)
+  for (int f = tid; f < A.d; f += NT)
     if ((bits[f >> 5] >> (f & 31)) & 1u) used[slot(f)] = static_cast<uint16_t>(f);  // d <= 2^16 here
-  for (int e = tid; e < nn; e += kForestThreads) fs[e].x = slot(fs[e].x) * kBlk;
+  for (int e = tid; e < nn; e += NT) fs[e].x = slot(fs[e].x) * kBlk;
   const int fu = pre[nw - 1] + __popc(bits[nw - 1]);  // <= fu_max
   __syncthreads();
   const int n_ins = (fu + 3) >> 2;  // DMA instructions per tile (4 runs each)
   typedef __attribute__((address_space(3))) float lds_float;
   GroupFold fold;
-  __shared__ unsigned long long wmin[2][2][kForestWaves];
+  __shared__ unsigned long long wmin[2][2][NW];
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {  // block-uniform
     const int64_t row = tile * kBlk + lane;
     const bool lead = wave == 0 && row < A.n;  // the rows' epilogue: wave 0
@@ -493,7 +497,7 @@ __global__ __launch_bounds__(kForestThreads) void forest_blocked_kernel(ForestAr
       if (A.dkind) dens_pre = static_cast<const long long*>(A.density)[row];
     }
     const char* src = reinterpret_cast<const char*>(xb + tile * A.d * kBlk);
-    for (int i = wave; i < n_ins; i += kForestWaves) {
+    for (int i = wave; i < n_ins; i += NW) {
       const int sl = 4 * i + (lane >> 4);
       const unsigned dst = __builtin_amdgcn_readfirstlane(
           static_cast<unsigned>(reinterpret_cast<uintptr_t>((lds_float*)(xs + 4 * i * kBlk))));
@@ -510,11 +514,11 @@ __global__ __launch_bounds__(kForestThreads) void forest_blocked_kernel(ForestAr
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) issue_fold(A, fold, wmin);  // after this tile's DMA wait
-    score_tile<true, true>(A, xs, 1, tile, kBlk, tpr, fs, ls, true, fl_pre, dens_pre, fold, wmin);
+    if (tid == 0) issue_fold<NW>(A, fold, wmin);  // after this tile's DMA wait
+    score_tile<true, true, NW>(A, xs, 1, tile, kBlk, tpr, fs, ls, true, fl_pre, dens_pre, fold, wmin);
     __syncthreads();  // every wave done with the tile before the next one is staged
   }
-  if (tid == 0) issue_fold(A, fold, wmin);
+  if (tid == 0) issue_fold<NW>(A, fold, wmin);
 }
 
 }  // namespace
@@ -532,6 +536,13 @@ namespace {
 // identical: 2M x 256 x 100 501 -> 468 us, 1M x 128 x 100 193 -> 155 us,
 // 100k x 64 x 10 12.7 -> 9.6 us, config 3 43.4 -> 41.9 us): conflict-free
 // gathers, LDS-DMA staging and a persistent grid for every width.
+// Waves per block of the blocked kernel (the trees are dealt over them): 4,
+// or 8 when a block's LDS lets at most two blocks onto a CU (a 256-run tile
+// and a 100-tree forest): 2M x 256 x 100 469.7 -> 437.4 us, while 8 waves
+// where four-wave blocks fit three or more per CU were slower (config 4 at
+// T = 10 206 -> 234 us, config 3 41.8 -> 45.0 us).
+constexpr int kBlockedWaves = 4;
+constexpr int kBlockedWavesWide = 8;
 #ifndef DAL_FOREST_BLOCKED_MAX_RUNS
 #define DAL_FOREST_BLOCKED_MAX_RUNS 256
 #endif
@@ -545,7 +556,7 @@ int blocked_fu_max(int64_t d, int32_t n_trees, int32_t depth) {
   const int64_t nodes = static_cast<int64_t>(n_trees) * ((int64_t{1} << depth) - 1);
   const int64_t fu = nodes < d ? nodes : d;
   // (16-bit feature list; a wave's partial vote fits the 8-bit LDS slot)
-  if (fu > DAL_FOREST_BLOCKED_MAX_RUNS || d > 65536 || n_trees > 255 * kForestWaves) return 0;
+  if (fu > DAL_FOREST_BLOCKED_MAX_RUNS || d > 65536 || n_trees > 255 * kBlockedWaves) return 0;  // (either form)
   return blocked_smem(static_cast<int>(fu), d, n_trees, depth) <= 96 * 1024 ? static_cast<int>(fu) : 0;
 }
 
@@ -614,17 +625,24 @@ int forest_score_launch(const float* x, const float* xb, int64_t n, int64_t d, i
                  depth, lut, density_kind ? density : nullptr, density_kind, density_err, row_flags, beta,
                  order, votes, scores, keys, keys_hi, hooks_in};
     const size_t smem = blocked_smem(fu_max, d, n_trees, depth);
-    const void* fn = reinterpret_cast<const void*>(forest_blocked_kernel);
+    const bool wide = smem > (160u << 10) / 3;  // at most two blocks per CU by LDS: 8-wave blocks
+    const int nw = wide ? kBlockedWavesWide : kBlockedWaves;
+    const void* fn = wide ? reinterpret_cast<const void*>(forest_blocked_kernel<kBlockedWavesWide>)
+                          : reinterpret_cast<const void*>(forest_blocked_kernel<kBlockedWaves>);
     int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1 ||
         hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(smem)) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kForestThreads, smem) != hipSuccess)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, nw * 64, smem) != hipSuccess)
       return DAL_ERR_HIP;
     if (per_cu < 1) per_cu = 1;
     const int64_t grid = tiles < static_cast<int64_t>(cus) * per_cu ? tiles : static_cast<int64_t>(cus) * per_cu;
-    hipLaunchKernelGGL(forest_blocked_kernel, dim3(static_cast<unsigned>(grid)), dim3(kForestThreads), smem, st, A,
-                       xb, fu_max, tiles);
+    if (wide)
+      hipLaunchKernelGGL(forest_blocked_kernel<kBlockedWavesWide>, dim3(static_cast<unsigned>(grid)), dim3(nw * 64),
+                         smem, st, A, xb, fu_max, tiles);
+    else
+      hipLaunchKernelGGL(forest_blocked_kernel<kBlockedWaves>, dim3(static_cast<unsigned>(grid)), dim3(nw * 64),
+                         smem, st, A, xb, fu_max, tiles);
     DAL_RETURN_IF_LAUNCH_FAILED();
     return DAL_OK;
   }

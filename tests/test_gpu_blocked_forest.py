@@ -58,7 +58,8 @@ def _same(a, b):
 
 @pytest.mark.parametrize("n,d,trees,kind", [(100_003, 256, 10, "fixed"), (5_000, 256, 10, "none"),
                                             (37, 256, 10, "exact"), (64, 96, 4, "fixed"), (20_000, 512, 10, "fixed"),
-                                            (12_345, 200, 7, "none")])
+                                            (12_345, 200, 7, "none"),
+                                            (3_001, 256, 100, "fixed")])  # 256 runs: the 8-wave blocks
 def test_blocked_forest_bit_identical(cuda, n, d, trees, kind):
     from dal.forest import Forest
 
