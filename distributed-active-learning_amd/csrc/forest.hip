@@ -34,6 +34,9 @@ constexpr int kForestThreads = DAL_FOREST_THREADS;
 #define DAL_FOREST_ILP 4
 #endif
 constexpr int kTreeIlp = DAL_FOREST_ILP;  // independent tree walks in flight per lane
+#ifndef DAL_FOREST_BLOCKED_ILP
+#define DAL_FOREST_BLOCKED_ILP 4  // ... in the blocked kernel
+#endif
 // Timing-only A/B (scripts/ab_build.sh -DDAL_FOREST_BITMASK=1; verdict r4 item
 // 5): depth-4 trees evaluated whole -- every wave walks one tree at a time for
 // 64 rows, reads the tree's 15 nodes at wave-uniform LDS addresses, gathers
@@ -129,7 +132,7 @@ __device__ __forceinline__ void issue_fold(const ForestArgs& A, GroupFold& f,
 // WROWS (the blocked feature-major path): wave w holds rows (w / tpr) * 64 +
 // lane and walks trees w % tpr, + tpr, ...; the waves' partial votes of a row
 // are summed through LDS.
-template <bool X_LDS, bool WROWS = false, int NW = kForestWaves>
+template <bool X_LDS, bool WROWS = false, int NW = kForestWaves, int ILP = kTreeIlp>
 __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs, int xstride, int64_t tile, int R,
                                            int tpr, const int2* inner, const uint8_t* leaf, bool pre,
                                            uint8_t fl_pre, long long dens_pre, GroupFold& fold,
@@ -168,20 +171,20 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
     }
   } else if (live) {
     int t = sub;
-    for (; t + (kTreeIlp - 1) * tpr < A.n_trees; t += kTreeIlp * tpr) {
-      int h[kTreeIlp];
+    for (; t + (ILP - 1) * tpr < A.n_trees; t += ILP * tpr) {
+      int h[ILP];
 #pragma unroll
-      for (int j = 0; j < kTreeIlp; ++j) h[j] = 0;
+      for (int j = 0; j < ILP; ++j) h[j] = 0;
       for (int lvl = 0; lvl < A.depth; ++lvl) {
 #pragma unroll
-        for (int j = 0; j < kTreeIlp; ++j) {
+        for (int j = 0; j < ILP; ++j) {
           const int2 nd = inner[(t + j * tpr) * n_inner + h[j]];
           const float xv = xrow[nd.x];
           h[j] = 2 * h[j] + (xv <= __int_as_float(nd.y) ? 1 : 2);
         }
       }
 #pragma unroll
-      for (int j = 0; j < kTreeIlp; ++j) v += leaf[(t + j * tpr) * n_leaf + (h[j] - n_inner)];
+      for (int j = 0; j < ILP; ++j) v += leaf[(t + j * tpr) * n_leaf + (h[j] - n_inner)];
     }
     for (; t < A.n_trees; t += tpr) {
       int h = 0;
@@ -515,7 +518,8 @@ __global__ __launch_bounds__(NW * 64) void forest_blocked_kernel(ForestArgs A, c
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) issue_fold<NW>(A, fold, wmin);  // after this tile's DMA wait
-    score_tile<true, true, NW>(A, xs, 1, tile, kBlk, tpr, fs, ls, true, fl_pre, dens_pre, fold, wmin);
+    score_tile<true, true, NW, DAL_FOREST_BLOCKED_ILP>(A, xs, 1, tile, kBlk, tpr, fs, ls, true, fl_pre, dens_pre,
+                                                       fold, wmin);
     __syncthreads();  // every wave done with the tile before the next one is staged
   }
   if (tid == 0) issue_fold<NW>(A, fold, wmin);
