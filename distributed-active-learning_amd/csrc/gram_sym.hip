@@ -485,10 +485,6 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
 //  3. per row r of the requested super blocks: acc[r] += rint(2^8 *
 //     (<L_r, R_B> + <u~_r, C_B>)) with the dots in fp64 in a fixed order.
 
-__device__ __forceinline__ long long half_units(uint16_t bits) {  // fp16 value * 2^24, exact
-  return static_cast<long long>(static_cast<float>(__builtin_bit_cast(_Float16, bits)) * 16777216.0f);
-}
-
 // One block per (super block, group of 256 16-byte chunk columns): the
 // super block's 512 operand rows are 512 x CPR 16-byte chunks (CPR = ldh / 8
 // per row: the H and L halves of every slice); thread t always reads chunk
@@ -507,7 +503,10 @@ __global__ __launch_bounds__(256) void csym_sigma_kernel(const uint16_t* __restr
   // this block's rows of the super block: [rb, re) (gridDim.z row slices)
   const int rb = kSB * static_cast<int>(blockIdx.z) / static_cast<int>(gridDim.z);
   const int re = kSB * (static_cast<int>(blockIdx.z) + 1) / static_cast<int>(gridDim.z);
-  long long acc[8] = {};
+  // Summed in fp64, exactly: every term is a multiple of 2^-24 below 2^13 and
+  // a thread adds at most kSB of them (< 2^22), so every partial sum has at
+  // most 46 significant bits; converted to int64 units once at the end.
+  double acc[8] = {};
   if (col < cpr && r0 < rstep) {
     const uint4* base = reinterpret_cast<const uint4*>(ops + static_cast<int64_t>(Q) * kSB * ldh) + col;
     for (int r = rb + r0; r < re; r += 8 * rstep) {
@@ -519,14 +518,16 @@ __global__ __launch_bounds__(256) void csym_sigma_kernel(const uint16_t* __restr
         const uint32_t w[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          acc[2 * e] += half_units(static_cast<uint16_t>(w[e] & 0xFFFFu));
-          acc[2 * e + 1] += half_units(static_cast<uint16_t>(w[e] >> 16));
+          acc[2 * e] += static_cast<double>(
+              static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(w[e] & 0xFFFFu))));
+          acc[2 * e + 1] += static_cast<double>(
+              static_cast<float>(__builtin_bit_cast(_Float16, static_cast<uint16_t>(w[e] >> 16))));
         }
       }
     }
   }
 #pragma unroll
-  for (int e = 0; e < 8; ++e) red[threadIdx.x][e] = acc[e];
+  for (int e = 0; e < 8; ++e) red[threadIdx.x][e] = static_cast<long long>(acc[e] * 16777216.0);
   __syncthreads();
   // thread t < cols finishes chunk column t: sum over the rstep row phases
   if (threadIdx.x < cols && col < cpr) {
@@ -565,14 +566,22 @@ __global__ __launch_bounds__(64 * kScanWaves) void csym_scan_kernel(const long l
   const int q1 = static_cast<int>(static_cast<int64_t>(ns) * (w + 1) / kW);
   // u~ sums per parity class of the super block (even, odd); named
   // registers, not arrays indexed by q & 1 (those would live in scratch)
+  // loads in batches of kScanBatch, all in flight before the adds (a wave walks
+  // ns / kW super blocks: 244 at config 4)
+  constexpr int kScanBatch = 16;
   long long ue = 0, uo = 0;
   if (live) {
-#pragma unroll 8
-    for (int q = q0; q < q1; ++q) {
-      const long long su = sig_u[static_cast<int64_t>(q) * d_pad + f];
-      const bool odd = q & 1;
-      ue += odd ? 0 : su;
-      uo += odd ? su : 0;
+    for (int qb = q0; qb < q1; qb += kScanBatch) {
+      long long v[kScanBatch];
+#pragma unroll
+      for (int j = 0; j < kScanBatch; ++j)
+        v[j] = qb + j < q1 ? sig_u[static_cast<int64_t>(qb + j) * d_pad + f] : 0;
+#pragma unroll
+      for (int j = 0; j < kScanBatch; ++j) {
+        const bool odd = (qb + j) & 1;
+        ue += odd ? 0 : v[j];
+        uo += odd ? v[j] : 0;
+      }
     }
   }
   part[w][0][lane] = ue;
@@ -590,72 +599,105 @@ __global__ __launch_bounds__(64 * kScanWaves) void csym_scan_kernel(const long l
     tuo += a1;
   }
   if (!live) return;
-#pragma unroll 4
-  for (int q = q0; q < q1; ++q) {
-    // e* = exclusive prefix (super blocks < q) per class; b = q's class
-    const bool odd = q & 1;
-    if (q >= b0 && q < b1) {
-      // R_B = sum_{Q >= B, same class} + sum_{Q < B, other class} of sigma~
-      // (the super blocks B takes); C_B = sum_{P < B, same class} + sum_{P >
-      // B, other class} of sigma~ (the other super blocks that take B: their
-      // pairs' column sums for B's rows)
-      const long long R = odd ? (tuo - euo + eue) : (tue - eue + euo);
-      const long long Cc = odd ? (euo + tue - eue) : (eue + tuo - euo);
-      rb[static_cast<int64_t>(q - b0) * d_pad + f] = static_cast<double>(R);
-      cb[static_cast<int64_t>(q - b0) * d_pad + f] = static_cast<double>(Cc);
+  for (int qb = q0; qb < q1; qb += kScanBatch) {
+    long long v[kScanBatch];
+#pragma unroll
+    for (int j = 0; j < kScanBatch; ++j)
+      v[j] = qb + j < q1 ? sig_u[static_cast<int64_t>(qb + j) * d_pad + f] : 0;
+#pragma unroll
+    for (int j = 0; j < kScanBatch; ++j) {
+      const int q = qb + j;
+      // e* = exclusive prefix (super blocks < q) per class; b = q's class
+      const bool odd = q & 1;
+      if (q < q1 && q >= b0 && q < b1) {
+        // R_B = sum_{Q >= B, same class} + sum_{Q < B, other class} of sigma~
+        // (the super blocks B takes); C_B = sum_{P < B, same class} + sum_{P >
+        // B, other class} of sigma~ (the other super blocks that take B: their
+        // pairs' column sums for B's rows)
+        const long long R = odd ? (tuo - euo + eue) : (tue - eue + euo);
+        const long long Cc = odd ? (euo + tue - eue) : (eue + tuo - euo);
+        rb[static_cast<int64_t>(q - b0) * d_pad + f] = static_cast<double>(R);
+        cb[static_cast<int64_t>(q - b0) * d_pad + f] = static_cast<double>(Cc);
+      }
+      eue += odd ? 0 : v[j];
+      euo += odd ? v[j] : 0;
     }
-    const long long su = sig_u[static_cast<int64_t>(q) * d_pad + f];
-    eue += odd ? 0 : su;
-    euo += odd ? su : 0;
   }
 }
 
 // One thread per row: a block's 256 rows lie in one super block B, whose R_B
 // and C_B are staged in LDS once; each thread sums its row's features in
 // order, t = t + l_f R_f, t = t + (h_f + l_f) C_f for f = 0, 1, ... (fp64, no
-// FMA) -- a fixed order, so the bits are the same on every GPU count.  The
-// row's operand is read 16 B (8 halves) at a time.  rows: the operand of the
-// requested super blocks.  (Round 4: one wave per row, lanes over features and
-// a butterfly -- 2-byte loads, 57 us of the 0.81 ms config-2 Gram.)
+// FMA) -- a fixed order, so the bits are the same on every GPU count.  rows:
+// the operand of the requested super blocks.  The rows reach the threads
+// through LDS, kResFeat features at a time: the block reads each row's H and L
+// runs of those features with coalesced 16-B loads (consecutive threads,
+// consecutive chunks of one row), so every fetched line is used at once.
+// (Round 5 before: each thread read its own row 16 B at a time, 64 rows one
+// ldh apart per wave instruction -- the lines left L2 before their other
+// chunks were read, 2.2 ms for config 4's 2 GB operand.  Round 4: one wave per
+// row, lanes over features and a butterfly -- 2-byte loads.)
 constexpr int kResRows = 256;
+constexpr int kResFeat = 32;                 // features per LDS stage (divides every KS)
+constexpr int kResQ = kResFeat / 4;          // 16-B chunks per row per stage: H kResFeat/8, L kResFeat/8
+constexpr int kResLd = kResQ + 1;            // LDS row stride in 16-B chunks (+1: the threads' rows spread over the banks)
 __global__ __launch_bounds__(kResRows) void csym_residual_kernel(const uint16_t* __restrict__ rows, int64_t ldh, int ks,
                                                                  int d_pad, int b0, int n_rows,
                                                                  const double* __restrict__ rb,
                                                                  const double* __restrict__ cb,
                                                                  long long* __restrict__ acc) {
   extern __shared__ double rc[];  // [d_pad] R_B | [d_pad] C_B
+  __shared__ uint4 tile[kResRows * kResLd];
+  const int tid = threadIdx.x;
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kResRows;  // (a multiple of 256: one super block)
   const int64_t B = r0 / kSB;                                       // relative to b0
-  for (int f = threadIdx.x; f < d_pad; f += kResRows) {
+  for (int f = tid; f < d_pad; f += kResRows) {
     rc[f] = rb[B * d_pad + f];
     rc[d_pad + f] = cb[B * d_pad + f];
   }
-  __syncthreads();
-  const int64_t rr = r0 + threadIdx.x;
-  if (rr >= n_rows) return;
-  const uint4* row = reinterpret_cast<const uint4*>(rows + rr * ldh);
-  const int hs = ks / 8;  // 16-B chunks per half of a slice
+  const int live_rows = n_rows - r0 < kResRows ? static_cast<int>(n_rows - r0) : kResRows;
+  const uint16_t* blk = rows + r0 * ldh;
   double t = 0.0;
-  for (int s0 = 0; s0 < d_pad; s0 += ks) {
-    const uint4* sl = row + (s0 / ks) * 2 * hs;
-    for (int c = 0; c < hs; ++c) {
-      const uint4 hq = sl[c], lq = sl[hs + c];
-      const uint32_t hw[4] = {hq.x, hq.y, hq.z, hq.w}, lw[4] = {lq.x, lq.y, lq.z, lq.w};
+  for (int f0 = 0; f0 < d_pad; f0 += kResFeat) {
+    // the stage's H run starts at halves (f0 / ks) * 2 ks + f0 % ks, its L run ks later
+    const int64_t hoff = static_cast<int64_t>(f0 / ks) * 2 * ks + f0 % ks;
+    uint4 q[kResQ];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int f = s0 + c * 8 + e;
-        const uint16_t hb = static_cast<uint16_t>(e & 1 ? hw[e >> 1] >> 16 : hw[e >> 1] & 0xFFFFu);
-        const uint16_t lb = static_cast<uint16_t>(e & 1 ? lw[e >> 1] >> 16 : lw[e >> 1] & 0xFFFFu);
-        const double h = static_cast<double>(static_cast<float>(__builtin_bit_cast(_Float16, hb)));
-        const double l = static_cast<double>(static_cast<float>(__builtin_bit_cast(_Float16, lb)));
-        t = t + l * rc[f];
-        t = t + (h + l) * rc[d_pad + f];
+    for (int j = 0; j < kResQ; ++j) {
+      const int e = tid + kResRows * j;
+      const int r = e / kResQ, c = e % kResQ;  // row of the block, chunk of the stage (H first, then L)
+      const int64_t off = r * ldh + hoff + (c < kResQ / 2 ? c * 8 : ks + (c - kResQ / 2) * 8);
+      q[j] = r < live_rows ? *reinterpret_cast<const uint4*>(blk + off) : uint4{};
+    }
+    if (f0) __syncthreads();  // the previous stage's tile is consumed
+#pragma unroll
+    for (int j = 0; j < kResQ; ++j) {
+      const int e = tid + kResRows * j;
+      tile[(e / kResQ) * kResLd + e % kResQ] = q[j];
+    }
+    __syncthreads();
+    if (tid < live_rows) {
+#pragma unroll
+      for (int c = 0; c < kResQ / 2; ++c) {
+        const uint4 hq = tile[tid * kResLd + c], lq = tile[tid * kResLd + kResQ / 2 + c];
+        const uint32_t hw[4] = {hq.x, hq.y, hq.z, hq.w}, lw[4] = {lq.x, lq.y, lq.z, lq.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int f = f0 + c * 8 + e;
+          const uint16_t hb = static_cast<uint16_t>(e & 1 ? hw[e >> 1] >> 16 : hw[e >> 1] & 0xFFFFu);
+          const uint16_t lb = static_cast<uint16_t>(e & 1 ? lw[e >> 1] >> 16 : lw[e >> 1] & 0xFFFFu);
+          const double h = static_cast<double>(static_cast<float>(__builtin_bit_cast(_Float16, hb)));
+          const double l = static_cast<double>(static_cast<float>(__builtin_bit_cast(_Float16, lb)));
+          t = t + l * rc[f];
+          t = t + (h + l) * rc[d_pad + f];
+        }
       }
     }
   }
   // R, C in units of 2^-24 x (split units); value = t * 2^-24 * 2^-24 ... in
   // fixed point (2^32): t * 2^-24 (operand units^2 = 2^24 x value) * 2^8
-  if (t != 0.0) acc[static_cast<int64_t>(b0) * kSB + rr] += static_cast<long long>(__builtin_rint(t * 0x1p-16));
+  if (tid < live_rows && t != 0.0)
+    acc[static_cast<int64_t>(b0) * kSB + r0 + tid] += static_cast<long long>(__builtin_rint(t * 0x1p-16));
 }
 
 // ---------------------------------------------------------------------------

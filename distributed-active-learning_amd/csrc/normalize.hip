@@ -78,44 +78,99 @@ __global__ __launch_bounds__(kNormThreads) void normalize_rows_kernel(
 }
 
 // partials[c][f] = sum_{r in chunk c, not excluded} x_rf / norm64[r]
-// (sequential over the chunk's rows).  The four waves divide 64 rows each
-// (lanes = features, coalesced loads) into an fp64 LDS tile; wave 0 then adds
-// the 256 rows in order -- the canonical sequence, but with the divisions and
-// loads in parallel.
-template <int kColFeat>
-__global__ __launch_bounds__(256) void canon_colsum_partials_kernel(
-    const float* __restrict__ x, int64_t n, int d, int64_t ldx, const double* __restrict__ norm64,
-    const uint8_t* __restrict__ flags, double* __restrict__ partials) {
-  // block = (256-row chunk, kColFeat features): all 256 threads compute the
-  // fp64 unit values (the divisions) into LDS, then kColFeat lanes add the 256
-  // rows in order.  Small blocks -> many chunks in flight per CU: the
-  // sequential add chains overlap instead of running one chunk per CU.
+// (sequential over the chunk's rows).  Two kernels, the same bits:
+//  * many chunks (config 4): one wave per (chunk, 64 features), lane =
+//    feature, so every row's features are one coalesced load; the chunk goes
+//    in batches of kColBatch rows, lane j of a batch also loading row j's norm
+//    and flag, broadcast to the wave for the in-order divisions and adds;
+//  * few chunks (configs 2, 3): a block per (chunk, 8 features), all 256
+//    threads forming the quotients into an fp64 LDS tile, then 8 lanes adding
+//    the 256 rows in order -- more waves for the same work (the wave kernel:
+//    100k x 64 43 -> 109 us, 284,807 x 30 55 -> 125 us for the whole prep).
+// The block kernel alone: 1.72 ms at config 4, the wave kernel 1.49 ms (fp64
+// VALU bound: ~21 instructions per row and wave; the 2 GB are fetched once).
+// Markstein's reciprocal division (3 fp64 operations per element in place of
+// the division sequence) measured no faster in either kernel and is not used.
+constexpr int kColBatch = 32;
+#ifndef DAL_COLSUM_WAVE_MIN
+#define DAL_COLSUM_WAVE_MIN 8192  // waves (chunks x 64-feature groups) from which the wave kernel runs
+#endif
+
+__global__ __launch_bounds__(256) void canon_colsum_wave_kernel(const float* __restrict__ x, int64_t n, int d,
+                                                                int64_t ldx, const double* __restrict__ norm64,
+                                                                const uint8_t* __restrict__ flags,
+                                                                double* __restrict__ partials) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int fgroups = (d + 63) / 64;
+  const int64_t c = wave / fgroups;
+  const int f = static_cast<int>(wave % fgroups) * 64 + lane;
+  const int64_t chunks = (n + DAL_CANON_CHUNK - 1) / DAL_CANON_CHUNK;
+  if (c >= chunks) return;  // (whole waves)
+  const bool lf = f < d;
+  // Excluded / padding rows contribute +0.0: the running sum starts at +0.0
+  // and can never become -0.0, so adding +0.0 is bit-identical to skipping.
+  double acc = 0.0;
+#pragma unroll 1
+  for (int64_t rb = c * DAL_CANON_CHUNK; rb < (c + 1) * DAL_CANON_CHUNK; rb += kColBatch) {
+    float xv[kColBatch];
+#pragma unroll
+    for (int j = 0; j < kColBatch; ++j) xv[j] = (lf && rb + j < n) ? x[(rb + j) * ldx + f] : 0.0f;
+    const int64_t rl = rb + lane;
+    const bool in = lane < kColBatch && rl < n;
+    const double nl = in ? norm64[rl] : 1.0;
+    const uint64_t nb = __builtin_bit_cast(uint64_t, nl);
+    const uint64_t live = __ballot(in && !(flags && (flags[rl] & DAL_ROW_EXCLUDED)));
+    const int nlo = static_cast<int>(static_cast<uint32_t>(nb)), nhi = static_cast<int>(static_cast<uint32_t>(nb >> 32));
+#pragma unroll
+    for (int j = 0; j < kColBatch; ++j) {
+      const double nj = __builtin_bit_cast(
+          double, static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(nlo, j))) |
+                      (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(nhi, j))) << 32));
+      const double u = ((live >> j) & 1) ? static_cast<double>(xv[j]) / nj : 0.0;
+      acc = acc + u;
+    }
+  }
+  if (lf) partials[c * d + f] = acc;
+}
+
+constexpr int kColFeat = 8;  // features per block of the few-chunks kernel
+__global__ __launch_bounds__(256) void canon_colsum_block_kernel(const float* __restrict__ x, int64_t n, int d,
+                                                                 int64_t ldx, const double* __restrict__ norm64,
+                                                                 const uint8_t* __restrict__ flags,
+                                                                 double* __restrict__ partials) {
   __shared__ double u[DAL_CANON_CHUNK][kColFeat];
+  __shared__ double sn[DAL_CANON_CHUNK];
+  __shared__ uint8_t sl[DAL_CANON_CHUNK];
   const int tid = threadIdx.x;
   const int fl = tid % kColFeat, rs = tid / kColFeat;
   const int64_t c = blockIdx.x;
   const int f = blockIdx.y * kColFeat + fl;
-  // Excluded / padding rows contribute +0.0: the running sum starts at +0.0
-  // and can never become -0.0, so adding +0.0 is bit-identical to skipping.
   constexpr int kRowsPerPass = 256 / kColFeat;
-  // all loads of the thread's 16 rows first (in flight together), then the
-  // divisions: a load-then-divide loop would serialise 16 memory latencies
   constexpr int kPer = DAL_CANON_CHUNK / kRowsPerPass;
+  // every thread: one row's norm and liveness; its kPer features
+  // loaded meanwhile (all in flight)
+  static_assert(DAL_CANON_CHUNK == 256, "one row per thread");
+  {
+    const int64_t r = c * DAL_CANON_CHUNK + tid;
+    const double nr = r < n ? norm64[r] : 1.0;
+    sn[tid] = nr;
+    sl[tid] = r < n && !(flags && (flags[r] & DAL_ROW_EXCLUDED));
+  }
   float xv[kPer];
-  double nv[kPer];
-  bool lv[kPer];
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
     const int64_t r = c * DAL_CANON_CHUNK + rs + k * kRowsPerPass;
-    lv[k] = r < n && f < d;
-    const int64_t rr = lv[k] ? r : 0;
-    xv[k] = lv[k] ? x[rr * ldx + f] : 0.0f;
-    nv[k] = lv[k] ? norm64[rr] : 1.0;
-    if (lv[k] && flags && (flags[rr] & DAL_ROW_EXCLUDED)) lv[k] = false;
+    xv[k] = (r < n && f < d) ? x[r * ldx + f] : 0.0f;
   }
+  __syncthreads();
+  // Excluded / padding rows contribute +0.0: the running sum starts at +0.0
+  // and can never become -0.0, so adding +0.0 is bit-identical to skipping.
 #pragma unroll
-  for (int k = 0; k < kPer; ++k)
-    u[rs + k * kRowsPerPass][fl] = lv[k] ? static_cast<double>(xv[k]) / nv[k] : 0.0;
+  for (int k = 0; k < kPer; ++k) {
+    const int rl = rs + k * kRowsPerPass;
+    u[rl][fl] = (sl[rl] && f < d) ? static_cast<double>(xv[k]) / sn[rl] : 0.0;
+  }
   __syncthreads();
   if (tid >= kColFeat || f >= d) return;
   double acc = 0.0;
@@ -303,14 +358,15 @@ extern "C" int dal_canon_colsum_partials(const float* x, int64_t n, int64_t d, i
                                          double* partials, dal_stream_t stream) {
   if (!x || !norm64 || !partials) return DAL_ERR_ARG;
   if (n < 1 || d < 1 || ldx < d) return DAL_ERR_SHAPE;
-  const int64_t chunks = ceil_div(n, DAL_CANON_CHUNK);
-  // features per block: 8 (scripts/colsum_ab.py: 100k x 64 33.3 -> 27.8 us, 284,807 x 30
-  // 48.4 -> 36.6, 2M x 256 2.31 -> 1.58 ms against 16; 4 and 32 slower): more, smaller
-  // blocks keep more of the sequential 256-add chains in flight
-  constexpr int kCf = 8;
-  hipLaunchKernelGGL(canon_colsum_partials_kernel<kCf>,
-                     dim3(static_cast<unsigned>(chunks), static_cast<unsigned>(ceil_div(d, kCf))), dim3(256), 0,
-                     as_stream(stream), x, n, static_cast<int>(d), ldx, norm64, row_flags, partials);
+  const int64_t chunks = ceil_div(n, DAL_CANON_CHUNK), waves = chunks * ceil_div(d, 64);
+  if (waves >= DAL_COLSUM_WAVE_MIN) {
+    hipLaunchKernelGGL(canon_colsum_wave_kernel, dim3(static_cast<unsigned>(ceil_div(waves, 4))), dim3(256), 0,
+                       as_stream(stream), x, n, static_cast<int>(d), ldx, norm64, row_flags, partials);
+  } else {
+    hipLaunchKernelGGL(canon_colsum_block_kernel,
+                       dim3(static_cast<unsigned>(chunks), static_cast<unsigned>(ceil_div(d, kColFeat))), dim3(256), 0,
+                       as_stream(stream), x, n, static_cast<int>(d), ldx, norm64, row_flags, partials);
+  }
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
 }
