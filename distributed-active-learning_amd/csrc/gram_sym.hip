@@ -481,7 +481,9 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
 //  1. per super block Q: sigma~_Q and sigma^L_Q, exact int64 in units of 2^-24
 //     (every H and L is a multiple of 2^-24 below 2^13);
 //  2. per feature: exclusive prefix sums over super blocks of each parity
-//     class and their totals, giving R_B and C_B for every requested B;
+//     class and their totals, giving R_B and C_B for every requested B (for
+//     d_pad <= 64 and few super blocks the launch-3 blocks form their own R_B,
+//     C_B from sigma~ instead: one launch less, 21 us at configs 2 and 3);
 //  3. per row r of the requested super blocks: acc[r] += rint(2^8 *
 //     (<L_r, R_B> + <u~_r, C_B>)) with the dots in fp64 in a fixed order.
 
@@ -554,6 +556,10 @@ __global__ __launch_bounds__(256) void csym_sigma_kernel(const uint16_t* __restr
 #define DAL_CSYM_SCAN_WAVES 16
 #endif
 constexpr int kScanWaves = DAL_CSYM_SCAN_WAVES;  // super-block ranges per feature (one wave each)
+constexpr int kScanBatch = 16;                   // sigma~ loads in flight per thread
+#ifndef DAL_CSYM_FUSED_MAX
+#define DAL_CSYM_FUSED_MAX 65536  // super blocks x d_pad up to which the residual blocks skip the scan
+#endif
 __global__ __launch_bounds__(64 * kScanWaves) void csym_scan_kernel(const long long* __restrict__ sig_u, int ns,
                                                                     int d_pad, int b0, int b1,
                                                                     double* __restrict__ rb, double* __restrict__ cb) {
@@ -568,7 +574,6 @@ __global__ __launch_bounds__(64 * kScanWaves) void csym_scan_kernel(const long l
   // registers, not arrays indexed by q & 1 (those would live in scratch)
   // loads in batches of kScanBatch, all in flight before the adds (a wave walks
   // ns / kW super blocks: 244 at config 4)
-  constexpr int kScanBatch = 16;
   long long ue = 0, uo = 0;
   if (live) {
     for (int qb = q0; qb < q1; qb += kScanBatch) {
@@ -641,19 +646,65 @@ constexpr int kResRows = 256;
 constexpr int kResFeat = 32;                 // features per LDS stage (divides every KS)
 constexpr int kResQ = kResFeat / 4;          // 16-B chunks per row per stage: H kResFeat/8, L kResFeat/8
 constexpr int kResLd = kResQ + 1;            // LDS row stride in 16-B chunks (+1: the threads' rows spread over the banks)
+// kFused (d_pad 32 or 64, few super blocks): no scan launch -- every block forms
+// its own R_B and C_B from sigma~ (256 / d_pad thread groups over the super
+// blocks, exact int64 sums reduced in LDS; the same integers as the scan's).
+template <bool kFused>
 __global__ __launch_bounds__(kResRows) void csym_residual_kernel(const uint16_t* __restrict__ rows, int64_t ldh, int ks,
                                                                  int d_pad, int b0, int n_rows,
                                                                  const double* __restrict__ rb,
                                                                  const double* __restrict__ cb,
+                                                                 const long long* __restrict__ sig_u, int ns,
                                                                  long long* __restrict__ acc) {
   extern __shared__ double rc[];  // [d_pad] R_B | [d_pad] C_B
   __shared__ uint4 tile[kResRows * kResLd];
   const int tid = threadIdx.x;
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kResRows;  // (a multiple of 256: one super block)
   const int64_t B = r0 / kSB;                                       // relative to b0
-  for (int f = tid; f < d_pad; f += kResRows) {
-    rc[f] = rb[B * d_pad + f];
-    rc[d_pad + f] = cb[B * d_pad + f];
+  if constexpr (kFused) {
+    __shared__ long long red[4][kResRows];
+    const int qB = b0 + static_cast<int>(B);  // this block's super block
+    const int G = kResRows / d_pad, f = tid % d_pad, grp = tid / d_pad;
+    long long pe = 0, po = 0, te = 0, to = 0;  // per class: sums over super blocks < qB, and totals
+    for (int qb = grp; qb < ns; qb += kScanBatch * G) {
+      long long v[kScanBatch];
+#pragma unroll
+      for (int j = 0; j < kScanBatch; ++j) {
+        const int q = qb + j * G;
+        v[j] = q < ns ? sig_u[static_cast<int64_t>(q) * d_pad + f] : 0;
+      }
+#pragma unroll
+      for (int j = 0; j < kScanBatch; ++j) {
+        const int q = qb + j * G;
+        const bool odd = q & 1, before = q < qB;
+        te += odd ? 0 : v[j];
+        to += odd ? v[j] : 0;
+        pe += before && !odd ? v[j] : 0;
+        po += before && odd ? v[j] : 0;
+      }
+    }
+    red[0][tid] = pe;
+    red[1][tid] = po;
+    red[2][tid] = te;
+    red[3][tid] = to;
+    __syncthreads();
+    if (tid < d_pad) {
+      long long eue = 0, euo = 0, tue = 0, tuo = 0;
+      for (int g = 0; g < G; ++g) {
+        eue += red[0][g * d_pad + tid];
+        euo += red[1][g * d_pad + tid];
+        tue += red[2][g * d_pad + tid];
+        tuo += red[3][g * d_pad + tid];
+      }
+      const bool odd = qB & 1;  // R_B, C_B as in csym_scan_kernel
+      rc[tid] = static_cast<double>(odd ? (tuo - euo + eue) : (tue - eue + euo));
+      rc[d_pad + tid] = static_cast<double>(odd ? (euo + tue - eue) : (eue + tuo - euo));
+    }
+  } else {
+    for (int f = tid; f < d_pad; f += kResRows) {
+      rc[f] = rb[B * d_pad + f];
+      rc[d_pad + f] = cb[B * d_pad + f];
+    }
   }
   const int live_rows = n_rows - r0 < kResRows ? static_cast<int>(n_rows - r0) : kResRows;
   const uint16_t* blk = rows + r0 * ldh;
@@ -1003,14 +1054,23 @@ extern "C" int dal_gram_sym_residual(const uint16_t* ops, int64_t nb_active, int
                      dim3(static_cast<unsigned>(na), static_cast<unsigned>(ceil_div(ldh / 8, 256)), 4), dim3(256), 0,
                      st, ops, ldh, ks, static_cast<int>(d_pad), sig_u);
   DAL_RETURN_IF_LAUNCH_FAILED();
-  hipLaunchKernelGGL(csym_scan_kernel, dim3(static_cast<unsigned>(ceil_div(d_pad, 64))), dim3(64 * kScanWaves), 0, st, sig_u,
-                     static_cast<int>(na), static_cast<int>(d_pad), static_cast<int>(s0), static_cast<int>(s0 + ns),
-                     rb, cb);
-  DAL_RETURN_IF_LAUNCH_FAILED();
   const int64_t n_rows = ns * kSB;
-  hipLaunchKernelGGL(csym_residual_kernel, dim3(static_cast<unsigned>(ceil_div(n_rows, kResRows))), dim3(kResRows),
-                     static_cast<size_t>(2 * d_pad) * 8, st, ops + s0 * kSB * ldh, ldh, ks, static_cast<int>(d_pad),
-                     static_cast<int>(s0), static_cast<int>(n_rows), rb, cb, reinterpret_cast<long long*>(acc));
+  const dim3 grid(static_cast<unsigned>(ceil_div(n_rows, kResRows)));
+  const size_t smem = static_cast<size_t>(2 * d_pad) * 8;
+  const uint16_t* rows = ops + s0 * kSB * ldh;
+  if (d_pad <= 64 && na * d_pad <= DAL_CSYM_FUSED_MAX) {  // the blocks form R_B, C_B themselves
+    hipLaunchKernelGGL(csym_residual_kernel<true>, grid, dim3(kResRows), smem, st, rows, ldh, ks,
+                       static_cast<int>(d_pad), static_cast<int>(s0), static_cast<int>(n_rows), rb, cb, sig_u,
+                       static_cast<int>(na), reinterpret_cast<long long*>(acc));
+  } else {
+    hipLaunchKernelGGL(csym_scan_kernel, dim3(static_cast<unsigned>(ceil_div(d_pad, 64))), dim3(64 * kScanWaves), 0,
+                       st, sig_u, static_cast<int>(na), static_cast<int>(d_pad), static_cast<int>(s0),
+                       static_cast<int>(s0 + ns), rb, cb);
+    DAL_RETURN_IF_LAUNCH_FAILED();
+    hipLaunchKernelGGL(csym_residual_kernel<false>, grid, dim3(kResRows), smem, st, rows, ldh, ks,
+                       static_cast<int>(d_pad), static_cast<int>(s0), static_cast<int>(n_rows), rb, cb, sig_u,
+                       static_cast<int>(na), reinterpret_cast<long long*>(acc));
+  }
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
 }
