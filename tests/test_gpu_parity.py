@@ -63,12 +63,15 @@ def test_zero_norm_row_raises(cuda):
         dw.information_density(X, device=cuda)
 
 
-@pytest.mark.parametrize("n,d", [(700, 30), (1000, 64), (513, 128), (300, 200)])
+# (530_001, 256): 2,071 chunks x 4 feature groups = the one-wave-per-(chunk,
+# 64 features) kernel of dal_canon_colsum_partials (>= 8,192 waves); the
+# others run its block kernel.  Excluded rows at chunk edges.
+@pytest.mark.parametrize("n,d", [(700, 30), (1000, 64), (513, 128), (300, 200), (530_001, 256)])
 def test_canonical_colsum_bit_exact(cuda, n, d):
     from dal.engine import PoolState
 
     X = O.synthetic_pool(n, d, seed=n)
-    E = [0, 1, 2, n - 1]
+    E = sorted({0, 1, 2, n - 1} | {e for e in (255, 256, 511) if e < n})
     st = PoolState(X, excluded=E, device=cuda)
     U = O.l2_normalize(X)
     ref = O.column_sum_canonical(U, O.exclusion_mask(n, E))
@@ -112,6 +115,33 @@ def test_gram_density_within_bound(cuda, n, d, dist, gram):
     # accuracy bar of the north star: 1e-5 relative (signed data: relative to sum |S_ij|)
     scale = np.abs(O.l2_normalize(X) @ O.l2_normalize(X)[ok].T).sum(axis=1)[ok]
     assert (err / scale).max() <= DENSITY_RTOL
+
+
+def test_gram_residual_scan_path(cuda):
+    """600,000 x 64: 1,172 super blocks x 64 features exceed the fused
+    residual's limit (65,536), so dal_gram_sym_residual runs its scan launch
+    (the fused form is covered by the smaller shapes above): the density
+    against the split operand's own fp64 row sums (only the MFMA accumulation
+    error remains) and against the canonical density within the bound."""
+    from dal import _lib
+    from dal.engine import PoolState
+
+    n, d = 600_000, 64
+    X = O.synthetic_pool(n, d, seed=11)
+    E = list(range(10))
+    st = PoolState(X, excluded=E, device=cuda, gram="sym")
+    assert (st.nb_active() // 2) * st.d_pad > 65_536
+    got = _np(st.density())
+    sp = _np(st.gram_operand()).view(np.float16).astype(np.float64)
+    ut = ((sp[:n, :d] + sp[:n, d:]) * 2.0**-12)
+    keep = np.ones(n, bool)
+    keep[E] = False
+    d_split = ut @ ut[keep].sum(axis=0)
+    ok = keep
+    assert np.abs(got[ok] - d_split[ok]).max() <= 1e-6 * (n - len(E))
+    ref = O.density_canonical(X, E)
+    bound = _lib.load().dal_density_error_bound_sym(n - len(E))
+    assert np.abs(got[ok] - ref[ok]).max() <= bound
 
 
 @pytest.mark.parametrize("d", [7, 30, 64, 65, 200, 500])
