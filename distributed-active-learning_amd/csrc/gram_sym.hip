@@ -914,7 +914,7 @@ int launch_csym(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint16
 }
 
 struct ResidualLayout {
-  size_t sig_u, sig_l, rb, cb, total;  // (sig_l: kept in the layout, unused since the closed-form column sums)
+  size_t sig_u, rb, cb, total;
 };
 ResidualLayout residual_layout(int64_t ns_active, int64_t n_srb, int64_t d_pad) {
   ResidualLayout L{};
@@ -925,7 +925,6 @@ ResidualLayout residual_layout(int64_t ns_active, int64_t n_srb, int64_t d_pad) 
     return at;
   };
   L.sig_u = take(static_cast<size_t>(ns_active * d_pad) * 8);
-  L.sig_l = take(static_cast<size_t>(ns_active * d_pad) * 8);
   L.rb = take(static_cast<size_t>(n_srb * d_pad) * 8);
   L.cb = take(static_cast<size_t>(n_srb * d_pad) * 8);
   L.total = o;

@@ -59,7 +59,8 @@ def test_host_helpers():
         assert abs(got - expect(chain, 100000)) <= 1e-12 * got, (d_pad, got)
     assert lib.dal_density_error_bound_sym_d(100000, 0) == bsym
     assert lib.dal_density_error_bound_sym_d(100000, 32) < bsym
-    assert lib.dal_gram_sym_residual_workspace_bytes(392, 392, 64) == 2 * 196 * 64 * 8 + 2 * 196 * 64 * 8
+    # sigma~ per super block, then R_B and C_B per requested super block
+    assert lib.dal_gram_sym_residual_workspace_bytes(392, 392, 64) == 196 * 64 * 8 + 2 * 196 * 64 * 8
     assert lib.dal_gram_sym_residual_workspace_bytes(0, 2, 64) == 0
     assert lib.dal_split_f16_halves(512, 64) == 512 * 128
     assert lib.dal_topk_workspace_bytes(1 << 21, 1000) > 0
