@@ -465,18 +465,42 @@ __global__ __launch_bounds__(NW * 64) void forest_blocked_kernel(ForestArgs A, c
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (A.hooks.status_reset && blockIdx.x == 0 && tid == 0) *A.hooks.status_reset = 0;
   for (int w = tid; w < nw; w += NT) bits[w] = 0u;
-  for (int e = tid; e < A.n_trees * n_leaf; e += NT) ls[e] = A.leaf[e];
+  // the forest's leaves and nodes, kSetupBatch loads per thread in flight at
+  // once (a load-then-use loop waits one memory latency per element)
+  constexpr int kSetupBatch = 8;
+  for (int e0 = tid; e0 < A.n_trees * n_leaf; e0 += kSetupBatch * NT) {
+    uint8_t b[kSetupBatch];
+#pragma unroll
+    for (int j = 0; j < kSetupBatch; ++j) b[j] = e0 + j * NT < A.n_trees * n_leaf ? A.leaf[e0 + j * NT] : 0;
+#pragma unroll
+    for (int j = 0; j < kSetupBatch; ++j)
+      if (e0 + j * NT < A.n_trees * n_leaf) ls[e0 + j * NT] = b[j];
+  }
   __syncthreads();
-  if (nw <= 2 && nn >= 2 * NT) {  // (block-uniform) d <= 64 and many nodes: the bitmap's words
-                                  // OR-reduced per wave, one atomic each
-    unsigned m0 = 0u, m1 = 0u;
-    for (int e = tid; e < nn; e += NT) {
-      int2 q = A.inner[e];
-      q.x = q.x < 0 ? 0 : q.x >= A.d ? A.d - 1 : q.x;  // (a valid forest tests features < d)
-      fs[e] = q;
-      m0 |= q.x < 32 ? 1u << q.x : 0u;
-      m1 |= q.x >= 32 ? 1u << (q.x - 32) : 0u;
+  // d <= 64 and many nodes: the bitmap's words OR-reduced per wave, one
+  // atomic each (same-word LDS atomics serialise: 1,500 at config 3, 42.5 ->
+  // 39.0 us; with 150 nodes (T = 10) the reduction cost more than it saved)
+  const bool wave_or = nw <= 2 && nn >= 2 * NT;  // (block-uniform)
+  unsigned m0 = 0u, m1 = 0u;
+  for (int e0 = tid; e0 < nn; e0 += kSetupBatch * NT) {
+    int2 q[kSetupBatch];
+#pragma unroll
+    for (int j = 0; j < kSetupBatch; ++j) q[j] = e0 + j * NT < nn ? A.inner[e0 + j * NT] : int2{0, 0};
+#pragma unroll
+    for (int j = 0; j < kSetupBatch; ++j) {
+      const int e = e0 + j * NT;
+      if (e >= nn) break;
+      q[j].x = q[j].x < 0 ? 0 : q[j].x >= A.d ? A.d - 1 : q[j].x;  // (a valid forest tests features < d)
+      fs[e] = q[j];
+      if (wave_or) {
+        m0 |= q[j].x < 32 ? 1u << q[j].x : 0u;
+        m1 |= q[j].x >= 32 ? 1u << (q[j].x - 32) : 0u;
+      } else {
+        atomicOr(&bits[q[j].x >> 5], 1u << (q[j].x & 31));
+      }
     }
+  }
+  if (wave_or) {
     for (int o = 32; o > 0; o >>= 1) {
       m0 |= __shfl_xor(m0, o);
       m1 |= __shfl_xor(m1, o);
@@ -484,14 +508,6 @@ __global__ __launch_bounds__(NW * 64) void forest_blocked_kernel(ForestArgs A, c
     if (lane == 0) {
       if (m0) atomicOr(&bits[0], m0);
       if (m1) atomicOr(&bits[1], m1);
-    }
-  } else {  // (same-word LDS atomics serialise: 1,500 at config 3, 42.1 -> 39.3 us above; with
-            // 150 nodes (T = 10) the reduction costs more than it saves, 9.1 -> 10.0 us)
-    for (int e = tid; e < nn; e += NT) {
-      int2 q = A.inner[e];
-      q.x = q.x < 0 ? 0 : q.x >= A.d ? A.d - 1 : q.x;
-      fs[e] = q;
-      atomicOr(&bits[q.x >> 5], 1u << (q.x & 31));
     }
   }
   __syncthreads();
