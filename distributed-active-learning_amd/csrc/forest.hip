@@ -70,17 +70,23 @@ struct ForestArgs {
 };
 
 
+// beta != 1 calls out of line: inlined, pow's registers counted against every
+// score kernel's occupancy although beta == 1 in the common case, where no
+// call is made (the blocked kernel 101 -> 74 VGPRs, 4 -> 6 waves per SIMD).
+__device__ __attribute__((noinline)) double density_pow_general(double d, double beta) { return pow(d, beta); }
 __device__ __forceinline__ double density_pow(double d, double beta) {
-  return beta == 1.0 ? d : pow(d, beta);
+  return beta == 1.0 ? d : density_pow_general(d, beta);
 }
 
 // |d^beta - d'^beta| bound for |d - d'| <= derr.
-__device__ __forceinline__ double density_pow_err(double d, double derr, double beta) {
-  if (beta == 1.0) return derr;
+__device__ __attribute__((noinline)) double density_pow_err_general(double d, double derr, double beta) {
   const double p = pow(fabs(d), beta);
   const double hi = pow(fabs(d) + derr, beta);
   const double lo = pow(fmax(fabs(d) - derr, 0.0), beta);
   return fmax(fabs(hi - p), fabs(p - lo)) * (1.0 + 1e-12) + fabs(p) * 1e-14;
+}
+__device__ __forceinline__ double density_pow_err(double d, double derr, double beta) {
+  return beta == 1.0 ? derr : density_pow_err_general(d, derr, beta);
 }
 
 // A row's flags: row_flags[row], or (warm-step plan) the pool's base flags
@@ -582,6 +588,9 @@ namespace {
 // and a 100-tree forest): 2M x 256 x 100 469.7 -> 437.4 us, while 8 waves
 // where four-wave blocks fit three or more per CU were slower (config 4 at
 // T = 10 206 -> 234 us, config 3 41.8 -> 45.0 us).
+#ifndef DAL_FOREST_BLOCKED_PER_CU
+#define DAL_FOREST_BLOCKED_PER_CU 5
+#endif
 constexpr int kBlockedWaves = 4;
 constexpr int kBlockedWavesWide = 8;
 #ifndef DAL_FOREST_BLOCKED_MAX_RUNS
@@ -676,6 +685,11 @@ int forest_score_launch(const float* x, const float* xb, int64_t n, int64_t d, i
         hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(smem)) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, nw * 64, smem) != hipSuccess)
       return DAL_ERR_HIP;
+    // at most DAL_FOREST_BLOCKED_PER_CU blocks per CU: every block stages the
+    // forest once, so more, shorter-lived blocks pay that setup more often
+    // (config 3 at 6 blocks per CU 37.0 us, at 5 35.5, at 4 -- the VGPR limit
+    // before pow went out of line -- 37.8)
+    if (per_cu > DAL_FOREST_BLOCKED_PER_CU) per_cu = DAL_FOREST_BLOCKED_PER_CU;
     if (per_cu < 1) per_cu = 1;
     const int64_t grid = tiles < static_cast<int64_t>(cus) * per_cu ? tiles : static_cast<int64_t>(cus) * per_cu;
     if (wide)
