@@ -93,6 +93,30 @@ def test_blocked_forest_degenerate_feature_sets(cuda, feature):
     _same(a, b)
 
 
+@pytest.mark.parametrize("d", [30, 33, 64])
+@pytest.mark.parametrize("feature", ["random", "first", "last", "ends"])
+def test_blocked_forest_small_d_many_nodes(cuda, d, feature):
+    """d <= 64 and >= 512 nodes (T = 100): the block setup ORs the feature
+    bitmap's one or two words per wave (forest.hip, wave_or) -- every node on
+    feature 0, on d - 1 (the second word when d > 32), on the two ends, or the
+    synthetic forest's random features."""
+    from dal.forest import Forest
+
+    n = 7_001
+    X = O.synthetic_pool(n, d, seed=d)
+    F = Forest.synthetic(100, 4, d, seed=13)
+    inner = F.inner.copy()
+    if feature == "first":
+        inner[..., 0] = 0
+    elif feature == "last":
+        inner[..., 0] = d - 1
+    elif feature == "ends":
+        inner[..., 0] = np.where(np.arange(inner.shape[1]) % 2 == 0, 0, d - 1)[None, :]
+    G = Forest(inner=inner, leaf=F.leaf.copy(), depth=F.depth)
+    _, a, b = _forest_score_pair(cuda, X, G, "fixed")
+    _same(a, b)
+
+
 def test_blocked_forest_ragged_trees(cuda):
     """Ragged trees padded into the depth-2 heap (Forest.from_nodes: padding
     nodes test feature 0 against +inf) through the blocked kernel."""
