@@ -662,43 +662,57 @@ __global__ __launch_bounds__(kResRows) void csym_residual_kernel(const uint16_t*
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kResRows;  // (a multiple of 256: one super block)
   const int64_t B = r0 / kSB;                                       // relative to b0
   if constexpr (kFused) {
-    __shared__ long long red[4][kResRows];
+    // feature pairs (16-B loads of sigma~): 256 / (d_pad / 2) thread groups
+    // over the super blocks -- 8 (d_pad 64) or 16 (d_pad 32)
+    __shared__ long long red[8][kResRows];
     const int qB = b0 + static_cast<int>(B);  // this block's super block
-    const int G = kResRows / d_pad, f = tid % d_pad, grp = tid / d_pad;
-    long long pe = 0, po = 0, te = 0, to = 0;  // per class: sums over super blocks < qB, and totals
+    const int hp = d_pad / 2, G = kResRows / hp, fp = tid % hp, grp = tid / hp;
+    long long pe[2] = {}, po[2] = {}, te[2] = {}, to[2] = {};  // per class: sums over super blocks < qB, and totals
+    const longlong2* su2 = reinterpret_cast<const longlong2*>(sig_u);
     for (int qb = grp; qb < ns; qb += kScanBatch * G) {
-      long long v[kScanBatch];
+      longlong2 v[kScanBatch];
 #pragma unroll
       for (int j = 0; j < kScanBatch; ++j) {
         const int q = qb + j * G;
-        v[j] = q < ns ? sig_u[static_cast<int64_t>(q) * d_pad + f] : 0;
+        v[j] = q < ns ? su2[static_cast<int64_t>(q) * hp + fp] : longlong2{0, 0};
       }
 #pragma unroll
       for (int j = 0; j < kScanBatch; ++j) {
         const int q = qb + j * G;
         const bool odd = q & 1, before = q < qB;
-        te += odd ? 0 : v[j];
-        to += odd ? v[j] : 0;
-        pe += before && !odd ? v[j] : 0;
-        po += before && odd ? v[j] : 0;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const long long x = c ? v[j].y : v[j].x;
+          te[c] += odd ? 0 : x;
+          to[c] += odd ? x : 0;
+          pe[c] += before && !odd ? x : 0;
+          po[c] += before && odd ? x : 0;
+        }
       }
     }
-    red[0][tid] = pe;
-    red[1][tid] = po;
-    red[2][tid] = te;
-    red[3][tid] = to;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      red[4 * c][tid] = pe[c];
+      red[4 * c + 1][tid] = po[c];
+      red[4 * c + 2][tid] = te[c];
+      red[4 * c + 3][tid] = to[c];
+    }
     __syncthreads();
-    if (tid < d_pad) {
-      long long eue = 0, euo = 0, tue = 0, tuo = 0;
-      for (int g = 0; g < G; ++g) {
-        eue += red[0][g * d_pad + tid];
-        euo += red[1][g * d_pad + tid];
-        tue += red[2][g * d_pad + tid];
-        tuo += red[3][g * d_pad + tid];
+    if (tid < hp) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        long long eue = 0, euo = 0, tue = 0, tuo = 0;
+        for (int g = 0; g < G; ++g) {
+          eue += red[4 * c][g * hp + tid];
+          euo += red[4 * c + 1][g * hp + tid];
+          tue += red[4 * c + 2][g * hp + tid];
+          tuo += red[4 * c + 3][g * hp + tid];
+        }
+        const bool odd = qB & 1;  // R_B, C_B as in csym_scan_kernel
+        const int f = 2 * tid + c;
+        rc[f] = static_cast<double>(odd ? (tuo - euo + eue) : (tue - eue + euo));
+        rc[d_pad + f] = static_cast<double>(odd ? (euo + tue - eue) : (eue + tuo - euo));
       }
-      const bool odd = qB & 1;  // R_B, C_B as in csym_scan_kernel
-      rc[tid] = static_cast<double>(odd ? (tuo - euo + eue) : (tue - eue + euo));
-      rc[d_pad + tid] = static_cast<double>(odd ? (euo + tue - eue) : (eue + tuo - euo));
     }
   } else {
     for (int f = tid; f < d_pad; f += kResRows) {
