@@ -21,6 +21,9 @@ selection of the exact separable density path on the same pool.
 With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py launches its
 own N ranks (child processes, 127.0.0.1 rendezvous) before any GPU call and
 re-prints rank 0's output, headline last; under torchrun it runs as one rank.
+DAL_BENCH_SHARDED=1 with --gpus 1 runs the same step through the sharded path
+(dal/parallel.py) on a one-rank RCCL group: the multi-GPU path's fixed cost at
+N = 1, beside the single-GPU headline.
 
 Output (rank 0): one compact JSON line per extra workload ({"extra": label,
 ...}, <= 1 KB each), then the compact headline as the LAST stdout line
@@ -74,6 +77,9 @@ CONFIGS = {
               n=8_000_000, d=128, k=1000, m=1024, dist="uniform", mode="div"),
 }
 N_EXCLUDED = 10
+# DAL_BENCH_SHARDED=1: run --gpus 1 through dal/parallel.py on a one-rank
+# process group (RCCL; DAL_BENCH_BACKEND=gloo for the host-staged rehearsal)
+SHARDED = os.environ.get("DAL_BENCH_SHARDED", "") == "1"
 # default extras beside the config-4 headline: configs 2, 3, 5
 # and config 4 at T = 100 and at k = 1000
 DEFAULT_EXTRA = "2,3,5,4:T100,4:k1000"
@@ -455,8 +461,65 @@ def cached_pool(n, d, dist, lo, hi, dev):
     return _POOLS[key]
 
 
+def time_step_select(state, forest, flags, dens, lut_dev, k: int, beta: float, xb=None):
+    """PoolState.step_select_probe: the selection launch of the fused step
+    (what dal_dw_step and the warm plan run after the score kernel folded the
+    row-group minima) timed on its own.  One full dal_dw_step keeps the minima
+    (DAL_STEP_KEEP_GROUPS), then EVENT_REPEAT DAL_STEP_SELECT_ONLY calls run
+    between two events (behind a GPU spin), then one more clears them.  The
+    selections must equal the step's; the events go to state.step_select_events."""
+    import torch
+
+    from dal import _lib
+    from dal._lib import DAL_STEP_KEEP_GROUPS, DAL_STEP_SELECT_ONLY, DAL_STEP_WS_CLEAN, call
+    from dal.engine import _fprep, _ptr, _stream, candidate_cap, density_error, level1_passes, workspace
+
+    lib = _lib.load()
+    n, dev = state.n, state.device
+    inner, leaf = forest.device(dev)
+    norm64, colsum = state.norms(), state.colsum()
+    base = candidate_cap(n, k) if state.cap_base is None else max(int(k), int(state.cap_base))
+    cap = int(min(n, base * state.cap_scale))
+    passes = level1_passes(state, n, k, cap)
+    if passes == 0:
+        return
+    wsb = int(lib.dal_dw_step_workspace_bytes(n, k, cap))
+    ws, wsp = workspace(wsb, dev)
+    ws.zero_()
+    bufs = [torch.empty(n, dtype=t, device=dev) for t in (torch.int32, torch.float64, torch.int64, torch.int64)]
+    outs = [(torch.empty(k, dtype=torch.int64, device=dev), torch.empty(k, dtype=torch.float64, device=dev))
+            for _ in range(2)]
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def step(flags_bits, out):
+        call("dal_dw_step", _ptr(state.x), 0 if xb is None else _ptr(xb), _fprep(forest, state, xb), n, state.d,
+             state.d, _ptr(inner),
+             _ptr(leaf), forest.n_trees, forest.depth, _ptr(lut_dev), _ptr(dens), float(density_error(state)),
+             _ptr(flags), float(beta),
+             state.row_base, _ptr(norm64), _ptr(colsum), k, cap, passes, flags_bits, wsp, wsb,
+             *[_ptr(b) for b in bufs], _ptr(out[0]), _ptr(out[1]), 0, _ptr(status), 0, _stream(dev))
+
+    step(DAL_STEP_WS_CLEAN | DAL_STEP_KEEP_GROUPS, outs[0])
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    if state.event_lead_cycles:
+        torch.cuda._sleep(state.event_lead_cycles)
+    ev[0].record()
+    for _ in range(state.event_repeat):
+        step(DAL_STEP_WS_CLEAN | DAL_STEP_KEEP_GROUPS | DAL_STEP_SELECT_ONLY, outs[1])
+    ev[1].record()
+    step(DAL_STEP_WS_CLEAN | DAL_STEP_SELECT_ONLY, outs[1])  # the last one clears the minima
+    if int(status.item()) != 0 or not (torch.equal(outs[0][0], outs[1][0]) and
+                                      torch.equal(outs[0][1].view(torch.int64), outs[1][1].view(torch.int64))):
+        return  # (an overflow or a mismatch: no timing recorded)
+    state.step_select_events.append(ev)
+
+
 def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, backend, cpu=True, cfg=None):
-    """Density-weighted selection on one config; returns the JSON dict."""
+    """Density-weighted selection on one config; returns the JSON dict.
+
+    The step runs through the sharded path (dal/parallel.py) when world > 1,
+    or at world 1 when DAL_BENCH_SHARDED=1 (an RCCL group of one rank: the
+    multi-GPU path's fixed cost on record beside the single-GPU headline)."""
     import torch
 
     from dal import engine, parallel
@@ -472,11 +535,13 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
     n_scored = n - N_EXCLUDED
     tdev = dev if backend == "nccl" else "cpu"
 
+    sharded = world > 1 or SHARDED
+
     def barrier():
         if world > 1:
             dist.barrier()
 
-    if world > 1:
+    if sharded:
         sel = parallel.ShardedSelector(x, n, rank, world, excluded=excluded, device=dev)
         comm = parallel.TorchComm()
         state = sel.state
@@ -497,7 +562,7 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
     for _ in range(warmup):
         step()
     state.gram_events, state.residual_events = [], []
-    if world > 1:
+    if sharded:
         sel.exchange_events = []
     elapsed, (idx_g, sc_g) = _timed(step, steps, barrier)
     events, state.gram_events = state.gram_events, None
@@ -507,7 +572,7 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
     resid_ms = sum(a.elapsed_time(b) for a, b in res_events) / max(steps, 1)
     gram_ms = sum(a.elapsed_time(b) for a, b in events) / max(steps, 1) + resid_ms
     ranks = None
-    if world > 1:  # the density exchange's collectives, per step, and their max over ranks
+    if sharded:  # the density exchange's collectives, per step, and their max over ranks
         xev, sel.exchange_events = sel.exchange_events, None
         ag_ms = sum(a.elapsed_time(b) for nm, a, b in xev if nm == "all_gather") / max(steps, 1)
         gram_min = -_max_over_ranks([-gram_ms], world, dist, tdev)[0]
@@ -551,13 +616,14 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
         step()
         # per-kernel HIP-event timing of K2 / K3 (eager launches, events on the launch stream)
         state.forest_events, state.select_events = [], []
-        state.step_select_events = [] if world == 1 else None
+        state.step_select_events = [] if not sharded else None
+        state.step_select_probe = time_step_select if not sharded else None
         state.event_lead_cycles, state.event_repeat = EVENT_LEAD_CYCLES, EVENT_REPEAT
         for _ in range(min(warm_steps, 20)):
             step(cold=False)
         torch.cuda.synchronize()
         fev, sev, ssev = state.forest_events, state.select_events, state.step_select_events
-        state.forest_events = state.select_events = state.step_select_events = None
+        state.forest_events = state.select_events = state.step_select_events = state.step_select_probe = None
         state.event_lead_cycles, state.event_repeat = 0, 1
         if fev:
             forest_ms = sum(a.elapsed_time(b) for a, b in fev) / len(fev) / EVENT_REPEAT
@@ -588,7 +654,7 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
 
     # k-th boundary gap: the (k+1)-best score from the exact path, beside the
     # observed Gram error (the exact re-rank makes the selection independent of it)
-    if world > 1:
+    if sharded:
         _, sc_k1 = parallel.select(sel, comm, unl, forest, k + 1, mode="dw", density_mode="separable")
     else:
         sc_k1 = engine.density_step(state, unl, forest, k + 1, mode="separable").selected_scores
@@ -617,12 +683,14 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
         "data": DATA_NOTE,
         "config": {"workload": cfg["workload"], "pool_rows": n, "features": d, "trees": cfg["trees"],
                    "depth": cfg["depth"], "k": k, "excluded": N_EXCLUDED, "rows_scored": n_scored,
-                   "parallelism": f"row-shard dp{world} (RCCL all-gather)" if world > 1 else "single GPU"},
+                   "parallelism": (f"row-shard dp{world} ({'RCCL' if backend == 'nccl' else backend} all-gather)"
+                                   if sharded else "single GPU")},
         "selection_latency_ms": ms_per_step,
         "warm_selection_latency_ms": warm_ms,
         "warm_path": ("hipGraph replay (votes/score + row-group minima -> candidate search -> fp64 re-rank -> "
-                      "sort) + input refresh, one status read" if world == 1 and state.use_graphs
-                      else "eager launches"),
+                      "sort) + input refresh, one status read" if not sharded and state.use_graphs
+                      else "per-rank dal_dw_plan replay -> packed all-gather -> one-launch merge, one status read"
+                      if sharded and state.use_graphs else "eager launches"),
         "warm_rows_per_s": (n_scored / (warm_ms * 1e-3)) if warm_ms else None,
         "self_check": {"gram_selection_equals_separable_selection": same,
                        "warm_selection_equals_cold_selection": warm_same, "k": k,
@@ -663,7 +731,7 @@ def bench_dw(args, config, steps, warmup, warm_steps, world, rank, dev, dist, ba
         of = O.synthetic_forest(cfg["trees"], cfg["depth"], d, seed=1, dist=cfg["dist"])
         out["cpu_baseline"] = cpu_baseline(x_host, cfg, of, budget_s=cpu if isinstance(cpu, float) else 12.0)
     del state, x
-    if world > 1:
+    if sharded:
         del sel
     torch.cuda.empty_cache()
     return out
@@ -729,11 +797,12 @@ def bench_div(args, steps, warmup, world, rank, dev, dist, backend, cpu=12.0):
     lab_host = host_pool(0, m, d, cfg["dist"])
     lab = upload(lab_host, dev).to(torch.bfloat16)
     cand = torch.arange(max(lo, m), hi, device=dev, dtype=torch.int64)
-    comm = parallel.TorchComm() if world > 1 else None
+    sharded = world > 1 or SHARDED
+    comm = parallel.TorchComm() if sharded else None
     tdev = dev if backend == "nccl" else "cpu"
 
     def step():
-        if world > 1:
+        if sharded:
             return parallel.diversity_select_sharded(x, lo, lab, k, comm, candidates=cand, device=dev)
         s = diversity_select(x, None, k, candidates=cand, device=dev, labeled_rows=lab)
         return s.indices, s.selected_scores
@@ -785,7 +854,7 @@ def bench_div(args, steps, warmup, world, rank, dev, dist, backend, cpu=12.0):
         "dtype": "bf16 pool (rows rescaled by powers of two to fp16 exactly; fp16 MFMA, fp32 accumulate)",
         "data": DATA_NOTE,
         "config": {"workload": cfg["workload"], "pool_rows": n, "features": d, "labeled": m, "k": k,
-                   "parallelism": f"row-shard dp{world}" if world > 1 else "single GPU"},
+                   "parallelism": f"row-shard dp{world}" if sharded else "single GPU"},
         "roofline": {"bound": "mfma", "kernel": "dal_max_cosine_unit (bf16 pool rows power-of-two scaled to fp16 in registers, folded fp16 unit labeled rows; v_mfma_f32_16x16x32_f16, max-only epilogue)",
                      "achieved": achieved, "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / BF16_MFMA_PEAK_TFLOPS,
@@ -871,7 +940,7 @@ def headline(out: dict) -> dict:
     cfg = out.get("config") or {}
     h["config"] = {k: cfg[k] for k in ("workload", "pool_rows", "features", "trees", "k", "labeled",
                                        "parallelism") if k in cfg}
-    for k in ("world_size", "backend"):
+    for k in ("world_size", "backend", "sharded_path"):
         h[k] = out.get(k)
     h["value"], h["ms_per_step"] = _r(out.get("value"), 6), _r(out.get("ms_per_step"), 6)
     h["warm_selection_latency_ms"] = _r(out.get("warm_selection_latency_ms"))
@@ -1060,11 +1129,15 @@ def main():
     n_dev = torch.cuda.device_count()
     dev = torch.device("cuda", local_rank % max(n_dev, 1))
     torch.cuda.set_device(dev)
-    if world > 1:
+    if world > 1 or SHARDED:
+        if world == 1:  # DAL_BENCH_SHARDED=1: a one-rank group of its own
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, rank=rank, world_size=world)
 
     if main_cfg.get("mode") == "div":
         out = bench_div(args, steps, warmup, world, rank, dev, dist, backend)
@@ -1095,11 +1168,12 @@ def main():
                                                             "line's O(N^2) Gram row-sum (cpu_baseline above)")
     if world == 1 and CONFIGS[args.config].get("mode") != "div":
         out.setdefault("extra", {})["rf_train"] = bench_rf_train(dev)
-    out["world_size"] = dist.get_world_size() if world > 1 else 1
-    out["backend"] = dist.get_backend() if world > 1 else None
+    out["world_size"] = dist.get_world_size() if world > 1 or SHARDED else 1
+    out["backend"] = dist.get_backend() if world > 1 or SHARDED else None
+    out["sharded_path"] = bool(world > 1 or SHARDED)
     if rank == 0:
         emit(out, args.out)
-    if world > 1:
+    if world > 1 or SHARDED:
         dist.destroy_process_group()
 
 

@@ -13,4 +13,4 @@ extern "C" const char* dal_status_string(int status) {
   }
 }
 
-extern "C" int dal_abi_version(void) { return 9; }
+extern "C" int dal_abi_version(void) { return 10; }

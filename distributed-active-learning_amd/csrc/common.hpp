@@ -127,8 +127,10 @@ struct ForestStepHooks {
 int forest_rows_per_block(const float* x, const float* xb, int64_t d, int64_t ldx, int32_t n_trees,
                           int32_t depth);
 
-int forest_score_launch(const float* x, const float* xb, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
-                        const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
+// fprep: the forest prepared by dal_forest_prepare for this d (nullable; with
+// xb only): the blocked kernel's blocks copy it instead of building it.
+int forest_score_launch(const float* x, const float* xb, const void* fprep, int64_t n, int64_t d, int64_t ldx,
+                        const int32_t* inner, const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
                         const void* density, int density_kind, double density_err, const uint8_t* row_flags,
                         double beta, int order, int32_t* votes, double* scores, uint64_t* keys,
                         uint64_t* keys_hi, const ForestStepHooks& hooks, hipStream_t st);
@@ -136,7 +138,8 @@ int forest_score_launch(const float* x, const float* xb, int64_t n, int64_t d, i
 // dal_dw_step with the plan's publishing hooks (topk.hip, SortTail): the
 // selection is also written to *out_slot (a host-mapped word holding a device
 // address; nullable) and the final status word to *status_mirror (host-mapped).
-int dw_step_impl(const float* x, const float* xb, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
+int dw_step_impl(const float* x, const float* xb, const void* fprep, int64_t n, int64_t d, int64_t ldx,
+                 const int32_t* inner,
                  const uint8_t* leaf,
                  int32_t n_trees, int32_t depth, const double* lut, const int64_t* density_fixed, double density_err,
                  const uint8_t* row_flags, double beta, int64_t idx_base, const double* norm64, const double* colsum,

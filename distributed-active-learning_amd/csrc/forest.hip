@@ -37,14 +37,6 @@ constexpr int kTreeIlp = DAL_FOREST_ILP;  // independent tree walks in flight pe
 #ifndef DAL_FOREST_BLOCKED_ILP
 #define DAL_FOREST_BLOCKED_ILP 4  // ... in the blocked kernel
 #endif
-// Timing-only A/B (scripts/ab_build.sh -DDAL_FOREST_BITMASK=1; verdict r4 item
-// 5): depth-4 trees evaluated whole -- every wave walks one tree at a time for
-// 64 rows, reads the tree's 15 nodes at wave-uniform LDS addresses, gathers
-// and compares all 15 predicates (no dependent node-then-feature round trips),
-// then resolves the leaf from the 15-bit mask.  0 in the product.
-#ifndef DAL_FOREST_BITMASK
-#define DAL_FOREST_BITMASK 0
-#endif
 
 struct ForestArgs {
   const float* x;
@@ -148,9 +140,7 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
   const int n_leaf = 1 << A.depth;
   const int tid = threadIdx.x;
   const int64_t row0 = tile * R;
-  // bitmask form: wave w holds rows (w / tpr) * 64 + lane and trees w % tpr, +tpr, ...
-  const bool bm = DAL_FOREST_BITMASK && X_LDS && A.depth == 4 && R * tpr == NT && R % 64 == 0;
-  const bool wr = WROWS || bm;  // rows by wave lanes, trees by waves
+  constexpr bool wr = WROWS;  // rows by wave lanes, trees by waves
   const int r = wr ? (tid >> 6) / tpr * 64 + (tid & 63) : tid / tpr;
   const int sub = wr ? (tid >> 6) % tpr : tid - r * tpr;
   const int64_t row = row0 + r;
@@ -159,23 +149,7 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
   const float* xrow = X_LDS ? xs + r * xstride : A.x + (live ? row : 0) * A.ldx;
 
   int v = 0;
-  if (DAL_FOREST_BITMASK && bm) {
-    if (live) {
-      for (int t = sub; t < A.n_trees; t += tpr) {  // (wave-uniform tree)
-        const int2* nd = inner + t * 15;
-        unsigned m = 0;
-#pragma unroll
-        for (int h = 0; h < 15; ++h) {
-          const int2 q = nd[h];  // the same address in every lane: an LDS broadcast
-          m |= (xrow[q.x] <= __int_as_float(q.y) ? 1u : 0u) << h;
-        }
-        int h = 0;
-#pragma unroll
-        for (int l = 0; l < 4; ++l) h = 2 * h + 2 - static_cast<int>((m >> h) & 1u);
-        v += leaf[t * 16 + (h - 15)];
-      }
-    }
-  } else if (live) {
+  if (live) {
     int t = sub;
     for (; t + (ILP - 1) * tpr < A.n_trees; t += ILP * tpr) {
       int h[ILP];
@@ -201,7 +175,7 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
       v += leaf[t * n_leaf + (h - n_inner)];
     }
   }
-  if (wr) {  // a row's tree phases are in different waves (partial votes < 256: T <= 1020 here)
+  if constexpr (wr) {  // a row's tree phases are in different waves (partial votes < 256: T <= 1020 here)
     __shared__ uint8_t s_vote[NT];
     s_vote[sub * R + r] = static_cast<uint8_t>(v);
     __syncthreads();
@@ -319,10 +293,8 @@ __global__ __launch_bounds__(kForestThreads) void forest_score_kernel(ForestArgs
   // d + 4 (rows stay 16-B aligned, one ds_write_b128 per load, consecutive
   // lanes on consecutive banks; rows of a wave start 4 banks apart)
   const int xstride = A.d + (pad4 ? 4 : 1);
-  // (the row / tree-phase mapping of score_tile: the bitmask form's row leaders differ)
-  const bool bm = DAL_FOREST_BITMASK && X_LDS && A.depth == 4 && R * tpr == kForestThreads && R % 64 == 0;
-  const int r = bm ? (tid >> 6) / tpr * 64 + (tid & 63) : tid / tpr;
-  const int sub = bm ? (tid >> 6) % tpr : tid - r * tpr;
+  const int r = tid / tpr;  // (the row / tree-phase mapping of score_tile)
+  const int sub = tid - r * tpr;
   GroupFold fold;  // the previous tile's group fold, not yet issued (persistent kernel)
   __shared__ unsigned long long wmin[2][2][kForestWaves];
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {  // block-uniform
@@ -453,8 +425,31 @@ __global__ __launch_bounds__(256) void pool_blocked_kernel(const float* __restri
 // 64 consecutive words of a run whatever slot each lane's tree asks for --
 // no bank conflicts).  Bytes per row: 4 F_used + the epilogue's, against
 // 4 d for the row-major tile (config 4, T = 10: ~113 of 256 features).
-template <int NW>
+// PREP (ABI v10): the forest was prepared once per (forest, d) by
+// dal_forest_prepare -- feature list, remapped nodes and leaves in the LDS
+// layout below -- and every block copies that blob instead of building it
+// (the per-block bitmap, popcounts and remap are gone).
+
+// The prepared forest (dal_forest_prepare): a 16-B header {fu, bad, nn,
+// fu_max} then the payload [nodes int2 nn (feature -> slot * kBlk) | leaves u8
+// round4(T * 2^depth) | feature list u16 round2(fu_max)], zero-padded to 16 B:
+// the blocked kernel's LDS layout from its forest region on.
+struct BlockedPrepLayout {
+  int64_t nodes, leaves, used, payload, total;
+};
+__host__ __device__ inline BlockedPrepLayout blocked_prep_layout(int64_t n_trees, int32_t depth, int64_t fu_max) {
+  BlockedPrepLayout L;
+  L.nodes = n_trees * ((int64_t{1} << depth) - 1) * 8;
+  L.leaves = round_up(n_trees << depth, 4);
+  L.used = round_up(fu_max, 2) * 2;
+  L.payload = round_up(L.nodes + L.leaves + L.used, 16);
+  L.total = 16 + L.payload;
+  return L;
+}
+
+template <int NW, bool PREP>
 __global__ __launch_bounds__(NW * 64) void forest_blocked_kernel(ForestArgs A, const float* __restrict__ xb,
+                                                                 const unsigned char* __restrict__ prep,
                                                                  int fu_max, int64_t n_tiles) {
   constexpr int NT = NW * 64;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -470,6 +465,24 @@ __global__ __launch_bounds__(NW * 64) void forest_blocked_kernel(ForestArgs A, c
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (A.hooks.status_reset && blockIdx.x == 0 && tid == 0) *A.hooks.status_reset = 0;
+  int fu;
+  if constexpr (PREP) {
+    // the prepared payload -> LDS, 16 B per thread, kPrepBatch loads in flight
+    constexpr int kPrepBatch = 4;
+    const int n16 = static_cast<int>(blocked_prep_layout(A.n_trees, A.depth, fu_max).payload >> 4);
+    const uint4* src = reinterpret_cast<const uint4*>(prep + 16);
+    uint4* dst = reinterpret_cast<uint4*>(fs);
+    for (int e0 = tid; e0 < n16; e0 += kPrepBatch * NT) {
+      uint4 q[kPrepBatch];
+#pragma unroll
+      for (int j = 0; j < kPrepBatch; ++j) q[j] = e0 + j * NT < n16 ? src[e0 + j * NT] : uint4{};
+#pragma unroll
+      for (int j = 0; j < kPrepBatch; ++j)
+        if (e0 + j * NT < n16) dst[e0 + j * NT] = q[j];
+    }
+    fu = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const int*>(prep));
+    __syncthreads();
+  } else {
   for (int w = tid; w < nw; w += NT) bits[w] = 0u;
   // the forest's leaves and nodes, kSetupBatch loads per thread in flight at
   // once (a load-then-use loop waits one memory latency per element)
@@ -527,8 +540,9 @@ __global__ __launch_bounds__(NW * 64) void forest_blocked_kernel(ForestArgs A, c
   for (int f = tid; f < A.d; f += NT)
     if ((bits[f >> 5] >> (f & 31)) & 1u) used[slot(f)] = static_cast<uint16_t>(f);  // d <= 2^16 here
   for (int e = tid; e < nn; e += NT) fs[e].x = slot(fs[e].x) * kBlk;
-  const int fu = pre[nw - 1] + __popc(bits[nw - 1]);  // <= fu_max
+  fu = pre[nw - 1] + __popc(bits[nw - 1]);  // <= fu_max
   __syncthreads();
+  }
   const int n_ins = (fu + 3) >> 2;  // DMA instructions per tile (4 runs each)
   typedef __attribute__((address_space(3))) float lds_float;
   GroupFold fold;
@@ -566,6 +580,66 @@ __global__ __launch_bounds__(NW * 64) void forest_blocked_kernel(ForestArgs A, c
     __syncthreads();  // every wave done with the tile before the next one is staged
   }
   if (tid == 0) issue_fold<NW>(A, fold, wmin);
+}
+
+// dal_forest_prepare: one block builds the prepared forest (the blocked
+// kernel's per-block setup, done once): the distinct features (bitmap,
+// prefix popcounts), every node's feature as its slot * kBlk, the leaves, the
+// feature list.  A feature outside [0, d) is clamped as the unprepared kernel
+// does and counted in the header's ``bad`` word.
+constexpr int kPrepThreads = 1024;
+__global__ __launch_bounds__(kPrepThreads) void forest_prepare_kernel(const int2* __restrict__ inner,
+                                                                     const uint8_t* __restrict__ leaf, int n_trees,
+                                                                     int depth, int d, int fu_max,
+                                                                     unsigned char* __restrict__ prep) {
+  extern __shared__ unsigned pbits[];  // [nw] bitmap | [nw] prefix counts
+  const int n_inner = (1 << depth) - 1, n_leaf = 1 << depth;
+  const int nn = n_trees * n_inner, nw = (d + 31) >> 5, tid = threadIdx.x;
+  int* ppre = reinterpret_cast<int*>(pbits + nw);
+  __shared__ int s_bad;
+  if (tid == 0) s_bad = 0;
+  for (int w = tid; w < nw; w += kPrepThreads) pbits[w] = 0u;
+  __syncthreads();
+  int bad = 0;
+  for (int e = tid; e < nn; e += kPrepThreads) {
+    const int f = inner[e].x;
+    bad += f < 0 || f >= d;
+    const int fc = f < 0 ? 0 : f >= d ? d - 1 : f;
+    atomicOr(&pbits[fc >> 5], 1u << (fc & 31));
+  }
+  if (bad) atomicAdd(&s_bad, bad);
+  __syncthreads();
+  for (int w = tid; w < nw; w += kPrepThreads) {
+    int c = 0;
+    for (int j = 0; j < w; ++j) c += __popc(pbits[j]);
+    ppre[w] = c;
+  }
+  __syncthreads();
+  auto slot = [&](int f) { return ppre[f >> 5] + __popc(pbits[f >> 5] & ((1u << (f & 31)) - 1u)); };
+  const BlockedPrepLayout L = blocked_prep_layout(n_trees, depth, fu_max);
+  unsigned char* pay = prep + 16;
+  int2* nodes = reinterpret_cast<int2*>(pay);
+  uint8_t* leaves = pay + L.nodes;
+  uint16_t* used = reinterpret_cast<uint16_t*>(pay + L.nodes + L.leaves);
+  for (int e = tid; e < nn; e += kPrepThreads) {
+    int2 q = inner[e];
+    q.x = slot(q.x < 0 ? 0 : q.x >= d ? d - 1 : q.x) * kBlk;
+    nodes[e] = q;
+  }
+  for (int64_t e = tid; e < L.leaves; e += kPrepThreads) leaves[e] = e < int64_t{n_trees} * n_leaf ? leaf[e] : 0;
+  const int fu = ppre[nw - 1] + __popc(pbits[nw - 1]);
+  for (int sl = tid; sl < static_cast<int>(L.used / 2); sl += kPrepThreads) used[sl] = 0;
+  __syncthreads();  // (the padding zeros before the list entries over them)
+  for (int f = tid; f < d; f += kPrepThreads)
+    if ((pbits[f >> 5] >> (f & 31)) & 1u) used[slot(f)] = static_cast<uint16_t>(f);
+  for (int64_t b = L.nodes + L.leaves + L.used + tid; b < L.payload; b += kPrepThreads) pay[b] = 0;
+  if (tid == 0) {
+    int* hdr = reinterpret_cast<int*>(prep);
+    hdr[0] = fu;
+    hdr[1] = s_bad;
+    hdr[2] = nn;
+    hdr[3] = fu_max;
+  }
 }
 
 }  // namespace
@@ -654,12 +728,13 @@ int forest_rows_per_block(const float* x, const float* xb, int64_t d, int64_t ld
   return forest_tiling(x, d, ldx, n_trees).R;
 }
 
-int forest_score_launch(const float* x, const float* xb, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
-                        const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
+int forest_score_launch(const float* x, const float* xb, const void* fprep, int64_t n, int64_t d, int64_t ldx,
+                        const int32_t* inner, const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
                         const void* density, int density_kind, double density_err, const uint8_t* row_flags,
                         double beta, int order, int32_t* votes, double* scores, uint64_t* keys,
                         uint64_t* keys_hi, const ForestStepHooks& hooks_in, hipStream_t st) {
   if (!x || !inner || !leaf || !lut || !votes || !scores || !keys) return DAL_ERR_ARG;
+  if (fprep && reinterpret_cast<uintptr_t>(fprep) % 16 != 0) return DAL_ERR_ARG;
   if (order != DAL_ASCENDING && order != DAL_DESCENDING) return DAL_ERR_ARG;
   if (density_kind < 0 || density_kind > 2 || (density_kind && !density)) return DAL_ERR_ARG;
   if (n < 0 || d < 1 || ldx < d || n_trees < 1) return DAL_ERR_SHAPE;
@@ -674,11 +749,17 @@ int forest_score_launch(const float* x, const float* xb, int64_t n, int64_t d, i
     ForestArgs A{x, n, static_cast<int>(d), ldx, reinterpret_cast<const int2*>(inner), leaf, n_trees,
                  depth, lut, density_kind ? density : nullptr, density_kind, density_err, row_flags, beta,
                  order, votes, scores, keys, keys_hi, hooks_in};
-    const size_t smem = blocked_smem(fu_max, d, n_trees, depth);
+    const bool pr = fprep != nullptr;
+    // prepared: the forest region holds the payload only (no bitmap / prefix counts)
+    const size_t smem = pr ? static_cast<size_t>(fu_max) * kBlk * 4 +
+                                 static_cast<size_t>(blocked_prep_layout(n_trees, depth, fu_max).payload)
+                           : blocked_smem(fu_max, d, n_trees, depth);
     const bool wide = smem > (160u << 10) / 3;  // at most two blocks per CU by LDS: 8-wave blocks
     const int nw = wide ? kBlockedWavesWide : kBlockedWaves;
-    const void* fn = wide ? reinterpret_cast<const void*>(forest_blocked_kernel<kBlockedWavesWide>)
-                          : reinterpret_cast<const void*>(forest_blocked_kernel<kBlockedWaves>);
+    const void* fn = wide ? (pr ? reinterpret_cast<const void*>(forest_blocked_kernel<kBlockedWavesWide, true>)
+                                : reinterpret_cast<const void*>(forest_blocked_kernel<kBlockedWavesWide, false>))
+                          : (pr ? reinterpret_cast<const void*>(forest_blocked_kernel<kBlockedWaves, true>)
+                                : reinterpret_cast<const void*>(forest_blocked_kernel<kBlockedWaves, false>));
     int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1 ||
@@ -692,12 +773,15 @@ int forest_score_launch(const float* x, const float* xb, int64_t n, int64_t d, i
     if (per_cu > DAL_FOREST_BLOCKED_PER_CU) per_cu = DAL_FOREST_BLOCKED_PER_CU;
     if (per_cu < 1) per_cu = 1;
     const int64_t grid = tiles < static_cast<int64_t>(cus) * per_cu ? tiles : static_cast<int64_t>(cus) * per_cu;
-    if (wide)
-      hipLaunchKernelGGL(forest_blocked_kernel<kBlockedWavesWide>, dim3(static_cast<unsigned>(grid)), dim3(nw * 64),
-                         smem, st, A, xb, fu_max, tiles);
-    else
-      hipLaunchKernelGGL(forest_blocked_kernel<kBlockedWaves>, dim3(static_cast<unsigned>(grid)), dim3(nw * 64),
-                         smem, st, A, xb, fu_max, tiles);
+    const unsigned char* pb = static_cast<const unsigned char*>(fprep);
+#define DAL_BLOCKED_LAUNCH(W, P)                                                                          \
+  hipLaunchKernelGGL((forest_blocked_kernel<W, P>), dim3(static_cast<unsigned>(grid)), dim3(nw * 64), smem, st, A, \
+                     xb, pb, fu_max, tiles)
+    if (wide && pr) DAL_BLOCKED_LAUNCH(kBlockedWavesWide, true);
+    else if (wide) DAL_BLOCKED_LAUNCH(kBlockedWavesWide, false);
+    else if (pr) DAL_BLOCKED_LAUNCH(kBlockedWaves, true);
+    else DAL_BLOCKED_LAUNCH(kBlockedWaves, false);
+#undef DAL_BLOCKED_LAUNCH
     DAL_RETURN_IF_LAUNCH_FAILED();
     return DAL_OK;
   }
@@ -771,7 +855,7 @@ extern "C" int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ld
                                 const uint8_t* row_flags,
                                 double beta, int order, int32_t* votes, double* scores, uint64_t* keys,
                                 uint64_t* keys_hi, dal_stream_t stream) {
-  return forest_score_launch(x, nullptr, n, d, ldx, inner, leaf, n_trees, depth, lut, density, density_kind,
+  return forest_score_launch(x, nullptr, nullptr, n, d, ldx, inner, leaf, n_trees, depth, lut, density, density_kind,
                              density_err, row_flags, beta, order, votes, scores, keys, keys_hi, ForestStepHooks{},
                              as_stream(stream));
 }
@@ -795,13 +879,35 @@ extern "C" int dal_pool_blocked(const float* x, int64_t n, int64_t d, int64_t ld
   return DAL_OK;
 }
 
-extern "C" int dal_forest_score_blocked(const float* x, const float* xb, int64_t n, int64_t d, int64_t ldx,
-                                        const int32_t* inner, const uint8_t* leaf, int32_t n_trees, int32_t depth,
-                                        const double* lut, const void* density, int density_kind,
+extern "C" size_t dal_forest_prep_bytes(int64_t d, int32_t n_trees, int32_t depth) {
+  if (d < 1 || n_trees < 1 || depth < 1 || depth > DAL_MAX_TREE_DEPTH) return 0;
+  const int fu_max = blocked_fu_max(d, n_trees, depth);
+  return fu_max ? static_cast<size_t>(blocked_prep_layout(n_trees, depth, fu_max).total) : 0;
+}
+
+extern "C" int dal_forest_prepare(const int32_t* inner, const uint8_t* leaf, int32_t n_trees, int32_t depth,
+                                  int64_t d, void* prep, size_t prep_bytes, dal_stream_t stream) {
+  if (!inner || !leaf || !prep || reinterpret_cast<uintptr_t>(prep) % 16 != 0) return DAL_ERR_ARG;
+  if (d < 1 || n_trees < 1) return DAL_ERR_SHAPE;
+  if (depth < 1 || depth > DAL_MAX_TREE_DEPTH) return DAL_ERR_UNSUPPORTED;
+  const int fu_max = blocked_fu_max(d, n_trees, depth);
+  if (!fu_max) return DAL_ERR_UNSUPPORTED;  // the blocked path does not apply (dal_forest_blocked_rows == 0)
+  if (prep_bytes < static_cast<size_t>(blocked_prep_layout(n_trees, depth, fu_max).total)) return DAL_ERR_SHAPE;
+  const size_t smem = static_cast<size_t>((d + 31) / 32) * 8;
+  hipLaunchKernelGGL(forest_prepare_kernel, dim3(1), dim3(kPrepThreads), smem, as_stream(stream),
+                     reinterpret_cast<const int2*>(inner), leaf, n_trees, depth, static_cast<int>(d), fu_max,
+                     static_cast<unsigned char*>(prep));
+  DAL_RETURN_IF_LAUNCH_FAILED();
+  return DAL_OK;
+}
+
+extern "C" int dal_forest_score_blocked(const float* x, const float* xb, const void* fprep, int64_t n, int64_t d,
+                                        int64_t ldx, const int32_t* inner, const uint8_t* leaf, int32_t n_trees,
+                                        int32_t depth, const double* lut, const void* density, int density_kind,
                                         double density_err, const uint8_t* row_flags, double beta, int order,
                                         int32_t* votes, double* scores, uint64_t* keys, uint64_t* keys_hi,
                                         dal_stream_t stream) {
-  return forest_score_launch(x, xb, n, d, ldx, inner, leaf, n_trees, depth, lut, density, density_kind,
+  return forest_score_launch(x, xb, fprep, n, d, ldx, inner, leaf, n_trees, depth, lut, density, density_kind,
                              density_err, row_flags, beta, order, votes, scores, keys, keys_hi, ForestStepHooks{},
                              as_stream(stream));
 }

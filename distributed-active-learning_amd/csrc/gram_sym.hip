@@ -62,15 +62,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 #define AS3 __attribute__((address_space(3)))
 
-// Timing-only ablation builds (scripts/ab_build.sh -DDAL_GRAM_ABLATE=mask;
-// the results are wrong): 1 no column-sum epilogue, 2 no row fold, 4 no
-// per-stage barrier, 8 no B-stage DMA after the first, 16 no flushes, 32 every
-// DMA from the first column block (constant data, L2 hits), 64 DMA from 8
-// column blocks in turn (varying data, L2 hits).  0 in the product.
-#ifndef DAL_GRAM_ABLATE
-#define DAL_GRAM_ABLATE 0
-#endif
-constexpr int kAbl = DAL_GRAM_ABLATE;
 constexpr int kSB = 512;       // super block rows
 
 __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
@@ -286,8 +277,6 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
   // stage h of 256-column block J into LDS buffer buf.  Inline asm so the
   // compiler does not track the DMA on vmcnt (block_sync waits for it).
   auto issue = [&](int buf, int J, int h) {
-    if constexpr ((kAbl & 32) != 0) J = j_lo, h = 0;
-    if constexpr ((kAbl & 64) != 0) J = j_lo + (J & 7), h = 0;
     const char* sbase = reinterpret_cast<const char*>(
         ucols + (static_cast<int64_t>(J - jcol0) * 256 + h * C::SC) * ldh + slice_off);
     const unsigned fl = fresh_lane();
@@ -378,13 +367,6 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
   // reduce-scatter over the 16 column lanes leaves each lane 2 fully summed
   // rows, added by all 64 lanes at distinct LDS addresses.
   auto fold_rows = [&]() {
-    if constexpr ((kAbl & 2) != 0) {  // keep the chains live (their MFMAs stay)
-#pragma unroll
-      for (int rt = 0; rt < C::RT; ++rt)
-#pragma unroll
-        for (int ch = 0; ch < C::NCH; ++ch) asm volatile("" ::"v"(mc[ch][rt]));
-      return;
-    }
     float v[32];
 #pragma unroll
     for (int rt = 0; rt < C::RT; ++rt)
@@ -400,7 +382,6 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
     atomicAdd(&rowacc[row + 1], static_cast<double>(__builtin_rintf(v[1] * kFold)));
   };
   auto flush_one = [&](double& slot, int64_t out_row) {
-    if constexpr ((kAbl & 16) != 0) return;
     const double v = slot;
     if (v != 0.0) atomicAdd(acc_out + out_row, static_cast<unsigned long long>(static_cast<long long>(v)));
     slot = 0.0;
@@ -417,10 +398,7 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
   };
-  auto stage_sync = [&]() {
-    if constexpr ((kAbl & 4) != 0) return;
-    block_sync();
-  };
+  auto stage_sync = [&]() { block_sync(); };
 
   int r = -1;
   int unit = seek(contig ? 0 : g, r);
@@ -449,8 +427,7 @@ __global__ __launch_bounds__(64 * W, (Cfg<KS, W>::OCC)) void gram_csym_kernel(
         flush_rows(flushRU);
         flushRU = -1;
       }
-      if ((kAbl & 8) != 0) {
-      } else if (s + 1 < C::SPP) {
+      if (s + 1 < C::SPP) {
         issue(buf ^ 1, J, s + 1);
       } else if (has_next) {
         issue(buf ^ 1, nJ, 0);
@@ -646,10 +623,15 @@ constexpr int kResRows = 256;
 constexpr int kResFeat = 32;                 // features per LDS stage (divides every KS)
 constexpr int kResQ = kResFeat / 4;          // 16-B chunks per row per stage: H kResFeat/8, L kResFeat/8
 constexpr int kResLd = kResQ + 1;            // LDS row stride in 16-B chunks (+1: the threads' rows spread over the banks)
-// kFused (d_pad 32 or 64, few super blocks): no scan launch -- every block forms
-// its own R_B and C_B from sigma~ (256 / d_pad thread groups over the super
-// blocks, exact int64 sums reduced in LDS; the same integers as the scan's).
-template <bool kFused>
+// kMode kResFused (d_pad 32 or 64, few super blocks): no scan launch -- every
+// block forms its own R_B and C_B from sigma~ (256 / d_pad thread groups over
+// the super blocks, exact int64 sums reduced in LDS; the same integers as the
+// scan's).  kResStaged: the scan's R_B, C_B staged in LDS (16 d_pad bytes).
+// kResGlobal (d_pad > kResLdsMaxFeat, where they would not fit beside the
+// tile): read in place from the scan's output, uniform addresses.
+constexpr int kResStaged = 0, kResFused = 1, kResGlobal = 2;
+constexpr int kResLdsMaxFeat = 1024;  // 16 KiB of R_B | C_B + the 36 KiB tile: within 64 KiB per block
+template <int kMode>
 __global__ __launch_bounds__(kResRows) void csym_residual_kernel(const uint16_t* __restrict__ rows, int64_t ldh, int ks,
                                                                  int d_pad, int b0, int n_rows,
                                                                  const double* __restrict__ rb,
@@ -661,7 +643,7 @@ __global__ __launch_bounds__(kResRows) void csym_residual_kernel(const uint16_t*
   const int tid = threadIdx.x;
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kResRows;  // (a multiple of 256: one super block)
   const int64_t B = r0 / kSB;                                       // relative to b0
-  if constexpr (kFused) {
+  if constexpr (kMode == kResFused) {
     // feature pairs (16-B loads of sigma~): 256 / (d_pad / 2) thread groups
     // over the super blocks -- 8 (d_pad 64) or 16 (d_pad 32)
     __shared__ long long red[8][kResRows];
@@ -714,12 +696,14 @@ __global__ __launch_bounds__(kResRows) void csym_residual_kernel(const uint16_t*
         rc[d_pad + f] = static_cast<double>(odd ? (euo + tue - eue) : (eue + tuo - euo));
       }
     }
-  } else {
+  } else if constexpr (kMode == kResStaged) {
     for (int f = tid; f < d_pad; f += kResRows) {
       rc[f] = rb[B * d_pad + f];
       rc[d_pad + f] = cb[B * d_pad + f];
     }
   }
+  const double* __restrict__ Rv = kMode == kResGlobal ? rb + B * d_pad : rc;
+  const double* __restrict__ Cv = kMode == kResGlobal ? cb + B * d_pad : rc + d_pad;
   const int live_rows = n_rows - r0 < kResRows ? static_cast<int>(n_rows - r0) : kResRows;
   const uint16_t* blk = rows + r0 * ldh;
   double t = 0.0;
@@ -753,8 +737,8 @@ __global__ __launch_bounds__(kResRows) void csym_residual_kernel(const uint16_t*
           const uint16_t lb = static_cast<uint16_t>(e & 1 ? lw[e >> 1] >> 16 : lw[e >> 1] & 0xFFFFu);
           const double h = static_cast<double>(static_cast<float>(__builtin_bit_cast(_Float16, hb)));
           const double l = static_cast<double>(static_cast<float>(__builtin_bit_cast(_Float16, lb)));
-          t = t + l * rc[f];
-          t = t + (h + l) * rc[d_pad + f];
+          t = t + l * Rv[f];
+          t = t + (h + l) * Cv[f];
         }
       }
     }
@@ -1072,7 +1056,7 @@ extern "C" int dal_gram_sym_residual(const uint16_t* ops, int64_t nb_active, int
   const size_t smem = static_cast<size_t>(2 * d_pad) * 8;
   const uint16_t* rows = ops + s0 * kSB * ldh;
   if (d_pad <= 64 && na * d_pad <= DAL_CSYM_FUSED_MAX) {  // the blocks form R_B, C_B themselves
-    hipLaunchKernelGGL(csym_residual_kernel<true>, grid, dim3(kResRows), smem, st, rows, ldh, ks,
+    hipLaunchKernelGGL(csym_residual_kernel<kResFused>, grid, dim3(kResRows), smem, st, rows, ldh, ks,
                        static_cast<int>(d_pad), static_cast<int>(s0), static_cast<int>(n_rows), rb, cb, sig_u,
                        static_cast<int>(na), reinterpret_cast<long long*>(acc));
   } else {
@@ -1080,9 +1064,15 @@ extern "C" int dal_gram_sym_residual(const uint16_t* ops, int64_t nb_active, int
                        st, sig_u, static_cast<int>(na), static_cast<int>(d_pad), static_cast<int>(s0),
                        static_cast<int>(s0 + ns), rb, cb);
     DAL_RETURN_IF_LAUNCH_FAILED();
-    hipLaunchKernelGGL(csym_residual_kernel<false>, grid, dim3(kResRows), smem, st, rows, ldh, ks,
-                       static_cast<int>(d_pad), static_cast<int>(s0), static_cast<int>(n_rows), rb, cb, sig_u,
-                       static_cast<int>(na), reinterpret_cast<long long*>(acc));
+    if (d_pad <= kResLdsMaxFeat) {
+      hipLaunchKernelGGL(csym_residual_kernel<kResStaged>, grid, dim3(kResRows), smem, st, rows, ldh, ks,
+                         static_cast<int>(d_pad), static_cast<int>(s0), static_cast<int>(n_rows), rb, cb, sig_u,
+                         static_cast<int>(na), reinterpret_cast<long long*>(acc));
+    } else {  // wide pools: R_B, C_B read in place (they would not fit in LDS beside the tile)
+      hipLaunchKernelGGL(csym_residual_kernel<kResGlobal>, grid, dim3(kResRows), 0, st, rows, ldh, ks,
+                         static_cast<int>(d_pad), static_cast<int>(s0), static_cast<int>(n_rows), rb, cb, sig_u,
+                         static_cast<int>(na), reinterpret_cast<long long*>(acc));
+    }
   }
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;

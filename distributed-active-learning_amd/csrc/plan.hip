@@ -112,7 +112,8 @@ class DeviceGuard {
   bool ok_ = false;
 };
 
-extern "C" int dal_dw_plan_create(const float* x, const float* xb, int64_t n, int64_t d, int64_t ldx,
+extern "C" int dal_dw_plan_create(const float* x, const float* xb, const void* fprep, int64_t n, int64_t d,
+                                  int64_t ldx,
                                   const int32_t* inner,
                                   const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
                                   const int64_t* density_fixed, double density_err, const uint8_t* base_flags,
@@ -158,7 +159,7 @@ extern "C" int dal_dw_plan_create(const float* x, const float* xb, int64_t n, in
     hooks.base_flags = base_flags;
     hooks.stamp = p->stamp;
     hooks.step_id = p->step_dev;
-    const int step_rc = dw_step_impl(x, xb, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, density_err,
+    const int step_rc = dw_step_impl(x, xb, fprep, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, density_err,
                                      flags, beta, idx_base, norm64, colsum, k, cap, level1_passes,
                                      DAL_STEP_RESET_STATUS | DAL_STEP_WS_CLEAN, ws, ws_bytes, votes, scores, keys_lo,
                                      keys_hi, out_pair, reinterpret_cast<double*>(out_pair + k), out_keys,

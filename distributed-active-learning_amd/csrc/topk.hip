@@ -2134,7 +2134,8 @@ extern "C" size_t dal_dw_step_workspace_bytes(int64_t n, int64_t k, int64_t cap)
 // with DAL_STEP_RESET_STATUS.  Same bits as the two calls.
 namespace dal {
 
-int dw_step_impl(const float* x, const float* xb, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
+int dw_step_impl(const float* x, const float* xb, const void* fprep, int64_t n, int64_t d, int64_t ldx,
+                 const int32_t* inner,
                  const uint8_t* leaf,
                  int32_t n_trees, int32_t depth, const double* lut, const int64_t* density_fixed, double density_err,
                  const uint8_t* row_flags, double beta, int64_t idx_base, const double* norm64, const double* colsum,
@@ -2167,7 +2168,7 @@ int dw_step_impl(const float* x, const float* xb, int64_t n, int64_t d, int64_t 
   char* base = static_cast<char*>(ws);
   TopkHdr* h1 = reinterpret_cast<TopkHdr*>(base + W.L1.hdr);
   if (level1_passes == 0) {  // exact level 1: the two calls as they are
-    rc = forest_score_launch(x, xb, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, DAL_DENSITY_FIXED,
+    rc = forest_score_launch(x, xb, fprep, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, DAL_DENSITY_FIXED,
                              density_err, row_flags, beta, DAL_DESCENDING, votes, scores, keys_lo, keys_hi, hooks,
                              st);
     if (rc) return rc;
@@ -2200,7 +2201,7 @@ int dw_step_impl(const float* x, const float* xb, int64_t n, int64_t d, int64_t 
     if (folded) zero_words(reinterpret_cast<uint32_t*>(gmin), 2 * S.ng * 2, st);
   }
   if (!select_only) {
-    rc = forest_score_launch(x, xb, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, DAL_DENSITY_FIXED,
+    rc = forest_score_launch(x, xb, fprep, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, DAL_DENSITY_FIXED,
                              density_err, row_flags, beta, DAL_DESCENDING, votes, scores, keys_lo, keys_hi, hooks,
                              st);
     if (rc) return rc;
@@ -2238,7 +2239,8 @@ int dw_step_impl(const float* x, const float* xb, int64_t n, int64_t d, int64_t 
 
 }  // namespace dal
 
-extern "C" int dal_dw_step(const float* x, const float* xb, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
+extern "C" int dal_dw_step(const float* x, const float* xb, const void* fprep, int64_t n, int64_t d, int64_t ldx,
+                           const int32_t* inner,
                            const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
                            const int64_t* density_fixed, double density_err, const uint8_t* row_flags, double beta,
                            int64_t idx_base, const double* norm64, const double* colsum, int64_t k, int64_t cap,
@@ -2246,7 +2248,8 @@ extern "C" int dal_dw_step(const float* x, const float* xb, int64_t n, int64_t d
                            double* scores, uint64_t* keys_lo, uint64_t* keys_hi, int64_t* out_idx,
                            double* out_scores, uint64_t* out_keys, int32_t* dev_status, dal_event_t colsum_ready,
                            dal_stream_t stream) {
-  return dw_step_impl(x, xb, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, density_err, row_flags, beta,
+  return dw_step_impl(x, xb, fprep, n, d, ldx, inner, leaf, n_trees, depth, lut, density_fixed, density_err, row_flags,
+                      beta,
                       idx_base, norm64, colsum, k, cap, level1_passes, step_flags, ws, ws_bytes, votes, scores,
                       keys_lo, keys_hi, out_idx, out_scores, out_keys, dev_status, colsum_ready, stream, nullptr,
                       nullptr, nullptr);

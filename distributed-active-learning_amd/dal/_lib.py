@@ -78,7 +78,10 @@ SIGNATURES = {
     "dal_forest_blocked_rows": (c_int, [c_int64, c_int32, c_int32]),
     "dal_pool_blocked_floats": (c_int64, [c_int64, c_int64]),
     "dal_pool_blocked": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p]),
-    "dal_forest_score_blocked": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32,
+    "dal_forest_prep_bytes": (c_size_t, [c_int64, c_int32, c_int32]),
+    "dal_forest_prepare": (c_int, [c_void_p, c_void_p, c_int32, c_int32, c_int64, c_void_p, c_size_t, c_void_p]),
+    "dal_forest_score_blocked": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p,
+                                         c_int32,
                                          c_int32, c_void_p, c_void_p, c_int, c_double, c_void_p, c_double,
                                          c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "dal_density_separable": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p,
@@ -92,11 +95,11 @@ SIGNATURES = {
                               c_int64, c_int32, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_void_p]),
     "dal_dw_step_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int64]),
-    "dal_dw_step": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32, c_int32, c_void_p,
+    "dal_dw_step": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32, c_int32, c_void_p,
                             c_void_p, c_double, c_void_p, c_double, c_int64, c_void_p, c_void_p, c_int64, c_int64,
                             c_int32, ctypes.c_uint32, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "dal_dw_plan_create": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32, c_int32,
+    "dal_dw_plan_create": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32, c_int32,
                                    c_void_p, c_void_p, c_double, c_void_p, c_void_p, c_double, c_int64, c_void_p,
                                    c_void_p, c_int64, c_int64, c_int32, c_void_p, c_size_t, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

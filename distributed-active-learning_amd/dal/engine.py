@@ -20,7 +20,7 @@ from . import _lib
 from ._lib import (DAL_ASCENDING, DAL_CANON_CHUNK, DAL_DENSITY_EXACT, DAL_DENSITY_FIXED,
                    DAL_DENSITY_NONE, DAL_DESCENDING, DAL_FIXED_SCALE, DAL_FLAG_CAND_OVERFLOW,
                    DAL_FLAG_SAMPLE_MISS, DAL_FLAG_ZERO_NORM, DAL_ROW_CANDIDATE, DAL_ROW_EXCLUDED,
-                   DAL_SORT_CAP_PAYLOAD, DAL_STEP_KEEP_GROUPS, DAL_STEP_RESET_STATUS, DAL_STEP_SELECT_ONLY,
+                   DAL_SORT_CAP_PAYLOAD, DAL_STEP_RESET_STATUS,
                    DAL_STEP_WS_CLEAN, call)
 from .forest import Forest
 from .luts import ASCENDING, lut as make_lut
@@ -158,15 +158,17 @@ class PoolState:
         self._density_exact = None
         self._acc_pre = None  # density accumulator already zeroed by the prep kernel
         self._xb = None  # blocked feature-major copy of x (dal_pool_blocked), built by the first warm step
+        self.blocked_copy = True  # False: never build it (saves n x d fp32 of HBM; same bits, slower K2)
         self._us_steps = 0  # uncertainty steps taken on this pool (the blocked copy pays off from the second)
         self._ws_clean = {}   # (n, k, cap) -> workspace whose top-k header is zero (dal_dw_step)
         self.gram_events = None  # list -> (start, end) HIP events around each Gram call
         self.residual_events = []  # (start, end) HIP events around each residual call (with gram_events)
         self.forest_events = None  # list -> (start, end) HIP events around each forest-score call
         self.select_events = None  # list -> (start, end) HIP events around each dal_dw_select call
-        # list -> (start, end) around event_repeat selection-only launches of the
-        # fused step (bench; single GPU, fast level 1)
-        self.step_select_events = None
+        # bench only: a callable run after an eager (per-kernel timed) density
+        # step with the step's inputs -- it times the fused step's selection
+        # launch on its own (bench.time_step_select; single GPU, fast level 1)
+        self.step_select_probe = None
         # bench: a GPU spin (torch.cuda._sleep cycles) queued before each timed
         # call's start event, so the call's launches are all submitted before
         # the GPU reaches them -- the events then bracket the device span, not
@@ -195,16 +197,22 @@ class PoolState:
         forest is one the blocked score kernel applies to (it then reads only
         the features the forest tests), else None.  Built on first use
         (``build``) on the current stream and kept with the pool's caches:
-        the warm steps build it, the cold step keeps the row-major kernel."""
-        if self.n == 0:
+        the warm steps build it, the cold step keeps the row-major kernel.
+        The copy costs another n x d fp32 (2 GB at config 4): it is skipped
+        (the row-major kernel then runs, same bits) when ``blocked_copy`` is
+        False or the device lacks that much free memory plus a 1 GiB margin."""
+        if self.n == 0 or not self.blocked_copy:
             return None
         lib = _lib.load()
         if not lib.dal_forest_blocked_rows(self.d, forest.n_trees, forest.depth):
             return None
         if self._xb is None and build:
             torch = _torch()
-            xb = torch.empty(int(lib.dal_pool_blocked_floats(self.n, self.d)), dtype=torch.float32,
-                             device=self.device)
+            floats = int(lib.dal_pool_blocked_floats(self.n, self.d))
+            free, _ = torch.cuda.mem_get_info(self.device)
+            if free < 4 * floats + (1 << 30):
+                return None
+            xb = torch.empty(floats, dtype=torch.float32, device=self.device)
             call("dal_pool_blocked", _ptr(self.x), self.n, self.d, self.d, _ptr(xb), _stream(self.device))
             self._xb = xb
         return self._xb
@@ -358,8 +366,9 @@ class PoolState:
         any column split adds up to the same bits.
 
         gram "sym": acc is indexed by GLOBAL row (length >= nb_active * 256)
-        and also receives the column sums of the pairs this shard owns (the
-        other ranks' rows included); the ranks' accs are summed afterwards.
+        and receives ONLY the row sums of this shard's own rows over the
+        super-block pairs they take; the column sums of every pair come in
+        closed form from gram_residual, so no collective follows (ABI v8).
         ``skip`` = (row0, row1), global column rows (multiples of 256) left
         out (gram "sym" only: already accumulated)."""
         torch = _torch()
@@ -574,11 +583,19 @@ def forest_score(state: PoolState, forest: Forest, lut_dev, flags, order: int, d
         if xb is None:
             call("dal_forest_score", _ptr(state.x), *args)
         else:
-            call("dal_forest_score_blocked", _ptr(state.x), _ptr(xb), *args)
+            call("dal_forest_score_blocked", _ptr(state.x), _ptr(xb), _fprep(forest, state, xb), *args)
     if ev is not None:
         ev[1].record()
         state.forest_events.append(ev)
     return votes, scores, keys, keys_hi
+
+
+def _fprep(forest: Forest, state: PoolState, xb) -> int:
+    """Address of the forest prepared for the blocked kernel (0 without xb)."""
+    if xb is None:
+        return 0
+    p = forest.blocked_prep(state.device, state.d)
+    return 0 if p is None else _ptr(p)
 
 
 def topk_keys(keys, k: int, idx_base: int = 0):
@@ -724,7 +741,8 @@ def dw_step_local(state: PoolState, forest: Forest, flags, dens, lut_dev, k: int
         out_scores = torch.empty(k, dtype=torch.float64, device=dev)
         out_keys = None if sync else torch.empty(k, dtype=torch.int64, device=dev)
         try:
-            call("dal_dw_step", _ptr(state.x), 0 if xb is None else _ptr(xb), n, state.d, state.d, _ptr(inner),
+            call("dal_dw_step", _ptr(state.x), 0 if xb is None else _ptr(xb), _fprep(forest, state, xb), n,
+                 state.d, state.d, _ptr(inner),
                  _ptr(leaf), forest.n_trees, forest.depth, _ptr(lut_dev), _ptr(dens), derr, _ptr(flags),
                  float(beta), state.row_base,
                  _ptr(norm64), _ptr(colsum), k, cap, passes, DAL_STEP_WS_CLEAN, wsp, wsb, _ptr(votes),
@@ -857,55 +875,9 @@ def density_step(state: PoolState, unlabeled_idx, forest: Forest, k: int, beta: 
     idx, sel_scores, _ = dw_select_local(state, flags, votes, keys_lo, keys_hi, lut_dev, kk, beta,
                                          state.colsum(), colsum_ready=colsum_ready)
     state.check_status(state.last_status)  # the word dw_select_local read (no second sync)
-    if state.select_events is not None and state.step_select_events is not None and state.level1_fast:
-        _time_step_select(state, forest, flags, dens, lut_dev, kk, beta, xb)
+    if state.select_events is not None and state.step_select_probe is not None and state.level1_fast:
+        state.step_select_probe(state, forest, flags, dens, lut_dev, kk, beta, xb)
     return Selection(scores=(scores, loc), indices=idx, selected_scores=sel_scores, votes=(votes, loc))
-
-
-def _time_step_select(state: PoolState, forest: Forest, flags, dens, lut_dev, k: int, beta: float, xb=None):
-    """bench: the selection launch of the fused step (what dal_dw_step and the
-    warm plan run after the score kernel folded the row-group minima) timed on
-    its own: one full dal_dw_step that keeps the minima, then event_repeat
-    DAL_STEP_SELECT_ONLY calls between two events (behind a GPU spin), then one
-    more that clears them.  The selections must equal the step's."""
-    torch = _torch()
-    lib = _lib.load()
-    n, dev = state.n, state.device
-    inner, leaf = forest.device(dev)
-    norm64, colsum = state.norms(), state.colsum()
-    base = candidate_cap(n, k) if state.cap_base is None else max(int(k), int(state.cap_base))
-    cap = int(min(n, base * state.cap_scale))
-    passes = level1_passes(state, n, k, cap)
-    if passes == 0:
-        return
-    wsb = int(lib.dal_dw_step_workspace_bytes(n, k, cap))
-    ws, wsp = workspace(wsb, dev)
-    ws.zero_()
-    bufs = [torch.empty(n, dtype=t, device=dev) for t in (torch.int32, torch.float64, torch.int64, torch.int64)]
-    outs = [(torch.empty(k, dtype=torch.int64, device=dev), torch.empty(k, dtype=torch.float64, device=dev))
-            for _ in range(2)]
-    status = torch.zeros(1, dtype=torch.int32, device=dev)
-
-    def step(flags_bits, out):
-        call("dal_dw_step", _ptr(state.x), 0 if xb is None else _ptr(xb), n, state.d, state.d, _ptr(inner),
-             _ptr(leaf), forest.n_trees, forest.depth, _ptr(lut_dev), _ptr(dens), float(density_error(state)),
-             _ptr(flags), float(beta),
-             state.row_base, _ptr(norm64), _ptr(colsum), k, cap, passes, flags_bits, wsp, wsb,
-             *[_ptr(b) for b in bufs], _ptr(out[0]), _ptr(out[1]), 0, _ptr(status), 0, _stream(dev))
-
-    step(DAL_STEP_WS_CLEAN | DAL_STEP_KEEP_GROUPS, outs[0])
-    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-    if state.event_lead_cycles:
-        torch.cuda._sleep(state.event_lead_cycles)
-    ev[0].record()
-    for _ in range(state.event_repeat):
-        step(DAL_STEP_WS_CLEAN | DAL_STEP_KEEP_GROUPS | DAL_STEP_SELECT_ONLY, outs[1])
-    ev[1].record()
-    step(DAL_STEP_WS_CLEAN | DAL_STEP_SELECT_ONLY, outs[1])  # the last one clears the minima
-    if int(status.item()) != 0 or not (torch.equal(outs[0][0], outs[1][0]) and
-                                      torch.equal(outs[0][1].view(torch.int64), outs[1][1].view(torch.int64))):
-        return  # (an overflow or a mismatch: no timing recorded)
-    state.step_select_events.append(ev)
 
 
 class WarmStepGraph:
@@ -960,11 +932,20 @@ class WarmStepGraph:
         self.wsb = int(lib.dal_dw_step_workspace_bytes(n, k, cap))
         self.ws, self.wsp = workspace(self.wsb, dev)
         xb = state.blocked_pool(forest)  # the score kernel reads the pool's blocked copy when it applies
+        # the forest prepared for the blocked kernel, in a static buffer the
+        # plan reads at its captured address (re-prepared when the forest changes)
+        self.fprep = None
+        if xb is not None:
+            nb = int(lib.dal_forest_prep_bytes(state.d, self.n_trees, self.depth))
+            if nb:
+                self.fprep = torch.empty(nb, dtype=torch.uint8, device=dev)
+                self._prepare()
         self._keep = (state.density_fixed(), state.colsum() if colsum is None else colsum, state.norms(),
                       state.flags, state.x, xb)
         dens, colsum, norm64 = self._keep[:3]
         plan = ctypes.c_void_p()
-        call("dal_dw_plan_create", _ptr(state.x), 0 if xb is None else _ptr(xb), n, state.d, state.d,
+        call("dal_dw_plan_create", _ptr(state.x), 0 if xb is None else _ptr(xb),
+             0 if self.fprep is None else _ptr(self.fprep), n, state.d, state.d,
              _ptr(self.inner), _ptr(self.leaf),
              self.n_trees, self.depth, _ptr(self.lut), _ptr(dens), float(density_error(state)), _ptr(state.flags),
              _ptr(self.flags), float(beta), state.row_base, _ptr(norm64), _ptr(colsum), k, cap, passes, self.wsp,
@@ -975,6 +956,13 @@ class WarmStepGraph:
         self._status_ref = ctypes.byref(self._status)
         self._run = lib.dal_dw_plan_run
         self._finalizer = weakref.finalize(self, lib.dal_dw_plan_destroy, plan)
+
+    def _prepare(self):
+        """dal_forest_prepare of the plan's static forest copy into its static
+        prepared buffer (stream-ordered before the next replay)."""
+        if self.fprep is not None:
+            call("dal_forest_prepare", _ptr(self.inner), _ptr(self.leaf), self.n_trees, self.depth, self.state.d,
+                 _ptr(self.fprep), int(self.fprep.shape[0]), _stream(self.state.device))
 
     def run(self, forest: Forest, unl):
         """Refresh the inputs, replay, read the status: returns (votes,
@@ -992,6 +980,7 @@ class WarmStepGraph:
             inner, leaf = forest.device(dev)
             self.inner.copy_(inner)
             self.leaf.copy_(leaf)
+            self._prepare()
             self.forest_ref = forest
         idx = torch.empty(self.k, dtype=torch.int64, device=dev)
         sc = torch.empty(self.k, dtype=torch.float64, device=dev)
@@ -1009,6 +998,7 @@ class WarmStepGraph:
             inner, leaf = forest.device(self.state.device)
             self.inner.copy_(inner)
             self.leaf.copy_(leaf)
+            self._prepare()
             self.forest_ref = forest
         call("dal_dw_plan_launch", self.plan, unl.data_ptr(), int(unl.shape[0]), _raw_stream(self.state.device))
 

@@ -77,6 +77,30 @@ class Forest:
             )
         return self._dev[key]
 
+    def blocked_prep(self, device, d: int):
+        """The forest prepared for the blocked score kernel over d features
+        (dal_forest_prepare, ABI v10: feature list, remapped nodes, leaves), a
+        16-B aligned uint8 device tensor built once per (device, d) on the
+        current stream -- or None when the blocked path does not apply."""
+        import torch
+
+        from . import _lib
+
+        key = ("prep", str(device), int(d))
+        if key not in self._dev:
+            lib = _lib.load()
+            nb = int(lib.dal_forest_prep_bytes(int(d), self.n_trees, self.depth))
+            buf = None
+            if nb:
+                self.check_features(int(d))
+                inner, leaf = self.device(device)
+                buf = torch.empty(nb, dtype=torch.uint8, device=device)  # (caching allocator: 512-B aligned)
+                _lib.call("dal_forest_prepare", inner.data_ptr(), leaf.data_ptr(), self.n_trees, self.depth,
+                          int(d), buf.data_ptr(), nb,
+                          torch.cuda.current_stream(device).cuda_stream)
+            self._dev[key] = buf
+        return self._dev[key]
+
     # ------------------------------------------------------------ builders
     @classmethod
     def from_nodes(cls, feature, threshold, left, right, value, roots) -> "Forest":

@@ -459,19 +459,6 @@ class TorchComm:
         self.dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
         return out, None
 
-    def reduce_scatter_sum(self, t):
-        """Sum over ranks of a [world * m] tensor; returns this rank's [m] slice."""
-        torch = __import__("torch")
-        m = t.shape[0] // self.world
-        rank = self.dist.get_rank(self.group)
-        if self.backend == "gloo":
-            h = t.cpu()
-            self.dist.all_reduce(h, op=self.dist.ReduceOp.SUM, group=self.group)
-            return h[rank * m:(rank + 1) * m].to(t.device)
-        out = torch.empty(m, dtype=t.dtype, device=t.device)
-        self.dist.reduce_scatter_tensor(out, t.contiguous(), op=self.dist.ReduceOp.SUM, group=self.group)
-        return out
-
     def wait(self, work):
         """Order the current stream after the collective (no host block)."""
         if work is not None:

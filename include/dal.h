@@ -248,15 +248,36 @@ int dal_forest_score(const float* x, int64_t n, int64_t d, int64_t ldx,
  * features at <= 256, and a tile of those plus the forest fits 96 KiB of LDS)
  * it reads only the features the forest tests -- each tile's listed features
  * as 256-B runs (config 4, T = 10: ~116 of 256 features) -- else it runs
- * dal_forest_score's row-major kernel on x.  xb must be 16-B aligned. */
+ * dal_forest_score's row-major kernel on x.  xb must be 16-B aligned.
+ * Every inner node's feature must lie in [0, d) (the forest is device data, so
+ * the library does not read it back to check; dal.forest.Forest.check_features
+ * does before upload).  For an invalid forest the outputs are unspecified and
+ * the two entry points differ: the blocked kernel clamps a feature into
+ * [0, d - 1], the row-major kernel does not. */
 int dal_forest_blocked_rows(int64_t d, int32_t n_trees, int32_t depth);
 int64_t dal_pool_blocked_floats(int64_t n, int64_t d);
 int dal_pool_blocked(const float* x, int64_t n, int64_t d, int64_t ldx, float* xb, dal_stream_t stream);
-int dal_forest_score_blocked(const float* x, const float* xb, int64_t n, int64_t d, int64_t ldx,
-                             const int32_t* inner, const uint8_t* leaf, int32_t n_trees, int32_t depth,
-                             const double* lut, const void* density, int density_kind, double density_err,
-                             const uint8_t* row_flags, double beta, int order, int32_t* votes, double* scores,
-                             uint64_t* keys, uint64_t* keys_hi, dal_stream_t stream);
+/* The prepared forest (ABI v10): the blocked kernel's per-block forest setup
+ * (the distinct tested features, every node's feature remapped to its slot in
+ * that list, the leaves) done ONCE per (forest, d) into a caller-owned device
+ * buffer of dal_forest_prep_bytes(d, n_trees, depth) bytes (16-B aligned; 0
+ * when dal_forest_blocked_rows is 0).  Pass it as ``fprep`` to
+ * dal_forest_score_blocked / dal_dw_step / dal_dw_plan_create with the same
+ * forest (inner, leaf, n_trees, depth) and d: each block of the score kernel
+ * then copies it into LDS instead of rebuilding it; the outputs are the same
+ * bits.  A stale fprep (another forest) gives that forest's votes: re-prepare
+ * after the forest changes (stream-ordered: one launch, one block).  Reads the
+ * forest arrays; a node feature outside [0, d) is clamped (as the unprepared
+ * blocked kernel does) and counted in the buffer's second int32 word. */
+size_t dal_forest_prep_bytes(int64_t d, int32_t n_trees, int32_t depth);
+int dal_forest_prepare(const int32_t* inner, const uint8_t* leaf, int32_t n_trees, int32_t depth, int64_t d,
+                       void* fprep, size_t fprep_bytes, dal_stream_t stream);
+int dal_forest_score_blocked(const float* x, const float* xb, const void* fprep, int64_t n, int64_t d,
+                             int64_t ldx, const int32_t* inner, const uint8_t* leaf, int32_t n_trees,
+                             int32_t depth, const double* lut, const void* density, int density_kind,
+                             double density_err, const uint8_t* row_flags, double beta, int order,
+                             int32_t* votes, double* scores, uint64_t* keys, uint64_t* keys_hi,
+                             dal_stream_t stream);
 
 /* ---- (a11) top-k: sortBy(score).take(k) --------------------------------
  * Replaces uncertainty_sampling.py:106,109 / density_weighting.py:168,172.
@@ -317,26 +338,35 @@ int dal_dw_select(const uint64_t* keys_lo, const uint64_t* keys_hi, const int32_
  *                          dal_dw_step left it so, or the caller zeroed the
  *                          workspace once): no zeroing launch.  The header is
  *                          left zero on exit whenever this flag is given.
- *   DAL_STEP_KEEP_GROUPS   (ABI v8; fast level 1) the row-group minima the step
- *                          folded are left in the workspace instead of cleared,
- *                          so that DAL_STEP_SELECT_ONLY calls can re-run the
- *                          selection; a later call without this flag clears them.
- *   DAL_STEP_SELECT_ONLY   (ABI v8; with DAL_STEP_WS_CLEAN, fast level 1, no
- *                          DAL_STEP_RESET_STATUS) only the selection launch: it
- *                          re-reads the votes, keys and group minima that the
- *                          previous call with DAL_STEP_KEEP_GROUPS left on the
- *                          same buffers and workspace (the same arguments),
- *                          and gives the same outputs.  Used to time the
- *                          selection launch of the fused step on its own.
+ *   DAL_STEP_KEEP_GROUPS   (ABI v8; MEASUREMENT flag, fast level 1) the row-group
+ *                          minima the step folded are left in the workspace
+ *                          instead of cleared, so that DAL_STEP_SELECT_ONLY
+ *                          calls can re-run the selection.  The workspace is
+ *                          then NOT clean for a full step: the next call on it
+ *                          MUST be DAL_STEP_SELECT_ONLY, and the sequence ends
+ *                          with a SELECT_ONLY call without KEEP_GROUPS (which
+ *                          clears the minima) before any full step uses the
+ *                          workspace with DAL_STEP_WS_CLEAN again.
+ *   DAL_STEP_SELECT_ONLY   (ABI v8; MEASUREMENT flag; with DAL_STEP_WS_CLEAN, fast
+ *                          level 1, no DAL_STEP_RESET_STATUS) only the selection
+ *                          launch: it re-reads the votes, keys and group minima
+ *                          that the previous call with DAL_STEP_KEEP_GROUPS left
+ *                          on the same buffers and workspace (the same
+ *                          arguments), and gives the same outputs.  bench.py
+ *                          times the fused step's selection launch on its own
+ *                          with these two flags (time_step_select); the product
+ *                          path never sets them.
  * xb (ABI v9; nullable): the pool's blocked copy (dal_pool_blocked) -- the
- * score kernel is then dal_forest_score_blocked's.
+ * score kernel is then dal_forest_score_blocked's; fprep (ABI v10; nullable,
+ * with xb): the forest prepared by dal_forest_prepare.
  * Workspace: dal_dw_step_workspace_bytes (== dal_dw_select's). */
 #define DAL_STEP_RESET_STATUS 1u
 #define DAL_STEP_WS_CLEAN 2u
 #define DAL_STEP_KEEP_GROUPS 4u
 #define DAL_STEP_SELECT_ONLY 8u
 size_t dal_dw_step_workspace_bytes(int64_t n, int64_t k, int64_t cap);
-int dal_dw_step(const float* x, const float* xb, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
+int dal_dw_step(const float* x, const float* xb, const void* fprep, int64_t n, int64_t d, int64_t ldx,
+                const int32_t* inner,
                 const uint8_t* leaf,
                 int32_t n_trees, int32_t depth, const double* lut, const int64_t* density_fixed,
                 double density_err, const uint8_t* row_flags, double beta, int64_t idx_base,
@@ -362,10 +392,13 @@ int dal_dw_step(const float* x, const float* xb, int64_t n, int64_t d, int64_t l
  * wait for that word (a bounded spin, then a stream sync) and return the
  * status in *status -- the
  * density_weighting.py:133-176 iteration in one call.  Buffers must outlive
- * the plan; dal_dw_plan_destroy frees it.  xb (ABI v9; nullable): as
- * dal_dw_step's. */
+ * the plan; dal_dw_plan_destroy frees it.  xb (ABI v9) and fprep (ABI v10;
+ * both nullable): as dal_dw_step's -- the plan reads fprep at its captured
+ * address on every replay, so a new forest is re-prepared into the same
+ * buffer before the next run. */
 typedef struct dal_dw_plan dal_dw_plan_t;
-int dal_dw_plan_create(const float* x, const float* xb, int64_t n, int64_t d, int64_t ldx, const int32_t* inner,
+int dal_dw_plan_create(const float* x, const float* xb, const void* fprep, int64_t n, int64_t d, int64_t ldx,
+                       const int32_t* inner,
                        const uint8_t* leaf, int32_t n_trees, int32_t depth, const double* lut,
                        const int64_t* density_fixed, double density_err, const uint8_t* base_flags,
                        uint8_t* flags, double beta, int64_t idx_base, const double* norm64,

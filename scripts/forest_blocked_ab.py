@@ -67,7 +67,7 @@ def main():
             if m == "row":
                 call("dal_forest_score", _ptr(x), n, d, d, *tail)
             else:
-                call("dal_forest_score_blocked", _ptr(x), _ptr(xb), n, d, d, *tail)
+                call("dal_forest_score_blocked", _ptr(x), _ptr(xb), 0, n, d, d, *tail)
 
         for m in outs:
             run(m)

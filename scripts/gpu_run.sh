@@ -9,6 +9,8 @@
 #   smoke                 __graft_entry__.smoke()             -> gpurun_out/smoke.log
 #   bench[=ARGS]          python bench.py ARGS (',' = space)  -> gpurun_out/bench_<n>.log
 #                         (full result: gpurun_out/bench_full_<n>.json)
+#   sharded[=ARGS]        DAL_BENCH_SHARDED=1 python bench.py ARGS: --gpus 1 through dal/parallel.py on a
+#                         one-rank RCCL group -> gpurun_out/sharded_<n>.log
 #   gloo=N[=ARGS]         bench.py on N gloo ranks sharing the one GPU (torch.distributed.run)
 #                         -> gpurun_out/gloo_<n>.log
 #   selfgloo=N[=ARGS]     bench.py --gpus N on gloo with NO outside launcher (bench.py starts its ranks)
@@ -48,6 +50,13 @@ for step in "$@"; do
       rc=$?
       echo "[$n] bench ${rest//,/ } rc=$rc"
       tail -1 gpurun_out/bench_$n.log | cut -c1-600
+      ;;
+    sharded)
+      DAL_BENCH_SHARDED=1 timeout -k 10 900 python -u bench.py ${rest//,/ } --out gpurun_out/sharded_full_$n.json \
+        > gpurun_out/sharded_$n.log 2>&1
+      rc=$?
+      echo "[$n] sharded ${rest//,/ } rc=$rc"
+      tail -1 gpurun_out/sharded_$n.log | cut -c1-600
       ;;
     gloo)
       np=${rest%%=*}

@@ -154,11 +154,11 @@ def test_headline_is_compact_and_complete():
     assert all(isinstance(v, bool) for v in h["self_check"].values())
     assert h["value"] == round(out["value"], -1) or abs(h["value"] / out["value"] - 1) < 1e-5
     # a multi-GPU record names its rank count and the per-rank exchange maxima
-    out.update(world_size=8, backend="nccl", n_gpus=8,
-               ranks={"gram_ms_max": 160.1, "gram_ms_min": 158.0, "all_gather_ms_max": 3.2,
-                      "reduce_scatter_ms_max": 0.4})
+    out.update(world_size=8, backend="nccl", n_gpus=8, sharded_path=True,
+               ranks={"gram_ms_max": 160.1, "gram_ms_min": 158.0, "all_gather_ms_max": 3.2})
     h8 = bench.headline(out)
     assert h8["world_size"] == 8 and h8["backend"] == "nccl" and h8["ranks"]["all_gather_ms_max"] == 3.2
+    assert h8["sharded_path"] is True
     assert len(json.dumps(h8).encode()) <= bench.HEADLINE_MAX_BYTES
 
 

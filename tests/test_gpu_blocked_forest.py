@@ -1,5 +1,6 @@
 """K2 over the pool's blocked feature-major copy (ABI v9: dal_pool_blocked +
-dal_forest_score_blocked; uncertainty_sampling.py:88-98,
+dal_forest_score_blocked; ABI v10: the forest prepared once by
+dal_forest_prepare, checked entry by entry; uncertainty_sampling.py:88-98,
 density_weighting.py:136-167).  The blocked kernel reads only the features
 the forest tests, so it must give dal_forest_score's votes, scores and keys
 bit for bit on every shape the rule admits: ragged tile tails (n not a
@@ -43,7 +44,30 @@ def _forest_score_pair(cuda, X, F, density_kind, order=None, flags_unl=None):
     a = engine.forest_score(st, F, lut, flags, order, density=dens, density_err=derr, want_hi=True,
                             density_kind=kind if dens is not None else None)
     b = engine.forest_score(st, F, lut, flags, order, density=dens, density_err=derr, want_hi=True,
-                            density_kind=kind if dens is not None else None, xb=xb)
+                            density_kind=kind if dens is not None else None, xb=xb)  # prepared forest (ABI v10)
+    # the prepared forest itself: header {fu, bad, nodes, fu_max}, the sorted
+    # distinct features as the list, every node's feature as its slot * 64
+    prep = F.blocked_prep(cuda, d)
+    assert prep is not None
+    hdr = prep[:16].view(torch.int32).cpu().numpy()
+    feats = np.unique(F.inner[..., 0])
+    nn = F.inner.shape[0] * F.inner.shape[1]
+    assert hdr[0] == feats.size and hdr[1] == 0 and hdr[2] == nn and hdr[3] >= feats.size
+    pay = prep[16:].cpu().numpy()
+    nodes = pay[:nn * 8].view(np.int32).reshape(-1, 2)
+    assert np.array_equal(nodes[:, 0], np.searchsorted(feats, F.inner[..., 0].reshape(-1)) * 64)
+    assert np.array_equal(nodes[:, 1], F.inner[..., 1].reshape(-1))
+    lb = -(-F.leaf.size // 4) * 4
+    assert np.array_equal(pay[nn * 8:nn * 8 + F.leaf.size], F.leaf.reshape(-1))
+    used = pay[nn * 8 + lb:nn * 8 + lb + 2 * feats.size].view(np.uint16)
+    assert np.array_equal(used, feats)
+    # the same kernel building its forest per block (fprep = NULL): the same bits
+    inner, leaf = F.device(cuda)
+    c = [torch.empty_like(t) for t in b]
+    P = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
+    call("dal_forest_score_blocked", P(st.x), P(xb), 0, n, d, d, P(inner), P(leaf), F.n_trees, F.depth, P(lut),
+         P(dens), kind, float(derr), P(flags), 1.0, int(order), *[P(t) for t in c], S)
+    _same(b, c)
     return st, a, b
 
 
@@ -174,7 +198,7 @@ def test_dw_step_and_plan_with_blocked_copy(cuda):
         i1 = torch.empty(k, dtype=torch.int64, device=cuda)
         c1 = torch.empty(k, dtype=torch.float64, device=cuda)
         st.status.zero_()
-        call("dal_dw_step", P(st.x), 0 if use is None else P(use), n, d, d, P(inner), P(leaf), 10, 4, P(lut),
+        call("dal_dw_step", P(st.x), 0 if use is None else P(use), 0, n, d, d, P(inner), P(leaf), 10, 4, P(lut),
              P(dens), float(engine.density_error(st)), P(flags), 1.0, 0, P(norm64), P(colsum), k, cap, 1,
              DAL_STEP_WS_CLEAN, wsp, wsb, *[P(t) for t in outs], P(i1), P(c1), 0, P(st.status), 0, S)
         assert int(st.status.item()) == 0

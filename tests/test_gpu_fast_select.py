@@ -212,7 +212,7 @@ def test_dw_step_matches_separate_calls(cuda, n, d, trees, passes):
         c1 = torch.empty(k, dtype=torch.float64, device=cuda)
         ok1 = torch.empty(k, dtype=torch.int64, device=cuda)
         st.status.fill_(_lib.DAL_FLAG_CAND_OVERFLOW)  # stale: the step must clear it on the device
-        call("dal_dw_step", P(st.x), 0, n, d, d, P(inner), P(leaf), trees, 4, P(lut), P(dens), float(derr), P(flags),
+        call("dal_dw_step", P(st.x), 0, 0, n, d, d, P(inner), P(leaf), trees, 4, P(lut), P(dens), float(derr), P(flags),
              1.0, 0, P(norm64), P(colsum), k, cap, passes, DAL_STEP_RESET_STATUS | DAL_STEP_WS_CLEAN, wsp,
              int(lib.dal_dw_step_workspace_bytes(n, k, cap)), P(v), P(s), P(klo), P(khi), P(i1), P(c1), P(ok1),
              P(st.status), 0, S)
@@ -252,7 +252,7 @@ def test_dw_step_sample_miss_flag(cuda):
     i1 = torch.empty(k, dtype=torch.int64, device=cuda)
     c1 = torch.empty(k, dtype=torch.float64, device=cuda)
     st.status.zero_()
-    call("dal_dw_step", P(st.x), 0, n, d, d, P(inner), P(leaf), 10, 4, P(lut), P(dens), float(engine.density_error(st)),
+    call("dal_dw_step", P(st.x), 0, 0, n, d, d, P(inner), P(leaf), 10, 4, P(lut), P(dens), float(engine.density_error(st)),
          P(flags), 1.0, 0, P(norm64), P(colsum), k, cap, 1, 0, wsp, wsb, *[P(t) for t in outs], P(i1), P(c1), 0,
          P(st.status), 0, torch.cuda.current_stream(cuda).cuda_stream)
     assert int(st.status.item()) & _lib.DAL_FLAG_SAMPLE_MISS
@@ -497,7 +497,7 @@ def test_dw_step_select_only_repeats_the_selection(cuda, n, d, trees):
         i = torch.empty(k, dtype=torch.int64, device=cuda)
         c = torch.empty(k, dtype=torch.float64, device=cuda)
         st.status.zero_()
-        call("dal_dw_step", P(st.x), 0, n, d, d, P(inner), P(leaf), trees, 4, P(lut), P(dens),
+        call("dal_dw_step", P(st.x), 0, 0, n, d, d, P(inner), P(leaf), trees, 4, P(lut), P(dens),
              float(engine.density_error(st)), P(flags), 1.0, 0, P(norm64), P(colsum), k, cap, 1, bits, wsp, wsb,
              *[P(b) for b in bufs], P(i), P(c), 0, P(st.status), 0, S)
         assert int(st.status.item()) == 0

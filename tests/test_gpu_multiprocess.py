@@ -1,15 +1,16 @@
 """Multi-process sharded selection with the REAL HIP kernels (VERDICT r01
 item 7): two spawned ranks share cuda:0, each runs the HIP ShardedSelector on
 its row shard, and the exchanges go through real torch.distributed collectives
-(TorchComm over gloo -- RCCL needs one GPU per rank; gloo stages the same
-all-gathers and the symmetric Gram's int64 reduce-scatter through the host).
-The merged selections are compared with the CPU oracle.
+(TorchComm over gloo -- RCCL needs one GPU per rank, see test_gpu_rccl.py for
+the RCCL branch at world size 1; gloo stages the same all-gathers through the
+host).  The merged selections are compared with the CPU oracle.
 
-Covers: density-weighted select (gram mode: split-operand all-gather, fixed-
-point reduce-scatter, canonical partials, local exact top-k, packed top-k
-all-gather + merge; separable mode), uncertainty select (no normalisation, so
-a zero row is accepted), and the sharded diversity select with global
-candidates that all live in ONE shard (the other rank has none).
+Covers: density-weighted select (gram mode: split-operand all-gather with the
+canonical partials, each rank's own-row density with no density collective,
+local exact top-k, packed top-k all-gather + merge; separable mode),
+uncertainty select (no normalisation, so a zero row is accepted), and the
+sharded diversity select with global candidates that all live in ONE shard
+(the other rank has none).
 
 Reference: density_weighting.py:73 (BlockMatrix shuffle), :168,:172 (sortBy +
 take to the driver); similarity.py:34-38.

@@ -144,6 +144,37 @@ def test_gram_residual_scan_path(cuda):
     assert np.abs(got[ok] - ref[ok]).max() <= bound
 
 
+@pytest.mark.parametrize("d", [1000, 1100, 8192, 9000])
+def test_gram_residual_wide_pools(cuda, d):
+    """Wide pools: above 1,024 padded features the
+    residual reads R_B, C_B from global memory instead of staging 16 d_pad
+    bytes in LDS beside its 36 KiB tile (d_pad 8,192 would exceed the 160 KiB
+    LDS).  The density against the split operand's own fp64 row sums and the
+    canonical density within the bound, at d_pad 1,024 (LDS), 1,280, 8,192
+    and 9,216."""
+    from dal import _lib
+    from dal.engine import PoolState
+
+    n = 700
+    X = O.synthetic_pool(n, d, seed=12)
+    E = list(range(10))
+    st = PoolState(X, excluded=E, device=cuda, gram="sym")
+    got = _np(st.density())
+    sp = _np(st.gram_operand()).view(np.float16).astype(np.float64)
+    ks = 128 if st.d_pad % 128 == 0 else 64
+    ut = np.zeros((st.n_pad, st.d_pad))
+    for s0 in range(0, st.d_pad, ks):
+        ut[:, s0:s0 + ks] = (sp[:, 2 * s0:2 * s0 + ks] + sp[:, 2 * s0 + ks:2 * s0 + 2 * ks]) * 2.0**-12
+    ut = ut[:n]
+    keep = np.ones(n, bool)
+    keep[E] = False
+    d_split = ut @ ut[keep].sum(axis=0)
+    assert np.abs(got[keep] - d_split[keep]).max() <= 1e-6 * (n - len(E))
+    ref = O.density_canonical(X, E)
+    bound = _lib.load().dal_density_error_bound_sym(n - len(E))
+    assert np.abs(got[keep] - ref[keep]).max() <= bound
+
+
 @pytest.mark.parametrize("d", [7, 30, 64, 65, 200, 500])
 def test_fused_prep_matches_separate_kernels(cuda, d):
     """dal_prep_split == dal_normalize_rows + dal_split_f16 +
@@ -653,9 +684,6 @@ class _RecordingComm:
         assert work in ("work", None)
         self.waited = self.waited or work == "work"
 
-    def reduce_scatter_sum(self, t):
-        raise AssertionError("the density exchange has no reduce-scatter")
-
 
 @pytest.mark.parametrize("world,n", [(2, 5000), (3, 7000), (4, 2500), (8, 9000)])
 def test_exchange_density_column_split_bit_identical(cuda, world, n):
@@ -731,9 +759,6 @@ class _AsyncComm:
         if work is not None:
             work.wait()
 
-    def reduce_scatter_sum(self, t):
-        raise AssertionError("the density exchange has no reduce-scatter")
-
 
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_exchange_density_async_producer_bit_identical(cuda, world):
@@ -788,9 +813,6 @@ class _OneRankComm:
 
     def wait(self, work):
         assert work is None
-
-    def reduce_scatter_sum(self, t):
-        return t
 
 
 def test_sharded_warm_plan_across_iterations(cuda):

@@ -36,7 +36,7 @@ def test_library_exports_every_header_symbol():
 
 def test_host_helpers():
     lib = _lib.load()
-    assert lib.dal_abi_version() == 9
+    assert lib.dal_abi_version() == 10
     assert lib.dal_pad_rows(1) == 512 and lib.dal_pad_rows(100000) == 100352
     assert [lib.dal_pad_features(d) for d in (1, 30, 33, 64, 65, 128, 129, 256, 500, 784)] == \
         [32, 32, 64, 64, 128, 128, 256, 256, 512, 1024]
@@ -113,9 +113,39 @@ def test_blocked_pool_rule_without_gpu():
     assert lib.dal_pool_blocked(None, 10, 4, 4, p, None) == -1
     assert lib.dal_pool_blocked(p, 10, 4, 3, p, None) == -2
     assert lib.dal_pool_blocked(p, 0, 4, 4, p, None) == 0  # nothing to copy: no launch
-    odd = ctypes.c_void_p(264)  # xb must be 16-B aligned
-    assert lib.dal_forest_score_blocked(p, odd, 10, 256, 256, p, p, 10, 4, p, None, 0, 0.0, None, 1.0, 0,
+    odd = ctypes.c_void_p(264)  # xb and fprep must be 16-B aligned
+    assert lib.dal_forest_score_blocked(p, odd, None, 10, 256, 256, p, p, 10, 4, p, None, 0, 0.0, None, 1.0, 0,
                                         p, p, p, None, None) == -1
+    assert lib.dal_forest_score_blocked(p, p, odd, 10, 256, 256, p, p, 10, 4, p, None, 0, 0.0, None, 1.0, 0,
+                                        p, p, p, None, None) == -1
+
+
+def test_forest_prep_rule_without_gpu():
+    """ABI v10: the prepared forest is a 16-B header and the blocked kernel's
+    LDS forest region (nodes int2, leaves rounded to 4 B, the u16 feature list
+    for at most min(nodes, d) features), padded to 16 B; 0 bytes where the
+    blocked path does not apply.  Bad arguments are rejected before any HIP call."""
+    lib = _lib.load()
+
+    def expect(d, t, depth):
+        nn = t * (2 ** depth - 1)
+        fu = min(nn, d)
+        pay = nn * 8 + -(-t * 2 ** depth // 4) * 4 + -(-fu // 2) * 4
+        return 16 + -(-pay // 16) * 16
+
+    for d, t in ((256, 10), (256, 100), (64, 10), (30, 100)):
+        assert lib.dal_forest_prep_bytes(d, t, 4) == expect(d, t, 4), (d, t)
+    assert lib.dal_forest_prep_bytes(512, 100, 4) == 0 and lib.dal_forest_prep_bytes(0, 10, 4) == 0
+    assert lib.dal_forest_prep_bytes(256, 10, 17) == 0
+    p = ctypes.c_void_p(256)
+    odd = ctypes.c_void_p(264)
+    nb = lib.dal_forest_prep_bytes(256, 10, 4)
+    assert lib.dal_forest_prepare(None, p, 10, 4, 256, p, nb, None) == -1
+    assert lib.dal_forest_prepare(p, p, 10, 4, 256, odd, nb, None) == -1
+    assert lib.dal_forest_prepare(p, p, 10, 4, 256, p, nb - 16, None) == -2
+    assert lib.dal_forest_prepare(p, p, 10, 4, 0, p, nb, None) == -2
+    assert lib.dal_forest_prepare(p, p, 10, 17, 256, p, nb, None) == -3
+    assert lib.dal_forest_prepare(p, p, 100, 4, 512, p, 1 << 20, None) == -3  # not blocked: 512 runs
 
 
 def test_merge_and_mark_count_validation_without_gpu():

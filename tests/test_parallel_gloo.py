@@ -210,10 +210,10 @@ def _comm_worker(rank, world, port, q):
         # fp16-split Gram operands travel as uint16 bit patterns (no gloo type)
         u = (torch.arange(6, dtype=torch.int32) + 1000 * rank + 60000).to(torch.uint16).view(3, 2)
         g = comm.all_gather(u)
-        # the comm's reduce-scatter primitive (a global-length int64 vector)
-        acc = torch.arange(world * 4, dtype=torch.int64) * (rank + 1)
-        rs = comm.reduce_scatter_sum(acc)
-        q.put((rank, g.dtype == torch.uint16, g.to(torch.int32).numpy(), rs.numpy()))
+        # the warm step's packed top-k row (int64)
+        row = torch.arange(7, dtype=torch.int64) + 100 * rank
+        rows = comm.all_gather_rows(row)
+        q.put((rank, g.dtype == torch.uint16, g.to(torch.int32).numpy(), rows.numpy()))
     except Exception as e:
         q.put((rank, repr(e), None, None))
         raise
@@ -221,7 +221,7 @@ def _comm_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_gloo_comm_unsigned_gather_and_reduce_scatter():
+def test_gloo_comm_unsigned_gather_and_rows():
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -234,8 +234,8 @@ def test_gloo_comm_unsigned_gather_and_reduce_scatter():
         p.join(timeout=60)
         assert p.exitcode == 0
     want_g = np.concatenate([np.arange(6).reshape(3, 2) + 1000 * r + 60000 for r in range(world)])
-    full = np.arange(world * 4) * sum(r + 1 for r in range(world))
-    for rank, is_u16, g, rs in res:
+    want_rows = np.stack([np.arange(7) + 100 * r for r in range(world)])
+    for rank, is_u16, g, rows in res:
         assert is_u16 is True, is_u16
         assert np.array_equal(g, want_g)
-        assert np.array_equal(rs, full[rank * 4:(rank + 1) * 4])
+        assert np.array_equal(rows, want_rows)
