@@ -130,11 +130,19 @@ __device__ __forceinline__ void issue_fold(const ForestArgs& A, GroupFold& f,
 // WROWS (the blocked feature-major path): wave w holds rows (w / tpr) * 64 +
 // lane and walks trees w % tpr, + tpr, ...; the waves' partial votes of a row
 // are summed through LDS.
-template <bool X_LDS, bool WROWS = false, int NW = kForestWaves, int ILP = kTreeIlp>
+// BYTEA (the prepared blocked path: LDS nodes whose feature is the BYTE
+// offset slot * 256 of its run): each walk keeps its node's LDS byte address
+// a; node h of tree t sits at tb + 8 h (tb = the tree's base), so its child
+// 2h + 1 (x <= thr) or 2h + 2 sits at 2a + (8 - tb) or 2a + (16 - tb) -- one
+// select and one shift-add per level, no index arithmetic: 4 VALU per node
+// visit (x address, compare, select, shift-add) against 5, and the tree index
+// stays wave-uniform (scalar).
+template <bool X_LDS, bool WROWS = false, int NW = kForestWaves, int ILP = kTreeIlp, bool BYTEA = false>
 __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs, int xstride, int64_t tile, int R,
                                            int tpr, const int2* inner, const uint8_t* leaf, bool pre,
                                            uint8_t fl_pre, long long dens_pre, GroupFold& fold,
                                            unsigned long long (*wmin)[2][NW]) {
+  static_assert(!BYTEA || (WROWS && X_LDS), "byte-addressed walks: the blocked kernel's LDS tiles only");
   constexpr int NT = NW * 64;  // threads of the block
   const int n_inner = (1 << A.depth) - 1;
   const int n_leaf = 1 << A.depth;
@@ -149,7 +157,58 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
   const float* xrow = X_LDS ? xs + r * xstride : A.x + (live ? row : 0) * A.ldx;
 
   int v = 0;
-  if (live) {
+  if constexpr (BYTEA) {
+    typedef __attribute__((address_space(3))) const int2 lds_int2;
+    typedef __attribute__((address_space(3))) const float lds_float;
+    typedef __attribute__((address_space(3))) const uint8_t lds_u8;
+    typedef __attribute__((address_space(3))) const unsigned long long lds_u64;
+    const unsigned fbase = static_cast<unsigned>(reinterpret_cast<uintptr_t>((lds_int2*)inner));
+    const unsigned lbase = static_cast<unsigned>(reinterpret_cast<uintptr_t>((lds_u8*)leaf));
+    const unsigned xb = static_cast<unsigned>(reinterpret_cast<uintptr_t>((lds_float*)xrow));
+    const int tree0 = __builtin_amdgcn_readfirstlane(sub);  // (WROWS: the wave's tree phase)
+    auto walk_base = [&](int t) { return fbase + static_cast<unsigned>(8 * t * n_inner); };
+    // leaf byte address from the final node address: (a >> 3) + lbase + t * n_leaf - n_inner - tb / 8
+    auto leaf_off = [&](int t) {
+      return lbase + static_cast<unsigned>(t * n_leaf - n_inner) - (walk_base(t) >> 3);
+    };
+    if (live) {
+      int t = tree0;
+      for (; t + (ILP - 1) * tpr < A.n_trees; t += ILP * tpr) {
+        unsigned a[ILP], kl[ILP], kr[ILP];
+#pragma unroll
+        for (int j = 0; j < ILP; ++j) {
+          const unsigned tb = walk_base(t + j * tpr);
+          a[j] = tb;
+          kl[j] = 8u - tb;
+          kr[j] = 16u - tb;
+          // opaque to the optimiser and held in vector registers, so the step stays
+          // select + shift-add instead of shift, subtract, select, add
+          asm volatile("" : "+v"(kl[j]), "+v"(kr[j]));
+        }
+        for (int lvl = 0; lvl < A.depth; ++lvl) {
+#pragma unroll
+          for (int j = 0; j < ILP; ++j) {
+            const unsigned long long nd = *(lds_u64*)static_cast<uintptr_t>(a[j]);  // {feature run offset, thr}
+            const float xv = *(lds_float*)static_cast<uintptr_t>(xb + static_cast<unsigned>(nd));
+            a[j] = 2u * a[j] + (xv <= __uint_as_float(static_cast<unsigned>(nd >> 32)) ? kl[j] : kr[j]);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < ILP; ++j) v += *(lds_u8*)static_cast<uintptr_t>((a[j] >> 3) + leaf_off(t + j * tpr));
+      }
+      for (; t < A.n_trees; t += tpr) {
+        const unsigned tb = walk_base(t);
+        unsigned a = tb, kl = 8u - tb, kr = 16u - tb;
+        asm volatile("" : "+v"(kl), "+v"(kr));
+        for (int lvl = 0; lvl < A.depth; ++lvl) {
+          const unsigned long long nd = *(lds_u64*)static_cast<uintptr_t>(a);
+          const float xv = *(lds_float*)static_cast<uintptr_t>(xb + static_cast<unsigned>(nd));
+          a = 2u * a + (xv <= __uint_as_float(static_cast<unsigned>(nd >> 32)) ? kl : kr);
+        }
+        v += *(lds_u8*)static_cast<uintptr_t>((a >> 3) + leaf_off(t));
+      }
+    }
+  } else if (live) {
     int t = sub;
     for (; t + (ILP - 1) * tpr < A.n_trees; t += ILP * tpr) {
       int h[ILP];
@@ -431,7 +490,8 @@ __global__ __launch_bounds__(256) void pool_blocked_kernel(const float* __restri
 // (the per-block bitmap, popcounts and remap are gone).
 
 // The prepared forest (dal_forest_prepare): a 16-B header {fu, bad, nn,
-// fu_max} then the payload [nodes int2 nn (feature -> slot * kBlk) | leaves u8
+// fu_max} then the payload [nodes int2 nn (feature -> byte offset slot * kBlk * 4 of its
+// run in the LDS tile) | leaves u8
 // round4(T * 2^depth) | feature list u16 round2(fu_max)], zero-padded to 16 B:
 // the blocked kernel's LDS layout from its forest region on.
 struct BlockedPrepLayout {
@@ -575,8 +635,8 @@ __global__ __launch_bounds__(NW * 64) void forest_blocked_kernel(ForestArgs A, c
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) issue_fold<NW>(A, fold, wmin);  // after this tile's DMA wait
-    score_tile<true, true, NW, DAL_FOREST_BLOCKED_ILP>(A, xs, 1, tile, kBlk, tpr, fs, ls, true, fl_pre, dens_pre,
-                                                       fold, wmin);
+    score_tile<true, true, NW, DAL_FOREST_BLOCKED_ILP, PREP>(A, xs, 1, tile, kBlk, tpr, fs, ls, true, fl_pre,
+                                                             dens_pre, fold, wmin);
     __syncthreads();  // every wave done with the tile before the next one is staged
   }
   if (tid == 0) issue_fold<NW>(A, fold, wmin);
@@ -584,7 +644,8 @@ __global__ __launch_bounds__(NW * 64) void forest_blocked_kernel(ForestArgs A, c
 
 // dal_forest_prepare: one block builds the prepared forest (the blocked
 // kernel's per-block setup, done once): the distinct features (bitmap,
-// prefix popcounts), every node's feature as its slot * kBlk, the leaves, the
+// prefix popcounts), every node's feature as its run's byte offset slot * kBlk * 4,
+// the leaves, the
 // feature list.  A feature outside [0, d) is clamped as the unprepared kernel
 // does and counted in the header's ``bad`` word.
 constexpr int kPrepThreads = 1024;
@@ -623,7 +684,7 @@ __global__ __launch_bounds__(kPrepThreads) void forest_prepare_kernel(const int2
   uint16_t* used = reinterpret_cast<uint16_t*>(pay + L.nodes + L.leaves);
   for (int e = tid; e < nn; e += kPrepThreads) {
     int2 q = inner[e];
-    q.x = slot(q.x < 0 ? 0 : q.x >= d ? d - 1 : q.x) * kBlk;
+    q.x = slot(q.x < 0 ? 0 : q.x >= d ? d - 1 : q.x) * kBlk * 4;  // the run's byte offset in the tile
     nodes[e] = q;
   }
   for (int64_t e = tid; e < L.leaves; e += kPrepThreads) leaves[e] = e < int64_t{n_trees} * n_leaf ? leaf[e] : 0;

@@ -305,7 +305,11 @@ class ShardedSelector:
 
     def local_select(self, u_full, partials_full, unlabeled_idx, forest, k: int, mode: str = "dw",
                      strategy: str = "least_confidence", beta: float = 1.0,
-                     density_mode: str = "gram") -> LocalTopk:
+                     density_mode: str = "gram", warm: bool = None) -> LocalTopk:
+        """This rank's exact local top-k.  ``warm``: the density was cached
+        before this step (the score kernel then reads the shard's blocked
+        copy, as the single-GPU warm step does; a cold step keeps the
+        row-major kernel and builds no copy).  None: cached now."""
         from .engine import (density_error, device_lut, dw_select_local, dw_step_local, forest_score,
                              topk_keys, uncertainty_blocked)
         from .luts import ASCENDING
@@ -334,7 +338,8 @@ class ShardedSelector:
             s = sc[i - st.row_base]
         elif mode == "dw":
             # warm (density cached): the score kernel reads the shard's blocked copy, as on one GPU
-            xb = st.blocked_pool(forest) if self._density is not None else None
+            warm_now = self._density is not None if warm is None else warm
+            xb = st.blocked_pool(forest) if warm_now else None
             dens = self.local_density(u_full)
             colsum = self.global_colsum(partials_full)
             lut_dev = device_lut("entropy", forest.n_trees, st.device)
@@ -472,6 +477,7 @@ def select(sel: ShardedSelector, comm, unlabeled_idx, forest, k: int, mode: str 
     identical on every rank."""
     unl = sel.index_tensor(unlabeled_idx)
     u_full = parts_full = None
+    warm = sel._density is not None  # (a cold step's score kernel keeps the row-major pool)
     if mode == "dw":  # uncertainty sampling never normalises (no density, no zero-norm check)
         need_u = density_mode == "gram" and sel._density is None
         if need_u or sel._parts_full is None:
@@ -495,7 +501,7 @@ def select(sel: ShardedSelector, comm, unlabeled_idx, forest, k: int, mode: str 
         plan.launch(forest, unl)
         out, st = merge_row(comm, plan.packed, k, all_valid=n_unl_global >= k)
         return _finish(sel, comm, unlabeled_idx, forest, k, mode, strategy, beta, sort_fn, density_mode, out, st)
-    top = sel.local_select(u_full, parts_full, unl, forest, k, mode, strategy, beta, density_mode)
+    top = sel.local_select(u_full, parts_full, unl, forest, k, mode, strategy, beta, density_mode, warm=warm)
     # every rank's status word (zero-norm rows, re-rank capacity overflow)
     # rides in the top-k all-gather and is read once, after the merge is
     # queued: the step's one host sync, and every rank sees the same bits

@@ -74,7 +74,7 @@ class OracleShard(parallel.ShardedSelector):
         self.retries = getattr(self, "retries", 0) + 1
 
     def local_select(self, u_full, parts_full, unl, forest, k, mode="dw", strategy="least_confidence",
-                     beta=1.0, density_mode="gram"):
+                     beta=1.0, density_mode="gram", warm=None):
         keys = torch.full((k,), parallel._as_i64(0xFFFFFFFFFFFFFFFF), dtype=torch.int64)
         idx = torch.full((k,), -1, dtype=torch.int64)
         sc = torch.full((k,), float("nan"), dtype=torch.float64)
