@@ -24,7 +24,8 @@ for m in (int(a) for a in sys.argv[1:]):
     s = base.replace(old, rnd + "    }\n    uint16_t* dst = out + row")
     out = os.path.join(REPO, "ab", f"lbits_{m}")
     os.makedirs(out, exist_ok=True)
-    src = f"/tmp/gram_split_lbits_{m}.hip"
+    os.makedirs(f"/tmp/dal_lbits_{m}", exist_ok=True)  # private: no stray common.hpp beside the copy
+    src = f"/tmp/dal_lbits_{m}/gram_split.hip"
     open(src, "w").write(s)
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
                     "-I" + os.path.join(REPO, "include"), "-I" + CSRC, "-c", src, "-o",

@@ -119,7 +119,10 @@ extern "C" int dal_k3_trace_reset() {
   return hipMemcpyToSymbol(HIP_SYMBOL(dal::g_k3), z, sizeof(z)) == hipSuccess ? 0 : 1;
 }
 """
-src = "/tmp/topk_k3trace.hip"
+# a private directory: a stray common.hpp beside the copy would shadow csrc's
+# (the quoted include searches the copy's own directory first)
+os.makedirs("/tmp/dal_k3trace", exist_ok=True)
+src = "/tmp/dal_k3trace/topk.hip"
 open(src, "w").write(s)
 hipcc = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-I" + os.path.join(REPO, "include"), "-I" + CSRC]

@@ -19,7 +19,10 @@ for block in open(patch).read().split("\n=====\n"):
     s = s.replace(old, new)
 out = os.path.join(REPO, "ab", name)
 os.makedirs(out, exist_ok=True)
-tmp = f"/tmp/variant_{name}_{src_name}"
+# a private directory: a stray common.hpp beside the copy would shadow csrc's
+# (the quoted include searches the copy's own directory first)
+os.makedirs(f"/tmp/dal_variant_{name}", exist_ok=True)
+tmp = f"/tmp/dal_variant_{name}/{src_name}"
 open(tmp, "w").write(s)
 obj = os.path.join(out, src_name.replace(".hip", ".o"))
 subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",

@@ -46,7 +46,8 @@ def _forest_score_pair(cuda, X, F, density_kind, order=None, flags_unl=None):
     b = engine.forest_score(st, F, lut, flags, order, density=dens, density_err=derr, want_hi=True,
                             density_kind=kind if dens is not None else None, xb=xb)  # prepared forest (ABI v10)
     # the prepared forest itself: header {fu, bad, nodes, fu_max}, the sorted
-    # distinct features as the list, every node's feature as its slot * 64
+    # distinct features as the list, every node's feature as its run's byte
+    # offset in the LDS tile (slot * 64 rows * 4 B)
     prep = F.blocked_prep(cuda, d)
     assert prep is not None
     hdr = prep[:16].view(torch.int32).cpu().numpy()
@@ -55,7 +56,7 @@ def _forest_score_pair(cuda, X, F, density_kind, order=None, flags_unl=None):
     assert hdr[0] == feats.size and hdr[1] == 0 and hdr[2] == nn and hdr[3] >= feats.size
     pay = prep[16:].cpu().numpy()
     nodes = pay[:nn * 8].view(np.int32).reshape(-1, 2)
-    assert np.array_equal(nodes[:, 0], np.searchsorted(feats, F.inner[..., 0].reshape(-1)) * 64)
+    assert np.array_equal(nodes[:, 0], np.searchsorted(feats, F.inner[..., 0].reshape(-1)) * 256)
     assert np.array_equal(nodes[:, 1], F.inner[..., 1].reshape(-1))
     lb = -(-F.leaf.size // 4) * 4
     assert np.array_equal(pay[nn * 8:nn * 8 + F.leaf.size], F.leaf.reshape(-1))
