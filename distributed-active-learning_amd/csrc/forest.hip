@@ -130,13 +130,60 @@ __device__ __forceinline__ void issue_fold(const ForestArgs& A, GroupFold& f,
 // WROWS (the blocked feature-major path): wave w holds rows (w / tpr) * 64 +
 // lane and walks trees w % tpr, + tpr, ...; the waves' partial votes of a row
 // are summed through LDS.
+// Byte-addressed walks of M trees (t, t + tpr, ...) at once for one row
+// (score_tile BYTEA): node h of tree t sits at LDS byte tb + 8 h, so its
+// child 2h + 1 (x <= thr) or 2h + 2 sits at 2a + (8 - tb) or 2a + (16 - tb)
+// -- a select and a shift-add per level; the leaf byte at (a >> 3) + lbase +
+// t * n_leaf - n_inner - tb / 8.  Returns the M trees' summed votes.
+struct ByteWalk {
+  unsigned fbase, lbase, xb;  // LDS byte addresses: nodes, leaves, this row's x
+  int tpr, n_inner, n_leaf, depth;
+};
+template <int M>
+__device__ __forceinline__ int walk_group(const ByteWalk& W, int t) {
+  typedef __attribute__((address_space(3))) const float lds_float;
+  typedef __attribute__((address_space(3))) const uint8_t lds_u8;
+  typedef __attribute__((address_space(3))) const unsigned long long lds_u64;
+  unsigned a[M], kl[M], kr[M], lo[M];
+#pragma unroll
+  for (int j = 0; j < M; ++j) {
+    const int tj = t + j * W.tpr;
+    const unsigned tb = W.fbase + static_cast<unsigned>(8 * tj * W.n_inner);
+    a[j] = tb;
+    kl[j] = 8u - tb;
+    kr[j] = 16u - tb;
+    lo[j] = W.lbase + static_cast<unsigned>(tj * W.n_leaf - W.n_inner) - (tb >> 3);
+    // opaque to the optimiser and held in vector registers, so the step stays
+    // select + shift-add instead of shift, subtract, select, add
+    asm volatile("" : "+v"(kl[j]), "+v"(kr[j]));
+  }
+  for (int lvl = 0; lvl < W.depth; ++lvl) {
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      const unsigned long long nd = *(lds_u64*)static_cast<uintptr_t>(a[j]);  // {feature run offset, thr}
+      const float xv = *(lds_float*)static_cast<uintptr_t>(W.xb + static_cast<unsigned>(nd));
+      a[j] = 2u * a[j] + (xv <= __uint_as_float(static_cast<unsigned>(nd >> 32)) ? kl[j] : kr[j]);
+    }
+  }
+  int v = 0;
+#pragma unroll
+  for (int j = 0; j < M; ++j) v += *(lds_u8*)static_cast<uintptr_t>((a[j] >> 3) + lo[j]);
+  return v;
+}
+// the last rem (< ILP) trees of a wave as one group (rem wave-uniform)
+template <int M>
+__device__ __forceinline__ int walk_tail(const ByteWalk& W, int t, int rem) {
+  if constexpr (M == 0) {
+    return 0;
+  } else {
+    return rem == M ? walk_group<M>(W, t) : walk_tail<M - 1>(W, t, rem);
+  }
+}
+
 // BYTEA (the prepared blocked path: LDS nodes whose feature is the BYTE
-// offset slot * 256 of its run): each walk keeps its node's LDS byte address
-// a; node h of tree t sits at tb + 8 h (tb = the tree's base), so its child
-// 2h + 1 (x <= thr) or 2h + 2 sits at 2a + (8 - tb) or 2a + (16 - tb) -- one
-// select and one shift-add per level, no index arithmetic: 4 VALU per node
-// visit (x address, compare, select, shift-add) against 5, and the tree index
-// stays wave-uniform (scalar).
+// offset slot * 256 of its run): walk_group -- 4 VALU per node visit (x
+// address, compare, select, shift-add) against 5, the tree index
+// wave-uniform (scalar), and a wave's last trees walked together.
 template <bool X_LDS, bool WROWS = false, int NW = kForestWaves, int ILP = kTreeIlp, bool BYTEA = false>
 __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs, int xstride, int64_t tile, int R,
                                            int tpr, const int2* inner, const uint8_t* leaf, bool pre,
@@ -161,51 +208,16 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
     typedef __attribute__((address_space(3))) const int2 lds_int2;
     typedef __attribute__((address_space(3))) const float lds_float;
     typedef __attribute__((address_space(3))) const uint8_t lds_u8;
-    typedef __attribute__((address_space(3))) const unsigned long long lds_u64;
-    const unsigned fbase = static_cast<unsigned>(reinterpret_cast<uintptr_t>((lds_int2*)inner));
-    const unsigned lbase = static_cast<unsigned>(reinterpret_cast<uintptr_t>((lds_u8*)leaf));
-    const unsigned xb = static_cast<unsigned>(reinterpret_cast<uintptr_t>((lds_float*)xrow));
-    const int tree0 = __builtin_amdgcn_readfirstlane(sub);  // (WROWS: the wave's tree phase)
-    auto walk_base = [&](int t) { return fbase + static_cast<unsigned>(8 * t * n_inner); };
-    // leaf byte address from the final node address: (a >> 3) + lbase + t * n_leaf - n_inner - tb / 8
-    auto leaf_off = [&](int t) {
-      return lbase + static_cast<unsigned>(t * n_leaf - n_inner) - (walk_base(t) >> 3);
-    };
+    const ByteWalk W{static_cast<unsigned>(reinterpret_cast<uintptr_t>((lds_int2*)inner)),
+                     static_cast<unsigned>(reinterpret_cast<uintptr_t>((lds_u8*)leaf)),
+                     static_cast<unsigned>(reinterpret_cast<uintptr_t>((lds_float*)xrow)), tpr, n_inner, n_leaf,
+                     A.depth};
     if (live) {
-      int t = tree0;
-      for (; t + (ILP - 1) * tpr < A.n_trees; t += ILP * tpr) {
-        unsigned a[ILP], kl[ILP], kr[ILP];
-#pragma unroll
-        for (int j = 0; j < ILP; ++j) {
-          const unsigned tb = walk_base(t + j * tpr);
-          a[j] = tb;
-          kl[j] = 8u - tb;
-          kr[j] = 16u - tb;
-          // opaque to the optimiser and held in vector registers, so the step stays
-          // select + shift-add instead of shift, subtract, select, add
-          asm volatile("" : "+v"(kl[j]), "+v"(kr[j]));
-        }
-        for (int lvl = 0; lvl < A.depth; ++lvl) {
-#pragma unroll
-          for (int j = 0; j < ILP; ++j) {
-            const unsigned long long nd = *(lds_u64*)static_cast<uintptr_t>(a[j]);  // {feature run offset, thr}
-            const float xv = *(lds_float*)static_cast<uintptr_t>(xb + static_cast<unsigned>(nd));
-            a[j] = 2u * a[j] + (xv <= __uint_as_float(static_cast<unsigned>(nd >> 32)) ? kl[j] : kr[j]);
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < ILP; ++j) v += *(lds_u8*)static_cast<uintptr_t>((a[j] >> 3) + leaf_off(t + j * tpr));
-      }
-      for (; t < A.n_trees; t += tpr) {
-        const unsigned tb = walk_base(t);
-        unsigned a = tb, kl = 8u - tb, kr = 16u - tb;
-        asm volatile("" : "+v"(kl), "+v"(kr));
-        for (int lvl = 0; lvl < A.depth; ++lvl) {
-          const unsigned long long nd = *(lds_u64*)static_cast<uintptr_t>(a);
-          const float xv = *(lds_float*)static_cast<uintptr_t>(xb + static_cast<unsigned>(nd));
-          a = 2u * a + (xv <= __uint_as_float(static_cast<unsigned>(nd >> 32)) ? kl : kr);
-        }
-        v += *(lds_u8*)static_cast<uintptr_t>((a >> 3) + leaf_off(t));
+      // groups of ILP trees, then the wave's last trees as ONE group of their
+      // count (T = 10 over 4 waves: 3 or 2 walks in flight, not one at a time)
+      for (int t = __builtin_amdgcn_readfirstlane(sub); t < A.n_trees; t += ILP * tpr) {  // (wave-uniform)
+        const int rem = (A.n_trees - t + tpr - 1) / tpr;
+        v += rem >= ILP ? walk_group<ILP>(W, t) : walk_tail<ILP - 1>(W, t, rem);
       }
     }
   } else if (live) {
@@ -507,6 +519,14 @@ __host__ __device__ inline BlockedPrepLayout blocked_prep_layout(int64_t n_trees
   return L;
 }
 
+// The prepared forest's tree walks by LDS byte address (score_tile BYTEA; 1)
+// or by heap index like the unprepared kernel (0).  The prepared node format
+// follows: a byte offset of the feature's run, or its float index.
+#ifndef DAL_FOREST_BYTEA
+#define DAL_FOREST_BYTEA 1
+#endif
+constexpr bool kByteWalk = DAL_FOREST_BYTEA != 0;
+
 template <int NW, bool PREP>
 __global__ __launch_bounds__(NW * 64) void forest_blocked_kernel(ForestArgs A, const float* __restrict__ xb,
                                                                  const unsigned char* __restrict__ prep,
@@ -635,8 +655,8 @@ __global__ __launch_bounds__(NW * 64) void forest_blocked_kernel(ForestArgs A, c
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) issue_fold<NW>(A, fold, wmin);  // after this tile's DMA wait
-    score_tile<true, true, NW, DAL_FOREST_BLOCKED_ILP, PREP>(A, xs, 1, tile, kBlk, tpr, fs, ls, true, fl_pre,
-                                                             dens_pre, fold, wmin);
+    score_tile<true, true, NW, DAL_FOREST_BLOCKED_ILP, PREP && kByteWalk>(A, xs, 1, tile, kBlk, tpr, fs, ls, true,
+                                                                          fl_pre, dens_pre, fold, wmin);
     __syncthreads();  // every wave done with the tile before the next one is staged
   }
   if (tid == 0) issue_fold<NW>(A, fold, wmin);
@@ -684,7 +704,7 @@ __global__ __launch_bounds__(kPrepThreads) void forest_prepare_kernel(const int2
   uint16_t* used = reinterpret_cast<uint16_t*>(pay + L.nodes + L.leaves);
   for (int e = tid; e < nn; e += kPrepThreads) {
     int2 q = inner[e];
-    q.x = slot(q.x < 0 ? 0 : q.x >= d ? d - 1 : q.x) * kBlk * 4;  // the run's byte offset in the tile
+    q.x = slot(q.x < 0 ? 0 : q.x >= d ? d - 1 : q.x) * kBlk * (kByteWalk ? 4 : 1);  // the run's byte (float) offset
     nodes[e] = q;
   }
   for (int64_t e = tid; e < L.leaves; e += kPrepThreads) leaves[e] = e < int64_t{n_trees} * n_leaf ? leaf[e] : 0;

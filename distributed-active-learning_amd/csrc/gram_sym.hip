@@ -894,6 +894,9 @@ int launch_csym_w(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint
   return DAL_OK;
 }
 
+#ifndef DAL_GRAM_CONTIG_MB
+#define DAL_GRAM_CONTIG_MB 32  // column operands up to this size take the contiguous schedule
+#endif
 template <int KS>
 int launch_csym(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint16_t* cols, int64_t jcol0,
                 int64_t j_lo, int64_t j_hi, int64_t skip_lo, int64_t skip_hi, int64_t ns_active, int64_t ldh,
@@ -902,7 +905,7 @@ int launch_csym(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint16
   // operand (<= 32 MB: 100k x 64 is 2-5 % faster), else round-robin column
   // chunks whose blocks sweep the same column stages together.  Exact integer
   // accumulation: the schedule never changes the bits.
-  const int contig = (j_hi - j_lo) * 256 * ldh * 2 <= (int64_t{32} << 20);
+  const int contig = (j_hi - j_lo) * 256 * ldh * 2 <= (int64_t{DAL_GRAM_CONTIG_MB} << 20);
   if constexpr ((KS == 128 && DAL_GRAM_WAVES8) || (KS == 64 && DAL_GRAM_W8_KS64))
     if (!contig)
       return launch_csym_w<KS, 8>(rows, srow0, n_srb, cols, jcol0, j_lo, j_hi, skip_lo, skip_hi, ns_active, ldh,
