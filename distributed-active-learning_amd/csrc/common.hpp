@@ -90,6 +90,22 @@ __device__ __forceinline__ double row_sq_norm_bf16(const uint16_t* __restrict__ 
   return s;
 }
 
+// Row-group minima of the optimistic keys carry a row hint in their low
+// kHintBits bits: (key & ~kHintMask) | (row offset in the group), so the
+// select kernel can prefetch each group's best row before tau is known (its
+// canonical re-rank then reads that row from L2).  The selection tests the
+// masked key (m & ~kHintMask) <= tau: implied by the exact minimum <= tau, so
+// the candidate set stays a superset; the offset is capped below the mask so
+// a packed key never reads DAL_KEY_NONE.
+constexpr int kHintBits = 24;
+constexpr unsigned long long kHintMask = (1ull << kHintBits) - 1ull;
+__device__ __forceinline__ unsigned long long pack_hint(unsigned long long key, long long off) {
+  if (key == DAL_KEY_NONE) return key;
+  const unsigned long long o = off < static_cast<long long>(kHintMask) ? static_cast<unsigned long long>(off)
+                                                                        : kHintMask - 1ull;
+  return (key & ~kHintMask) | o;
+}
+
 // Internal hooks of dal_dw_step into dal_forest_score's kernel (forest.hip):
 //   status_reset (nullable) is zeroed by the first thread, before any later
 //                kernel of the step can raise a flag (a replayed step starts clean);
@@ -102,7 +118,8 @@ __device__ __forceinline__ double row_sq_norm_bf16(const uint16_t* __restrict__ 
 //                per-step copy of the base flags;
 //   gmin         (nullable; the fast level 1 of the top-k, topk.hip) block b
 //                folds the minimum (pessimistic, optimistic) keys of its rows
-//                into group g = b / group_blocks: gmin[g] / gmin[n_groups + g],
+//                into group g = b / group_blocks: gmin[g] / gmin[n_groups + g]
+//                (the optimistic one with its row hint, pack_hint),
 //                stored inverted (~key, so a zero word reads DAL_KEY_NONE) --
 //                a plain store when group_blocks == 1, else an atomic max on a
 //                buffer the top-k leaves zero.

@@ -284,6 +284,8 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
     if (A.keys_hi) A.keys_hi[row] = khi;
   }
   if (!A.hooks.gmin) return;  // kernel-uniform
+  // the optimistic key carries the row's offset in its group (the select's prefetch hint)
+  khi = pack_hint(khi, static_cast<long long>(tile % A.hooks.group_blocks) * R + r);
   // the block's minimum keys -> its row group (the top-k's fast level 1);
   // with rows on wave lanes (wr) only the row leaders' wave (sub 0) holds keys
   if (!wr || sub == 0) {  // (wave-uniform)

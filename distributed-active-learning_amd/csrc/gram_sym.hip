@@ -138,6 +138,9 @@ __device__ __forceinline__ unsigned fresh_lane() {
 #ifndef DAL_GRAM_W8_KS64
 #define DAL_GRAM_W8_KS64 0  // KS 64 in the 8-wave two-super-block form (round robin schedule only)
 #endif
+#ifndef DAL_GRAM_W8_OCC64
+#define DAL_GRAM_W8_OCC64 1  // 8-wave KS-64 blocks per CU (128 VGPRs, 72 KiB of LDS: two fit)
+#endif
 #ifndef DAL_GRAM_KS32_OCC
 #define DAL_GRAM_KS32_OCC 5  // KS 32: 4-wave blocks per CU (3: 16 KiB stages; >= 4: 8 KiB stages. Config 3: 2 -> 3 -> 4 blocks 3.944 -> 3.827 -> 3.745 ms; row sums only (94 VGPRs): 4 -> 5 blocks 3.430 -> 3.391 ms)
 #endif
@@ -150,7 +153,8 @@ struct Cfg {
   static constexpr int SLOTS = ROWB / 16;           // 16-B slots per row
   static constexpr int HI = KS / 8;                 // slots of the H part
   // three 4-wave blocks per CU at KS 64 (OCC3): 16 KiB stages so three fit the LDS
-  static constexpr int OCC = W == 8 ? 1 : KS == 32 ? DAL_GRAM_KS32_OCC : KS == 64 ? DAL_GRAM_KS64_OCC : 2;
+  static constexpr int OCC = W == 8 ? (KS == 64 ? DAL_GRAM_W8_OCC64 : 1)
+                                    : KS == 32 ? DAL_GRAM_KS32_OCC : KS == 64 ? DAL_GRAM_KS64_OCC : 2;
   static constexpr int STAGE = W == 8 ? DAL_GRAM_STAGE8 : OCC >= 4 ? 8192 : OCC == 3 ? 16384 : 32768;  // bytes per LDS stage
   static constexpr int SC = STAGE / ROWB;           // columns per stage: 64 / 128 / 256
   static constexpr int SPP = 256 / SC;              // stages per 512 x 256 pair: 4 / 2 / 1
@@ -869,7 +873,7 @@ int launch_csym_w(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint
   // grid_blocks counts 4-wave blocks (two per CU); 8-wave blocks are one per CU
   constexpr int kOcc = Cfg<KS, W>::OCC;
   const int G0 = W == 4 ? (grid_blocks > 0 ? grid_blocks * kOcc / 2 : kOcc * device_cus())
-                        : (grid_blocks > 0 ? grid_blocks : 2 * device_cus()) * 4 / W;
+                        : (grid_blocks > 0 ? grid_blocks : 2 * device_cus()) * 4 / W * kOcc;
   const int64_t nj = j_hi - j_lo;
   int64_t cbk = nj, n_chunks = 1, G;
   if (contig) {

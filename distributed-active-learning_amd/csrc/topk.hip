@@ -597,6 +597,37 @@ __device__ __forceinline__ bool dw_canonical_score_lane(const DwRerank& R, int64
   return true;
 }
 
+// Prefetch of a candidate row's re-rank inputs into L2 (and the TLB) by
+// LDS-DMA loads whose landing slots nobody reads: every 64-B piece of x's row,
+// norm64, the vote and the row flags (or the plan's base flags and stamp).
+// One lane per row; a wave issues its lanes' loads together (64-bit
+// addresses, no VGPR results: nothing waits for them).
+__device__ __forceinline__ void lds_dma_dword(const void* p, unsigned* slots) {
+  typedef __attribute__((address_space(3))) unsigned lds_u32;
+  const unsigned dst = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(reinterpret_cast<uintptr_t>((lds_u32*)slots)));
+  const unsigned long long a = reinterpret_cast<uintptr_t>(p) & ~3ull;
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(a), "s"(dst)
+      : "memory");
+}
+__device__ __forceinline__ void prefetch_row(const DwRerank& R, int64_t i, unsigned* slots) {
+  const char* xr = reinterpret_cast<const char*>(R.x + i * R.ldx);
+  const int bytes = R.d * 4;
+  for (int b = 0; b < bytes; b += 64) lds_dma_dword(xr + b, slots);  // (d uniform: every lane the same count)
+  lds_dma_dword(R.norm64 + i, slots);
+  lds_dma_dword(R.votes + i, slots);
+  if (R.base_flags) {
+    lds_dma_dword(R.base_flags + i, slots);
+    lds_dma_dword(R.stamp + i, slots);
+  } else if (R.flags) {
+    lds_dma_dword(R.flags + i, slots);
+  }
+}
+
 // Re-rank target of summary_select_kernel's density-weighted form.
 struct AppendRerank {
   DwRerank R;
@@ -1441,7 +1472,14 @@ struct GroupSummary {
 #ifndef DAL_TAU_BUCKET
 #define DAL_TAU_BUCKET 64  // radix passes stop once the k-th key's bucket holds at most this many minima (256 / 1024: neutral)
 #endif
-__device__ unsigned long long group_threshold(const GroupSummary& S, int64_t k) {
+struct NoHook {
+  __device__ void operator()() const {}
+};
+// after_load: called by every thread once the minima are in registers (their
+// loads waited for), before the radix passes -- the select kernel issues its
+// prefetches there, to land while tau is computed.
+template <class Hook = NoHook>
+__device__ unsigned long long group_threshold(const GroupSummary& S, int64_t k, const Hook& after_load = Hook{}) {
   constexpr int PER = kMaxGroups / kSumThreads;
   constexpr int W = kSumThreads / 64;
   __shared__ unsigned int hist[256];
@@ -1479,6 +1517,7 @@ __device__ unsigned long long group_threshold(const GroupSummary& S, int64_t k) 
   // first pass) and then by the scanning wave as it reads each pass's bins:
   // two barriers per pass instead of three
   if (tid < 256) hist[tid] = 0u;
+  after_load();
   __syncthreads();
   nv = 0;
 #pragma unroll
@@ -1566,7 +1605,7 @@ __global__ __launch_bounds__(256) void group_min_kernel(const uint64_t* __restri
     const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + tid;
     if (i < n) {
       lo = keys_lo[i];
-      hi = keys_hi[i];
+      hi = pack_hint(keys_hi[i], i % group_rows);
     }
     for (int o = 1; o < group_rows; o <<= 1) {
       const unsigned long long a = __shfl_xor(lo, o), c = __shfl_xor(hi, o);
@@ -1595,8 +1634,9 @@ __global__ __launch_bounds__(256) void group_min_kernel(const uint64_t* __restri
     }
 #pragma unroll
     for (int j = 0; j < kIlp; ++j) {
+      const unsigned long long cj = pack_hint(c[j], b + j * 64 + lane - r0);
       lo = a[j] < lo ? a[j] : lo;
-      hi = c[j] < hi ? c[j] : hi;
+      hi = cj < hi ? cj : hi;
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -1648,20 +1688,32 @@ __global__ __launch_bounds__(kSumThreads) void summary_select_kernel(
   __shared__ long long s_li[DW ? kLocalSort : 1];
   __shared__ double s_lp[DW ? kLocalSort : 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const unsigned long long tau = group_threshold(S, k);
-  if (blockIdx.x == 0 && tid == 0) h->kstar = tau;
   const int64_t per = ceil_div(S.ng, static_cast<int64_t>(gridDim.x));
   const int64_t g0 = static_cast<int64_t>(blockIdx.x) * per;
   const int64_t g1 = g0 + per < S.ng ? g0 + per : S.ng;
+  // this block's groups' optimistic minima (<= 128: one per thread), loaded
+  // with tau's inputs; DW: each one's hinted row (its offset in the group,
+  // pack_hint) is prefetched while tau is computed -- the candidates are
+  // nearly always those rows, and their canonical re-rank then reads them
+  // from L2 (the warm plan's score kernel never touches the row-major pool)
+  const unsigned long long my_m = tid < g1 - g0 ? ~S.ginv[S.ng + g0 + tid] : DAL_KEY_NONE;
+  __shared__ __attribute__((aligned(16))) unsigned s_pf[DW ? 64 : 1];  // the prefetch DMA's landing slots (never read)
+  auto prefetch = [&]() {
+    if constexpr (DW) {
+      const int64_t off = static_cast<int64_t>(my_m & kHintMask);
+      const int64_t row = (g0 + tid) * S.group_rows + off;
+      if (my_m != DAL_KEY_NONE && off < S.group_rows && row < n) prefetch_row(AR.R, row, s_pf);
+    }
+  };
+  const unsigned long long tau = group_threshold(S, k, prefetch);
+  if (blockIdx.x == 0 && tid == 0) h->kstar = tau;
   if (tid == 0) {
     s_nh = 0u;
     s_nc = 0u;
   }
   __syncthreads();
-  for (int64_t g = g0 + tid; g < g1; g += kSumThreads) {
-    const unsigned long long m = ~S.ginv[S.ng + g];
-    if (m <= tau && m != DAL_KEY_NONE) s_hits[atomicAdd(&s_nh, 1u)] = static_cast<int>(g);
-  }
+  if ((my_m & ~kHintMask) <= tau && my_m != DAL_KEY_NONE)  // (masked: the exact minimum <= tau implies it)
+    s_hits[atomicAdd(&s_nh, 1u)] = static_cast<int>(g0 + tid);
   __syncthreads();
   const int nh = static_cast<int>(s_nh);
   const unsigned long long lt_mask = (1ull << lane) - 1ull;

@@ -4,7 +4,7 @@ libdal.so: AB_BASE (default ab/k3_base/libdal.so) and the in-tree library,
 switched by rebinding dal._lib between calls.  Per shape: selections
 (indices + fp64 score bits) must be identical; then back-to-back calls
 between two HIP events, interleaved A/B, median of the rounds.
-usage: python scripts/k3_lib_ab.py [NxD[xT][:kK] ...]"""
+usage: python scripts/k3_lib_ab.py [--base PATH] [NxD[xT][:kK] ...]"""
 import ctypes
 import os
 import statistics
@@ -33,10 +33,13 @@ def bind(path):
     return lib
 
 
-libs = {"base": bind(os.environ.get("AB_BASE", os.path.join(REPO, "ab", "k3_base", "libdal.so"))),
-        "new": bind(_lib.LIB_PATH)}
+args = sys.argv[1:]
+base = os.environ.get("AB_BASE", os.path.join(REPO, "ab", "k3_base", "libdal.so"))
+if args[:1] == ["--base"]:  # (instead of AB_BASE)
+    base, args = args[1] if os.path.isabs(args[1]) else os.path.join(REPO, args[1]), args[2:]
+libs = {"base": bind(base), "new": bind(_lib.LIB_PATH)}
 dev = torch.device("cuda:0")
-for spec in sys.argv[1:] or ["100000x64", "2000000x256", "284807x30x100", "2000000x256:k1000"]:
+for spec in args or ["100000x64", "2000000x256", "284807x30x100", "2000000x256:k1000"]:
     sh, _, kk = spec.partition(":k")
     K = int(kk) if kk else 100
     parts = [int(v) for v in sh.split("x")]

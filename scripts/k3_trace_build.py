@@ -37,9 +37,11 @@ def sub(old, new, last=False):
 sub("struct TopkHdr {", """__device__ unsigned long long g_k3[1024];
 #define K3T(slot) do { if (threadIdx.x == 0) g_k3[slot] = __builtin_amdgcn_s_memrealtime(); } while (0)
 struct TopkHdr {""")
-sub("""  const unsigned long long tau = group_threshold(S, k);
-  if (blockIdx.x == 0 && tid == 0) h->kstar = tau;""", """  if (blockIdx.x == 0) K3T(0);
-  const unsigned long long tau = group_threshold(S, k);
+TAU = ("group_threshold(S, k, prefetch)" if "group_threshold(S, k, prefetch)" in s
+       else "group_threshold(S, k)")  # (round 6: the hinted rows' prefetch runs inside tau)
+sub(f"""  const unsigned long long tau = {TAU};
+  if (blockIdx.x == 0 && tid == 0) h->kstar = tau;""", f"""  if (blockIdx.x == 0) K3T(0);
+  const unsigned long long tau = {TAU};
   if (blockIdx.x == 0) K3T(1);
   if (blockIdx.x == 0 && tid == 0) h->kstar = tau;""")
 sub("""  const int nh = static_cast<int>(s_nh);""", """  const int nh = static_cast<int>(s_nh);

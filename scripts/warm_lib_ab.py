@@ -4,7 +4,8 @@ libdal.so: AB_BASE (default: the in-tree library) and AB_NEW, switched by
 rebinding dal._lib; one PoolState per library (each computes its density
 once).  Selections (indices + fp64 score bits) must be identical; then
 interleaved wall timing of warm steps (host included, as a user runs them).
-usage: AB_NEW=path python scripts/warm_lib_ab.py [CONFIG ...]"""
+usage: AB_NEW=path python scripts/warm_lib_ab.py [CONFIG ...]
+       python scripts/warm_lib_ab.py --base PATH --new PATH [CONFIG ...]"""
 import ctypes
 import os
 import statistics
@@ -31,9 +32,14 @@ def bind(path):
     return lib
 
 
-libs = {"base": bind(os.environ.get("AB_BASE", _lib.LIB_PATH)), "new": bind(os.environ["AB_NEW"])}
+args = sys.argv[1:]
+paths = {"base": os.environ.get("AB_BASE", _lib.LIB_PATH), "new": os.environ.get("AB_NEW")}
+while args[:1] in (["--base"], ["--new"]):
+    paths[args[0][2:]] = args[1] if os.path.isabs(args[1]) else os.path.join(REPO, args[1])
+    args = args[2:]
+libs = {name: bind(path) for name, path in paths.items()}
 dev = torch.device("cuda:0")
-for c in sys.argv[1:] or ["4", "2"]:
+for c in args or ["4", "2"]:
     cfg = bench.CONFIGS[c]
     n, d, trees, dist = cfg["n"], cfg["d"], cfg["trees"], cfg["dist"]
     x = bench.upload(bench.host_pool(0, n, d, dist), dev)
