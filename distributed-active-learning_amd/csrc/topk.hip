@@ -1031,6 +1031,11 @@ __device__ bool select_compact(const uint64_t* __restrict__ keys, const int64_t*
 }
 
 // The sort tail as a block-level device function (kSortThreads threads): the
+// The rank selection's lanes per element stop doubling once FILL x lanes x m
+// would exceed the block (2: at most half the threads busy).
+#ifndef DAL_K3_RANK_FILL
+#define DAL_K3_RANK_FILL 2
+#endif
 // body of sort_kernel, also run by the last block of summary_select_kernel.
 template <bool PAY>
 __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t* __restrict__ idx,
@@ -1300,7 +1305,7 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
     double* const ds = reinterpret_cast<double*>(s_dest[1]);
     const int64_t kk = k < m ? k : m;
     int tpe = 1;  // lanes per element: a power of two <= 64, tpe * m <= kSortThreads
-    while (tpe < 64 && 2 * tpe * m <= kSortThreads) tpe <<= 1;
+    while (tpe < 64 && DAL_K3_RANK_FILL * tpe * m <= kSortThreads) tpe <<= 1;
     const int part = tid & (tpe - 1);
     for (int e0 = 0; e0 < m; e0 += kSortThreads / tpe) {  // block-uniform
       const int e = e0 + tid / tpe;
