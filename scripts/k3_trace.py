@@ -45,11 +45,13 @@ for it in range(30):
     rows.append(((t[10] - t0) / 100, (t[11] - t0) / 100, t[13], (t[1] - t0) / 100, (t[2] - t0) / 100, (min(arr) - t0) / 100, (max(arr) - t0) / 100,
                  (t[3] - t0) / 100, (t[7] - t0) / 100, (t[8] - t0) / 100, (t[9] - t0) / 100, (t[6] - t0) / 100,
                  t[4], G, sum(t[512 + b] for b in range(G)), t[20] / 100, t[21] / 100, t[22] / 100, t[23],
-                 (t[14] - t0) / 100, (t[16] - t0) / 100, (t[17] - t0) / 100, t[15]))
+                 (t[14] - t0) / 100, (t[16] - t0) / 100, (t[17] - t0) / 100, t[15],
+                 t[24] / 100, t[25] / 100, t[26] / 100))
     lib.dal_k3_trace_reset()
 print(f"{n}x{d} T={trees} k={k} level1_fast={st.level1_fast} (us from block 0's start; medians of 30)")
 names = ["minmax", "passes_done", "bucket", "tau", "hits", "first_arrive", "last_arrive", "sort_start", "sort_read_hdr", "sort_loaded", "sort_ranked",
          "end", "cands", "grid", "hit_groups", "max_scan", "max_score", "max_store_drain", "max_block_cands",
-         "rank_cleared", "sel_compacted", "sel_sorted", "sel_m"]
+         "rank_cleared", "sel_compacted", "sel_sorted", "sel_m",
+         "max_sc_loads", "max_sc_divs", "max_sc_sum"]  # (the last three: K3_TRACE_SCORE=1 builds only)
 for j, nm in enumerate(names):
     print(f"  {nm:13s} {statistics.median(r[j] for r in rows[5:]):9.2f}")

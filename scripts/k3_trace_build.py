@@ -22,6 +22,10 @@ RANK = os.environ.get("K3_TRACE_PATH") == "rank"
 # K3_TRACE_PATH=select: stamps 8 / 9 after the radix pre-selection and after
 # the bitonic sort of the long-list path (config 3), slot 15 the compacted count
 SELECT = os.environ.get("K3_TRACE_PATH") == "select"
+# K3_TRACE_SCORE=1 (with any path): the whole-wave canonical score split in three (max over
+# calls, the stamps' waits and atomics included): slot 24 its inputs' loads, 25 the
+# divisions, 26 the sequential sum
+SCORE = os.environ.get("K3_TRACE_SCORE") == "1"
 
 
 def sub(old, new, last=False):
@@ -37,8 +41,8 @@ def sub(old, new, last=False):
 sub("struct TopkHdr {", """__device__ unsigned long long g_k3[1024];
 #define K3T(slot) do { if (threadIdx.x == 0) g_k3[slot] = __builtin_amdgcn_s_memrealtime(); } while (0)
 struct TopkHdr {""")
-TAU = ("group_threshold(S, k, prefetch)" if "group_threshold(S, k, prefetch)" in s
-       else "group_threshold(S, k)")  # (round 6: the hinted rows' prefetch runs inside tau)
+TAU = next(t for t in ("group_threshold(S, k, stage_issue, stage_rows)", "group_threshold(S, k, prefetch)",
+                       "group_threshold(S, k)") if t in s)  # (round 6: the hinted rows' staging runs inside tau)
 sub(f"""  const unsigned long long tau = {TAU};
   if (blockIdx.x == 0 && tid == 0) h->kstar = tau;""", f"""  if (blockIdx.x == 0) K3T(0);
   const unsigned long long tau = {TAU};
@@ -121,6 +125,62 @@ extern "C" int dal_k3_trace_reset() {
   return hipMemcpyToSymbol(HIP_SYMBOL(dal::g_k3), z, sizeof(z)) == hipSuccess ? 0 : 1;
 }
 """
+if SCORE:
+    sub("""  const uint8_t fl = rerank_flag(R, i);
+  const double nr = R.norm64[i];
+  const int v = R.votes[i];
+  const float* xr = R.x + i * R.ldx;
+  double acc = 0.0;
+  for (int f0 = 0; f0 < R.d; f0 += 64 * kC) {
+    double p[kC];
+#pragma unroll
+    for (int c = 0; c < kC; ++c) {
+      const int f = f0 + 64 * c + lane;
+      p[c] = f < R.d ? (static_cast<double>(xr[f]) / nr) * R.colsum[f] : 0.0;
+    }""", """  const unsigned long long t_s = __builtin_amdgcn_s_memrealtime();
+  unsigned long long t_l = 0, t_p = 0;
+  const uint8_t fl = rerank_flag(R, i);
+  const double nr = R.norm64[i];
+  const int v = R.votes[i];
+  const float* xr = R.x + i * R.ldx;
+  double acc = 0.0;
+  for (int f0 = 0; f0 < R.d; f0 += 64 * kC) {
+    double p[kC];
+    float xv[kC];
+    double cs[kC];
+#pragma unroll
+    for (int c = 0; c < kC; ++c) {
+      const int f = f0 + 64 * c + lane;
+      xv[c] = f < R.d ? xr[f] : 0.f;
+      cs[c] = f < R.d ? R.colsum[f] : 0.0;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::"v"(xv[0]), "v"(cs[0]), "v"(nr), "v"(v), "v"(static_cast<int>(fl)) : "memory");
+    if (f0 == 0) t_l = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+    for (int c = 0; c < kC; ++c) {
+      const int f = f0 + 64 * c + lane;
+      p[c] = f < R.d ? (static_cast<double>(xv[c]) / nr) * cs[c] : 0.0;
+    }
+    asm volatile("" ::"v"(p[0]), "v"(p[kC - 1]));
+    if (f0 == 0) t_p = __builtin_amdgcn_s_memrealtime();""")
+    sub("""  if (!(fl & DAL_ROW_CANDIDATE)) {
+    s = __builtin_nan("");
+    return false;
+  }
+  if (fl & DAL_ROW_EXCLUDED) acc = __builtin_nan("");
+  // n_lut > 0""", """  asm volatile("" ::"v"(acc));
+  if ((threadIdx.x & 63) == 0) {
+    const unsigned long long t_c = __builtin_amdgcn_s_memrealtime();
+    atomicMax(&g_k3[24], t_l - t_s);
+    atomicMax(&g_k3[25], t_p - t_l);
+    atomicMax(&g_k3[26], t_c - t_p);
+  }
+  if (!(fl & DAL_ROW_CANDIDATE)) {
+    s = __builtin_nan("");
+    return false;
+  }
+  if (fl & DAL_ROW_EXCLUDED) acc = __builtin_nan("");
+  // n_lut > 0""")
 # a private directory: a stray common.hpp beside the copy would shadow csrc's
 # (the quoted include searches the copy's own directory first)
 os.makedirs("/tmp/dal_k3trace", exist_ok=True)
