@@ -789,29 +789,40 @@ inline int64_t pairs_skip(int64_t P, int64_t a, int64_t b, int64_t skip_lo, int6
 }
 
 // Column-chunk count for the round-robin units: the fewest chunks, at least
-// kMinChunks, whose most loaded block has at most 8 % more pairs than the best
+// min_chunks, whose most loaded block has at most 8 % more pairs than the best
 // balance found (exact pair counts; cached per shape).  More chunks = a
 // smaller column working set swept by every block together (MALL hits; 2M x
-// 256: 16 chunks 3.9 % faster than 1), fewer = fewer A loads and row flushes.
+// 256: 16 chunks 3.9 % faster than 1; 4 and 8: 0.6 % slower), fewer = fewer A
+// loads and row flushes.  KS 64 with a column operand of <= DAL_GRAM_SMALL_MB
+// (in L2 + MALL whole) takes >= 2 chunks instead of the contiguous schedule:
+// 100k x 64 (25.6 MB) 1.6-4.7 % faster in two of three same-process runs
+// (+0.7 % in the third), the clock 1.83 -> 1.88-1.92 GHz; at KS 32 and 128 the
+// same change lost (60k x 32 +7.4 %, 20k x 256 +4.3 %; round 6,
+// profiles/r06/pmc/clock_ab_chunk_counts.txt).
 #ifndef DAL_GRAM_MIN_CHUNKS
 #define DAL_GRAM_MIN_CHUNKS 16
 #endif
-constexpr int64_t kMinChunks = DAL_GRAM_MIN_CHUNKS;
+#ifndef DAL_GRAM_SMALL_MB
+#define DAL_GRAM_SMALL_MB 32
+#endif
+#ifndef DAL_GRAM_MIN_CHUNKS_SMALL
+#define DAL_GRAM_MIN_CHUNKS_SMALL 2
+#endif
 // hv = super blocks per row unit (gram_csym_kernel W / 4); a two-super-block
 // unit costs the pairs of the busier one (they take the same column blocks but
 // near the diagonal).
 int64_t choose_chunks(int64_t srow0, int64_t n_srb, int64_t lo, int64_t hi, int64_t skip_lo, int64_t skip_hi,
-                      int64_t ns_active, int64_t G0, int hv) {
+                      int64_t ns_active, int64_t G0, int hv, int64_t kMinChunks) {
   struct Entry {
-    int64_t k[9];
+    int64_t k[10];
     int64_t nc;
   };
   static thread_local Entry cache[8] = {};
   static thread_local int cache_next = 0;
-  const int64_t key[9] = {srow0, n_srb, lo, hi, skip_lo, skip_hi, ns_active, G0, hv};
+  const int64_t key[10] = {srow0, n_srb, lo, hi, skip_lo, skip_hi, ns_active, G0, hv, kMinChunks};
   for (const Entry& e : cache) {
     bool hit = e.nc > 0;
-    for (int i = 0; i < 9 && hit; ++i) hit = e.k[i] == key[i];
+    for (int i = 0; i < 10 && hit; ++i) hit = e.k[i] == key[i];
     if (hit) return e.nc;
   }
   const int64_t n_ru = hv == 1 ? n_srb : 2 * ceil_div(n_srb, 4);
@@ -854,7 +865,7 @@ int64_t choose_chunks(int64_t srow0, int64_t n_srb, int64_t lo, int64_t hi, int6
   if (best_nc < 0) best_nc = cand.back().first;
   Entry& e = cache[cache_next];
   cache_next = (cache_next + 1) % 8;
-  for (int i = 0; i < 9; ++i) e.k[i] = key[i];
+  for (int i = 0; i < 10; ++i) e.k[i] = key[i];
   e.nc = best_nc;
   return best_nc;
 }
@@ -869,11 +880,13 @@ int64_t choose_chunks(int64_t srow0, int64_t n_srb, int64_t lo, int64_t hi, int6
 template <int KS, int W>
 int launch_csym_w(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint16_t* cols, int64_t jcol0,
                   int64_t j_lo, int64_t j_hi, int64_t skip_lo, int64_t skip_hi, int64_t ns_active, int64_t ldh,
-                  int slice_off, int64_t* acc, int grid_blocks, int contig, hipStream_t stream) {
+                  int slice_off, int64_t* acc, int grid_blocks, int contig, int64_t min_chunks,
+                  hipStream_t stream) {
   // grid_blocks counts 4-wave blocks (two per CU); 8-wave blocks are one per CU
   constexpr int kOcc = Cfg<KS, W>::OCC;
-  const int G0 = W == 4 ? (grid_blocks > 0 ? grid_blocks * kOcc / 2 : kOcc * device_cus())
-                        : (grid_blocks > 0 ? grid_blocks : 2 * device_cus()) * 4 / W * kOcc;
+  const int G0r = W == 4 ? (grid_blocks > 0 ? grid_blocks * kOcc / 2 : kOcc * device_cus())
+                         : (grid_blocks > 0 ? grid_blocks : 2 * device_cus()) * 4 / W * kOcc;
+  const int G0 = G0r > 0 ? G0r : 1;  // (a one-block grid in the 8-wave form)
   const int64_t nj = j_hi - j_lo;
   int64_t cbk = nj, n_chunks = 1, G;
   if (contig) {
@@ -883,7 +896,7 @@ int launch_csym_w(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint
     if (raw <= 0) return DAL_OK;
     G = raw < G0 ? raw : G0;
   } else {
-    const int64_t nc = choose_chunks(srow0, n_srb, j_lo, j_hi, skip_lo, skip_hi, ns_active, G0, W / 4);
+    const int64_t nc = choose_chunks(srow0, n_srb, j_lo, j_hi, skip_lo, skip_hi, ns_active, G0, W / 4, min_chunks);
     cbk = ceil_div(nj, nc);
     n_chunks = ceil_div(nj, cbk);
     const int64_t n_units = (W == 4 ? n_srb : 2 * ceil_div(n_srb, 4)) * n_chunks;
@@ -899,23 +912,30 @@ int launch_csym_w(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint
 }
 
 #ifndef DAL_GRAM_CONTIG_MB
-#define DAL_GRAM_CONTIG_MB 32  // column operands up to this size take the contiguous schedule
+#define DAL_GRAM_CONTIG_MB 32  // column operands up to this size take the contiguous schedule (KS 32, 128)
+#endif
+#ifndef DAL_GRAM_KS64_CHUNKED
+#define DAL_GRAM_KS64_CHUNKED 1  // ... KS 64 takes >= DAL_GRAM_MIN_CHUNKS_SMALL column chunks instead
 #endif
 template <int KS>
 int launch_csym(const uint16_t* rows, int64_t srow0, int64_t n_srb, const uint16_t* cols, int64_t jcol0,
                 int64_t j_lo, int64_t j_hi, int64_t skip_lo, int64_t skip_hi, int64_t ns_active, int64_t ldh,
                 int slice_off, int64_t* acc, int grid_blocks, hipStream_t stream) {
   // contiguous equal shares of the pair grid per block for a small column
-  // operand (<= 32 MB: 100k x 64 is 2-5 % faster), else round-robin column
-  // chunks whose blocks sweep the same column stages together.  Exact integer
-  // accumulation: the schedule never changes the bits.
-  const int contig = (j_hi - j_lo) * 256 * ldh * 2 <= (int64_t{DAL_GRAM_CONTIG_MB} << 20);
+  // operand (<= 32 MB at KS 32 / 128), else round-robin column chunks whose
+  // blocks sweep the same column stages together (a small KS-64 operand in as
+  // few as two chunks).  Exact integer accumulation: the schedule never
+  // changes the bits.
+  const int64_t col_bytes = (j_hi - j_lo) * 256 * ldh * 2;
+  const bool small = col_bytes <= (int64_t{DAL_GRAM_SMALL_MB} << 20);
+  const int contig = col_bytes <= (int64_t{DAL_GRAM_CONTIG_MB} << 20) && !(KS == 64 && DAL_GRAM_KS64_CHUNKED);
+  const int64_t min_chunks = small ? DAL_GRAM_MIN_CHUNKS_SMALL : DAL_GRAM_MIN_CHUNKS;
   if constexpr ((KS == 128 && DAL_GRAM_WAVES8) || (KS == 64 && DAL_GRAM_W8_KS64))
     if (!contig)
       return launch_csym_w<KS, 8>(rows, srow0, n_srb, cols, jcol0, j_lo, j_hi, skip_lo, skip_hi, ns_active, ldh,
-                                  slice_off, acc, grid_blocks, contig, stream);
+                                  slice_off, acc, grid_blocks, contig, min_chunks, stream);
   return launch_csym_w<KS, 4>(rows, srow0, n_srb, cols, jcol0, j_lo, j_hi, skip_lo, skip_hi, ns_active, ldh,
-                              slice_off, acc, grid_blocks, contig, stream);
+                              slice_off, acc, grid_blocks, contig, min_chunks, stream);
 }
 
 struct ResidualLayout {

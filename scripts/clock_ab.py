@@ -25,7 +25,7 @@ import bench  # noqa: E402
 from dal import _lib  # noqa: E402
 from clock_probe import bind, stamped  # noqa: E402
 
-ROUNDS = 3
+ROUNDS = int(os.environ.get("DAL_AB_ROUNDS", "3"))  # interleaved rounds per library
 
 
 def main():
