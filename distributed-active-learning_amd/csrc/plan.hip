@@ -31,7 +31,6 @@ struct PlanSlot {
 namespace {
 
 constexpr int kPlanThreads = 256;
-constexpr int kMarkBlocks = 512;  // fixed at capture: the list length varies per iteration
 
 // In-graph row marking: stamp[r] = step for every listed row of this pool;
 // the score kernel ORs DAL_ROW_CANDIDATE into the base flags where stamp[r] ==
@@ -41,8 +40,19 @@ constexpr int kMarkBlocks = 512;  // fixed at capture: the list length varies pe
 // publishes the step id for the score kernel.  Stamps are 8-bit (a quarter of
 // the bytes to write, and to write back from L2 before the score kernel):
 // step ids cycle through 1..255 and dal_dw_plan_run clears the stamps when
-// they wrap.  Four list entries per thread are loaded before their stores.
+// they wrap.  Four list entries per thread are loaded before their stores;
+// the grid (fixed at capture: the list length varies per iteration) covers a
+// list as long as the pool in one pass, so every load is in flight at once
+// (512 blocks looping over config 4's 2M rows: 9.8 us in the step).
 constexpr int kMarkPer = 4;
+#ifndef DAL_PLAN_MARK_BLOCKS
+#define DAL_PLAN_MARK_BLOCKS 0  // > 0: a fixed grid (rounds 3-5: 512)
+#endif
+inline unsigned mark_grid(int64_t n) {
+  const int64_t g = DAL_PLAN_MARK_BLOCKS > 0 ? DAL_PLAN_MARK_BLOCKS
+                                             : dal::ceil_div(n, static_cast<int64_t>(kPlanThreads) * kMarkPer);
+  return static_cast<unsigned>(g < 1 ? 1 : g > 65535 ? 65535 : g);
+}
 __global__ __launch_bounds__(kPlanThreads) void plan_mark_direct_kernel(const int64_t* __restrict__ idx, int64_t count,
                                                                         uint32_t step, int64_t row_base, int64_t n,
                                                                         uint8_t* __restrict__ stamp,
@@ -153,7 +163,7 @@ extern "C" int dal_dw_plan_create(const float* x, const float* xb, const void* f
   if (!rc && hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) rc = DAL_ERR_HIP;
   if (!rc && hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) != hipSuccess) rc = DAL_ERR_HIP;
   if (!rc) {
-    hipLaunchKernelGGL(plan_mark_direct_kernel, dim3(kMarkBlocks), dim3(kPlanThreads), 0, cs,
+    hipLaunchKernelGGL(plan_mark_direct_kernel, dim3(mark_grid(n)), dim3(kPlanThreads), 0, cs,
                        static_cast<const int64_t*>(nullptr), int64_t{0}, 0u, idx_base, n, p->stamp, p->step_dev);
     ForestStepHooks hooks;
     hooks.base_flags = base_flags;
