@@ -188,7 +188,7 @@ template <bool X_LDS, bool WROWS = false, int NW = kForestWaves, int ILP = kTree
 __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs, int xstride, int64_t tile, int R,
                                            int tpr, const int2* inner, const uint8_t* leaf, bool pre,
                                            uint8_t fl_pre, long long dens_pre, GroupFold& fold,
-                                           unsigned long long (*wmin)[2][NW]) {
+                                           unsigned long long (*wmin)[2][NW], const double* lut_s = nullptr) {
   static_assert(!BYTEA || (WROWS && X_LDS), "byte-addressed walks: the blocked kernel's LDS tiles only");
   constexpr int NT = NW * 64;  // threads of the block
   const int n_inner = (1 << A.depth) - 1;
@@ -259,7 +259,7 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
   if (live && sub == 0) {
     const uint8_t fl = pre ? fl_pre : A.flags ? row_flag(A, row) : DAL_ROW_CANDIDATE;
     if (A.hooks.base_flags && A.hooks.write_flags) const_cast<uint8_t*>(A.flags)[row] = fl;  // for later kernels
-    const double e = A.lut[v];
+    const double e = lut_s ? lut_s[v] : A.lut[v];  // (lut_s: the LUT in LDS, no dependent global load)
     double s, err = 0.0;
     if (A.dkind) {
       const long long draw = pre ? dens_pre : static_cast<const long long*>(A.density)[row];
@@ -547,6 +547,14 @@ __global__ __launch_bounds__(NW * 64) void forest_blocked_kernel(ForestArgs A, c
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (A.hooks.status_reset && blockIdx.x == 0 && tid == 0) *A.hooks.status_reset = 0;
+  // the score LUT (T + 1 doubles) in LDS after the forest region: the rows'
+  // epilogue looks the vote up there instead of a dependent global load
+  double* lut_s = reinterpret_cast<double*>(
+      (reinterpret_cast<uintptr_t>(PREP ? reinterpret_cast<unsigned char*>(fs) +
+                                              blocked_prep_layout(A.n_trees, A.depth, fu_max).payload
+                                        : reinterpret_cast<unsigned char*>(pre + nw)) +
+       7) & ~static_cast<uintptr_t>(7));
+  for (int i = tid; i <= A.n_trees; i += NT) lut_s[i] = A.lut[i];  // (read after the setup's barrier)
   int fu;
   if constexpr (PREP) {
     // the prepared payload -> LDS, 16 B per thread, kPrepBatch loads in flight
@@ -658,7 +666,7 @@ __global__ __launch_bounds__(NW * 64) void forest_blocked_kernel(ForestArgs A, c
     __syncthreads();
     if (tid == 0) issue_fold<NW>(A, fold, wmin);  // after this tile's DMA wait
     score_tile<true, true, NW, DAL_FOREST_BLOCKED_ILP, PREP && kByteWalk>(A, xs, 1, tile, kBlk, tpr, fs, ls, true,
-                                                                          fl_pre, dens_pre, fold, wmin);
+                                                                          fl_pre, dens_pre, fold, wmin, lut_s);
     __syncthreads();  // every wave done with the tile before the next one is staged
   }
   if (tid == 0) issue_fold<NW>(A, fold, wmin);
@@ -753,11 +761,14 @@ constexpr int kBlockedWavesWide = 8;
 #ifndef DAL_FOREST_BLOCKED_MAX_RUNS
 #define DAL_FOREST_BLOCKED_MAX_RUNS 256
 #endif
+// the score LUT after the forest region (8-B aligned: up to 7 bytes of slack)
+size_t blocked_lut_bytes(int32_t n_trees) { return static_cast<size_t>(n_trees + 1) * 8 + 8; }
 size_t blocked_smem(int fu_max, int64_t d, int32_t n_trees, int32_t depth) {
   const int64_t nn = static_cast<int64_t>(n_trees) * ((int64_t{1} << depth) - 1);
   return static_cast<size_t>(fu_max) * kBlk * 4 + static_cast<size_t>(nn) * 8 +
          static_cast<size_t>(round_up(static_cast<int64_t>(n_trees) << depth, 4)) +
-         static_cast<size_t>(round_up(fu_max, 2)) * 2 + static_cast<size_t>((d + 31) / 32) * 8;
+         static_cast<size_t>(round_up(fu_max, 2)) * 2 + static_cast<size_t>((d + 31) / 32) * 8 +
+         blocked_lut_bytes(n_trees);
 }
 int blocked_fu_max(int64_t d, int32_t n_trees, int32_t depth) {
   const int64_t nodes = static_cast<int64_t>(n_trees) * ((int64_t{1} << depth) - 1);
@@ -835,7 +846,8 @@ int forest_score_launch(const float* x, const float* xb, const void* fprep, int6
     const bool pr = fprep != nullptr;
     // prepared: the forest region holds the payload only (no bitmap / prefix counts)
     const size_t smem = pr ? static_cast<size_t>(fu_max) * kBlk * 4 +
-                                 static_cast<size_t>(blocked_prep_layout(n_trees, depth, fu_max).payload)
+                                 static_cast<size_t>(blocked_prep_layout(n_trees, depth, fu_max).payload) +
+                                 blocked_lut_bytes(n_trees)
                            : blocked_smem(fu_max, d, n_trees, depth);
     const bool wide = smem > (160u << 10) / 3;  // at most two blocks per CU by LDS: 8-wave blocks
     const int nw = wide ? kBlockedWavesWide : kBlockedWaves;
