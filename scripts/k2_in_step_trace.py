@@ -4,7 +4,7 @@ steps (dal_dw_step: group-minima fold, stored row flags), 5 warm-plan
 replays (hipGraph: the fold plus the stamp-derived row flags), 5 eager steps
 with the exact level 1 (no fold).  Analyse with
 --analyse DIR: per kernel name and phase, the median duration.
-usage: python scripts/k2_in_step_trace.py [CONFIG]   |   --analyse DIR"""
+usage: [K2_LIB=path] python scripts/k2_in_step_trace.py [CONFIG]   |   --analyse DIR"""
 import glob
 import os
 import statistics
@@ -36,8 +36,11 @@ def main():
     import numpy as np
     import torch
 
+    from dal import _lib
+    if os.environ.get("K2_LIB"):  # an A/B build in place of the product library
+        _lib.LIB_PATH = os.path.abspath(os.environ["K2_LIB"])
     import bench
-    from dal import _lib, engine
+    from dal import engine
     if os.environ.get("DAL_AB_LIB"):  # an A/B build in place of the product library
         import ctypes
 
