@@ -669,11 +669,16 @@ __device__ __forceinline__ float bf16f(uint16_t b) { return __uint_as_float(stat
 // u_i = x_i / sqrt(sum_f x_if^2) (sequential), cos_il = sum_f u_if * ulab_lf
 // (sequential in f, no FMA), max over l, ties -> lowest l.  A block takes
 // kRrC candidates: their unit rows are computed once into LDS, then each
-// lane carries kRrC x kRrJ independent accumulators over labeled rows
+// lane carries kRrC x kRrJ independent fp32 accumulators over labeled rows
 // l = lane + 64 * (wave + 4 j) (+ 1024 per outer pass), reading the
-// feature-major table ulabT[f * m + l] coalesced; the per-(c, l) sums keep
-// the canonical sequential order in f.
-constexpr int kRrC = 4;  // candidates per block (8 measured 92 vs 77 us at config 5: fewer blocks)
+// feature-major table ulabT[f * m + l] coalesced.  Only the rows whose fp32
+// dot lies within 2 B of the candidate's fp32 maximum get the canonical fp64
+// sum (round 6: every row's fp64 sum before, 1.5 M sequential 128-step chains
+// per config-5 call).
+#ifndef DAL_RR_CANDS
+#define DAL_RR_CANDS 4  // candidates per block (8 measured 92 vs 77 us at config 5 with fp64 dots: fewer blocks)
+#endif
+constexpr int kRrC = DAL_RR_CANDS;
 constexpr int kRrJ = 4;
 __global__ __launch_bounds__(256) void rerank_maxcos_kernel(const TopkHdr* __restrict__ h, int64_t idx_base,
                                                             const uint16_t* __restrict__ pool, int d,
@@ -683,6 +688,9 @@ __global__ __launch_bounds__(256) void rerank_maxcos_kernel(const TopkHdr* __res
                                                             double* __restrict__ cpay, int64_t cap,
                                                             bool cap_miss, int32_t* __restrict__ status) {
   __shared__ double su[256][kRrC];  // [f][candidate]
+  __shared__ float sf[256][kRrC];
+  __shared__ float s_m32[4][kRrC];
+  __shared__ __attribute__((aligned(16))) double s_tr[4][64];
   __shared__ double rb[4][kRrC];
   __shared__ long long ra[4][kRrC];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -707,6 +715,67 @@ __global__ __launch_bounds__(256) void rerank_maxcos_kernel(const TopkHdr* __res
     }
   }
   __syncthreads();
+  // fp32 copies of the unit rows: every (candidate, labeled row) dot first in
+  // fp32 (FMA chains), then the canonical fp64 sum only for the labeled rows
+  // within 2 B of the candidate's fp32 maximum.  |fp32 dot - canonical| <= B
+  // for unit rows at d <= 256 (d 2^-24 for the chain, 2^-23 for the operands'
+  // rounding to fp32, < 1e-13 for the canonical fp64 sum: B = 2^-16 holds
+  // with a 2x margin), so every row reaching the canonical maximum is among
+  // them and the (value, lowest row) result is the full scan's.
+  for (int e = tid; e < d * kRrC; e += 256) sf[e / kRrC][e % kRrC] = static_cast<float>(su[e / kRrC][e % kRrC]);
+  __syncthreads();
+  const bool one = m <= 256 * kRrJ;  // one chunk of labeled rows: the fp32 dots stay in registers
+  float a[kRrC][kRrJ];
+  int64_t l[kRrJ];
+  bool ok[kRrJ];
+  auto chunk = [&](int64_t lb) {
+#pragma unroll
+    for (int j = 0; j < kRrJ; ++j) {
+      l[j] = lb + lane + 64 * (wave + 4 * j);
+      ok[j] = l[j] < m;
+      if (!ok[j]) l[j] = m - 1;
+    }
+#pragma unroll
+    for (int q = 0; q < kRrC; ++q)
+#pragma unroll
+      for (int j = 0; j < kRrJ; ++j) a[q][j] = 0.f;
+#pragma unroll 4
+    for (int f = 0; f < d; ++f) {
+      float ul[kRrJ];
+#pragma unroll
+      for (int j = 0; j < kRrJ; ++j) ul[j] = static_cast<float>(ulabT[static_cast<int64_t>(f) * m + l[j]]);
+#pragma unroll
+      for (int q = 0; q < kRrC; ++q) {
+        const float uq = sf[f][q];
+#pragma unroll
+        for (int j = 0; j < kRrJ; ++j) a[q][j] = __builtin_fmaf(uq, ul[j], a[q][j]);
+      }
+    }
+  };
+  float m32[kRrC];
+#pragma unroll
+  for (int q = 0; q < kRrC; ++q) m32[q] = -__builtin_inff();
+  for (int64_t lb = 0; lb < m; lb += 256 * kRrJ) {
+    chunk(lb);
+#pragma unroll
+    for (int j = 0; j < kRrJ; ++j)
+#pragma unroll
+      for (int q = 0; q < kRrC; ++q)
+        if (ok[j]) m32[q] = __builtin_fmaxf(m32[q], a[q][j]);
+  }
+#pragma unroll
+  for (int q = 0; q < kRrC; ++q) {
+    for (int o = 32; o > 0; o >>= 1) m32[q] = __builtin_fmaxf(m32[q], __shfl_xor(m32[q], o));
+    if (lane == 0) s_m32[wave][q] = m32[q];
+  }
+  __syncthreads();
+  constexpr float kNear = 0x1p-15f;  // 2 B
+  float thr[kRrC];
+#pragma unroll
+  for (int q = 0; q < kRrC; ++q)  // (a slot past the candidates -- zero unit row -- takes no pair)
+    thr[q] = c0 + q < count ? __builtin_fmaxf(__builtin_fmaxf(s_m32[0][q], s_m32[1][q]),
+                                              __builtin_fmaxf(s_m32[2][q], s_m32[3][q])) - kNear
+                            : __builtin_inff();
   double best[kRrC];
   long long arg[kRrC];
 #pragma unroll
@@ -714,39 +783,49 @@ __global__ __launch_bounds__(256) void rerank_maxcos_kernel(const TopkHdr* __res
     best[q] = -__builtin_inf();
     arg[q] = 0x7FFFFFFFFFFFFFFFll;
   }
+  // a near (candidate, labeled row) pair: its canonical sum by the whole
+  // wave -- lane f's rounded products u_if * u_lf with every load in flight,
+  // then the sequential sum over f through the wave's LDS slot (the products'
+  // rounding and the adds' order are the canonical ones)
+  auto canon_dot = [&](int q, int64_t lr) -> double {
+    double p[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int f = 64 * c + lane;
+      p[c] = f < d ? su[f][q] * ulabT[static_cast<int64_t>(f) * m + lr] : 0.0;
+    }
+    double acc = 0.0;
+    double* tr = s_tr[wave];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int rest = __builtin_amdgcn_readfirstlane(d - 64 * c);
+      if (rest <= 0) break;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      tr[lane] = p[c];
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const int cnt = rest < 64 ? rest : 64;
+      for (int f = 0; f < cnt; ++f) acc = acc + tr[f];
+    }
+    return acc;
+  };
   for (int64_t lb = 0; lb < m; lb += 256 * kRrJ) {
-    int64_t l[kRrJ];
-    bool ok[kRrJ];
-#pragma unroll
-    for (int j = 0; j < kRrJ; ++j) {
-      l[j] = lb + lane + 64 * (wave + 4 * j);
-      ok[j] = l[j] < m;
-      if (!ok[j]) l[j] = m - 1;
-    }
-    double acc[kRrC][kRrJ];
-#pragma unroll
-    for (int q = 0; q < kRrC; ++q)
-#pragma unroll
-      for (int j = 0; j < kRrJ; ++j) acc[q][j] = 0.0;
-    for (int f = 0; f < d; ++f) {
-      double ul[kRrJ];
-#pragma unroll
-      for (int j = 0; j < kRrJ; ++j) ul[j] = ulabT[static_cast<int64_t>(f) * m + l[j]];
-#pragma unroll
-      for (int q = 0; q < kRrC; ++q) {
-        const double uq = su[f][q];
-#pragma unroll
-        for (int j = 0; j < kRrJ; ++j) acc[q][j] = acc[q][j] + uq * ul[j];
-      }
-    }
-    // l increases with j: strict > keeps the lowest l among equal values
+    if (!one) chunk(lb);  // (one chunk: its dots are still in a)
 #pragma unroll
     for (int j = 0; j < kRrJ; ++j) {
 #pragma unroll
       for (int q = 0; q < kRrC; ++q) {
-        if (ok[j] && acc[q][j] > best[q]) {
-          best[q] = acc[q][j];
-          arg[q] = l[j];
+        unsigned long long near = __ballot(ok[j] && a[q][j] >= thr[q]);
+        while (near) {  // (wave-uniform)
+          const int src = __ffsll(static_cast<long long>(near)) - 1;
+          near &= near - 1;
+          const int64_t lr = static_cast<int64_t>(__shfl(l[j], src));
+          const double acc = canon_dot(q, lr);
+          if (acc > best[q] || (acc == best[q] && lr < arg[q])) {  // (wave-uniform)
+            best[q] = acc;
+            arg[q] = lr;
+          }
         }
       }
     }

@@ -60,7 +60,8 @@ def test_max_cosine_argmax_duplicate_labeled_rows(cuda, d):
     assert (ref_arg[1000:1010] == 5).all()  # first of the duplicated positions
 
 
-@pytest.mark.parametrize("n,d,m,k", [(4000, 128, 256, 50), (3000, 64, 700, 200), (2000, 256, 64, 1)])
+@pytest.mark.parametrize("n,d,m,k", [(4000, 128, 256, 50), (3000, 64, 700, 200), (2000, 256, 64, 1),
+                                     (4500, 64, 1500, 50)])  # m > 1024: the re-rank's fp32 dots per chunk
 def test_diversity_select_bit_exact(cuda, n, d, m, k):
     from dal import similarity as sim
 
