@@ -266,16 +266,18 @@ __global__ __launch_bounds__(256) void mark_rows_kernel(const int64_t* __restric
 }
 
 // The same marking, grid-stride over a bounded grid, counting the indices that
-// fall inside the shard (one atomic per block, at most 2048 same-address
-// atomics: 8192 blocks measured 100 us at 8M indices, 2048 40 us, 512 47 us).
-__global__ __launch_bounds__(256) void mark_rows_count_kernel(const int64_t* __restrict__ idx, int64_t count,
+// fall inside the shard (one atomic per block: the same-address atomics bound
+// it -- 8192 256-thread blocks measured 100 us at 8M indices, 2048 40 us, 512
+// 47 us -- so the blocks are 1,024 threads, at most 512 of them).
+constexpr int kMarkThreads = 1024;
+__global__ __launch_bounds__(kMarkThreads) void mark_rows_count_kernel(const int64_t* __restrict__ idx, int64_t count,
                                                               int64_t row_base, int64_t n, unsigned bits,
                                                               uint8_t* __restrict__ flags,
                                                               int32_t* __restrict__ in_range) {
   int c = 0;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kMarkThreads;
   // 4 index loads in flight per thread before the flag writes
-  for (int64_t t0 = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; t0 < count; t0 += 4 * stride) {
+  for (int64_t t0 = static_cast<int64_t>(blockIdx.x) * kMarkThreads + threadIdx.x; t0 < count; t0 += 4 * stride) {
     int64_t r[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -290,12 +292,13 @@ __global__ __launch_bounds__(256) void mark_rows_count_kernel(const int64_t* __r
       }
     }
   }
-  __shared__ int part[4];
+  __shared__ int part[kMarkThreads / 64];
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int b = part[0] + part[1] + part[2] + part[3];
+    int b = 0;
+    for (int w = 0; w < kMarkThreads / 64; ++w) b += part[w];
     if (b) atomicAdd(in_range, b);
   }
 }
@@ -312,8 +315,8 @@ extern "C" int dal_mark_rows_count(const int64_t* idx, int64_t count, int64_t ro
   hipStream_t st = as_stream(stream);
   if (hipMemsetAsync(in_range, 0, sizeof(int32_t), st) != hipSuccess) return DAL_ERR_HIP;
   if (count == 0) return DAL_OK;
-  const int64_t blocks = std::min<int64_t>(ceil_div(count, 256), 2048);
-  hipLaunchKernelGGL(mark_rows_count_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, idx, count,
+  const int64_t blocks = std::min<int64_t>(ceil_div(count, kMarkThreads), 512);
+  hipLaunchKernelGGL(mark_rows_count_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kMarkThreads), 0, st, idx, count,
                      row_base, n, static_cast<unsigned>(bits), flags, in_range);
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;

@@ -2416,16 +2416,37 @@ extern "C" int dal_maxcos_select(const uint64_t* keys_lo, const uint64_t* keys_h
 
 // Interval keys of fp32 values: lo/hi = keys of the pessimistic/optimistic
 // ends of [v - err, v + err] for ``order``; DAL_KEY_NONE for non-candidates.
+// Four rows per thread: one 16-B value load, one 4-B flag load and 16-B key
+// stores (vec4: v, flags, lo and hi 16-B aligned; the last rows one by one).
+__device__ __forceinline__ void interval_key_row(float v, bool cand, double err, int order, uint64_t& lo,
+                                                 uint64_t& hi) {
+  const double s = static_cast<double>(v);
+  lo = cand ? score_key(pessimistic(s, err, order), order) : DAL_KEY_NONE;
+  hi = cand ? score_key(optimistic(s, err, order), order) : DAL_KEY_NONE;
+}
 __global__ __launch_bounds__(256) void interval_keys_f32_kernel(const float* __restrict__ v, int64_t n,
                                                                 double err, const uint8_t* __restrict__ flags,
                                                                 int order, uint64_t* __restrict__ lo,
-                                                                uint64_t* __restrict__ hi) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  if (i >= n) return;
-  const bool cand = flags ? (flags[i] & DAL_ROW_CANDIDATE) : true;
-  const double s = static_cast<double>(v[i]);
-  lo[i] = cand ? score_key(pessimistic(s, err, order), order) : DAL_KEY_NONE;
-  hi[i] = cand ? score_key(optimistic(s, err, order), order) : DAL_KEY_NONE;
+                                                                uint64_t* __restrict__ hi, bool vec4) {
+  const int64_t i0 = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 4;
+  if (i0 >= n) return;
+  if (vec4 && i0 + 4 <= n) {
+    const float4 x = *reinterpret_cast<const float4*>(v + i0);
+    const unsigned fw = flags ? *reinterpret_cast<const unsigned*>(flags + i0) : ~0u;
+    const float xv[4] = {x.x, x.y, x.z, x.w};
+    uint64_t l[4], h[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) interval_key_row(xv[j], (fw >> (8 * j)) & DAL_ROW_CANDIDATE, err, order, l[j], h[j]);
+    reinterpret_cast<ulonglong2*>(lo + i0)[0] = make_ulonglong2(l[0], l[1]);
+    reinterpret_cast<ulonglong2*>(lo + i0)[1] = make_ulonglong2(l[2], l[3]);
+    reinterpret_cast<ulonglong2*>(hi + i0)[0] = make_ulonglong2(h[0], h[1]);
+    reinterpret_cast<ulonglong2*>(hi + i0)[1] = make_ulonglong2(h[2], h[3]);
+    return;
+  }
+  for (int64_t i = i0; i < i0 + 4 && i < n; ++i) {
+    const bool cand = flags ? (flags[i] & DAL_ROW_CANDIDATE) : true;
+    interval_key_row(v[i], cand, err, order, lo[i], hi[i]);
+  }
 }
 
 extern "C" int dal_interval_keys_f32(const float* values, int64_t n, double err, const uint8_t* row_flags,
@@ -2433,8 +2454,11 @@ extern "C" int dal_interval_keys_f32(const float* values, int64_t n, double err,
   if (!values || !keys_lo || !keys_hi) return DAL_ERR_ARG;
   if (order != DAL_ASCENDING && order != DAL_DESCENDING) return DAL_ERR_ARG;
   if (n < 1 || !(err > 0.0)) return DAL_ERR_SHAPE;
-  hipLaunchKernelGGL(interval_keys_f32_kernel, dim3(static_cast<unsigned>(ceil_div(n, 256))), dim3(256), 0,
-                     as_stream(stream), values, n, err, row_flags, order, keys_lo, keys_hi);
+  const bool vec4 = reinterpret_cast<uintptr_t>(values) % 16 == 0 && reinterpret_cast<uintptr_t>(keys_lo) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(keys_hi) % 16 == 0 &&
+                    (!row_flags || reinterpret_cast<uintptr_t>(row_flags) % 4 == 0);
+  hipLaunchKernelGGL(interval_keys_f32_kernel, dim3(static_cast<unsigned>(ceil_div(n, 1024))), dim3(256), 0,
+                     as_stream(stream), values, n, err, row_flags, order, keys_lo, keys_hi, vec4);
   DAL_RETURN_IF_LAUNCH_FAILED();
   return DAL_OK;
 }
