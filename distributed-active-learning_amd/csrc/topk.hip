@@ -968,7 +968,10 @@ struct RegionMap {
 };
 
 constexpr int64_t kSelMin = 1024;    // below this the full bitonic is cheap
-constexpr int64_t kRankMax = 512;    // at most this many: rank selection, no sorting network
+#ifndef DAL_RANK_MAX
+#define DAL_RANK_MAX 512
+#endif
+constexpr int64_t kRankMax = DAL_RANK_MAX;  // at most this many: rank selection, no sorting network
 
 constexpr int64_t kSelMaxK = 1536;   // k + kSelSmall must fit the sort arrays
 constexpr int kSelSmall = 512;

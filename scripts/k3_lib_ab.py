@@ -4,7 +4,7 @@ libdal.so: AB_BASE (default ab/k3_base/libdal.so) and the in-tree library,
 switched by rebinding dal._lib between calls.  Per shape: selections
 (indices + fp64 score bits) must be identical; then back-to-back calls
 between two HIP events, interleaved A/B, median of the rounds.
-usage: python scripts/k3_lib_ab.py [--base PATH] [NxD[xT][:kK] ...]"""
+usage: python scripts/k3_lib_ab.py [--base PATH] [--new PATH] [NxD[xT][:kK] ...]"""
 import ctypes
 import os
 import statistics
@@ -35,9 +35,15 @@ def bind(path):
 
 args = sys.argv[1:]
 base = os.environ.get("AB_BASE", os.path.join(REPO, "ab", "k3_base", "libdal.so"))
-if args[:1] == ["--base"]:  # (instead of AB_BASE)
-    base, args = args[1] if os.path.isabs(args[1]) else os.path.join(REPO, args[1]), args[2:]
-libs = {"base": bind(base), "new": bind(_lib.LIB_PATH)}
+new = _lib.LIB_PATH
+while args[:1] in (["--base"], ["--new"]):  # (--base instead of AB_BASE; --new instead of the in-tree library)
+    path = args[1] if os.path.isabs(args[1]) else os.path.join(REPO, args[1])
+    if args[0] == "--base":
+        base = path
+    else:
+        new = path
+    args = args[2:]
+libs = {"base": bind(base), "new": bind(new)}
 dev = torch.device("cuda:0")
 for spec in args or ["100000x64", "2000000x256", "284807x30x100", "2000000x256:k1000"]:
     sh, _, kk = spec.partition(":k")
