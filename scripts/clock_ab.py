@@ -87,6 +87,7 @@ def main():
         for name, lib in libs.items():
             _lib._lib = lib
             res[name].append(stamped(lib, launcher(name), max_blocks))
+            print(f"round {r} {name}: {res[name][-1]['launch_ms']:.4f} ms", flush=True)  # (progress)
     torch.cuda.synchronize()
     ref = next(iter(libs))
     ref_out = result(ref).clone()
