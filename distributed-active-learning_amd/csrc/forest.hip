@@ -123,6 +123,34 @@ __device__ __forceinline__ void issue_fold(const ForestArgs& A, GroupFold& f,
   f.tile = -1;
 }
 
+// The minimum of a u64 over the wave, on every lane: a prefix minimum by DPP
+// row shifts (1, 2, 4, 8) and row broadcasts (15, 31) -- lane 63 ends with the
+// total -- instead of six 64-bit ds_bpermute exchanges (two LDS round trips
+// each, on the rows' epilogue wave of every tile).  Out-of-row sources and
+// rows outside the mask read the identity (~0).
+#ifndef DAL_FOREST_DPP_MIN
+#define DAL_FOREST_DPP_MIN 1
+#endif
+template <int CTRL, int ROWS>
+__device__ __forceinline__ unsigned long long dpp_min_step(unsigned long long v) {
+  const int lo = __builtin_amdgcn_update_dpp(-1, static_cast<int>(v), CTRL, ROWS, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(-1, static_cast<int>(v >> 32), CTRL, ROWS, 0xf, false);
+  const unsigned long long t =
+      (static_cast<unsigned long long>(static_cast<unsigned>(hi)) << 32) | static_cast<unsigned>(lo);
+  return t < v ? t : v;
+}
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+  v = dpp_min_step<0x111, 0xf>(v);  // row_shr:1
+  v = dpp_min_step<0x112, 0xf>(v);  // row_shr:2
+  v = dpp_min_step<0x114, 0xf>(v);  // row_shr:4
+  v = dpp_min_step<0x118, 0xf>(v);  // row_shr:8: lane 15 of each row holds the row's minimum
+  v = dpp_min_step<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+  v = dpp_min_step<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3: lane 63 holds the total
+  const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+  const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(v >> 32), 63));
+  return (static_cast<unsigned long long>(hi) << 32) | lo;
+}
+
 // Votes, score and keys of tile `tile` (R rows from LDS or global memory),
 // and the tile's minimum keys folded into its row group (hooks.gmin).  With
 // several blocks per group in the persistent kernel (wmin non-null) the
@@ -289,11 +317,16 @@ __device__ __forceinline__ void score_tile(const ForestArgs& A, const float* xs,
   // the block's minimum keys -> its row group (the top-k's fast level 1);
   // with rows on wave lanes (wr) only the row leaders' wave (sub 0) holds keys
   if (!wr || sub == 0) {  // (wave-uniform)
+#if DAL_FOREST_DPP_MIN
+    klo = wave_min_u64(klo);
+    khi = wave_min_u64(khi);
+#else
     for (int o = 32; o > 0; o >>= 1) {
       const unsigned long long a = __shfl_xor(klo, o), b = __shfl_xor(khi, o);
       klo = a < klo ? a : klo;
       khi = b < khi ? b : khi;
     }
+#endif
   }
   if (wmin && A.hooks.group_blocks > 1) {  // kernel-uniform
     if ((tid & 63) == 0) {
