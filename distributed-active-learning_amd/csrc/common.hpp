@@ -106,6 +106,41 @@ __device__ __forceinline__ unsigned long long pack_hint(unsigned long long key, 
   return (key & ~kHintMask) | o;
 }
 
+// Wave reductions by DPP, the result on every lane: a prefix by row shifts
+// (1, 2, 4, 8) and row broadcasts (15, 31) leaves the total in lane 63, read
+// back as a scalar.  Sources outside the row (shifts) or rows outside the mask
+// (broadcasts) read the identity.  Six dependent VALU steps instead of six
+// ds_bpermute exchanges (two per 64-bit value) through the LDS pipe.
+template <int CTRL, int ROWS, class Op>
+__device__ __forceinline__ unsigned long long dpp_step_u64(unsigned long long v, unsigned long long id, Op op) {
+  const int lo = __builtin_amdgcn_update_dpp(static_cast<int>(id), static_cast<int>(v), CTRL, ROWS, 0xf, false);
+  const int hi =
+      __builtin_amdgcn_update_dpp(static_cast<int>(id >> 32), static_cast<int>(v >> 32), CTRL, ROWS, 0xf, false);
+  return op(v, (static_cast<unsigned long long>(static_cast<unsigned>(hi)) << 32) | static_cast<unsigned>(lo));
+}
+template <class Op>
+__device__ __forceinline__ unsigned long long wave_reduce_u64(unsigned long long v, unsigned long long id, Op op) {
+  v = dpp_step_u64<0x111, 0xf>(v, id, op);  // row_shr:1
+  v = dpp_step_u64<0x112, 0xf>(v, id, op);  // row_shr:2
+  v = dpp_step_u64<0x114, 0xf>(v, id, op);  // row_shr:4
+  v = dpp_step_u64<0x118, 0xf>(v, id, op);  // row_shr:8
+  v = dpp_step_u64<0x142, 0xa>(v, id, op);  // row_bcast:15
+  v = dpp_step_u64<0x143, 0xc>(v, id, op);  // row_bcast:31
+  const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+  const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(v >> 32), 63));
+  return (static_cast<unsigned long long>(hi) << 32) | lo;
+}
+__device__ __forceinline__ unsigned long long wave_min_u64_dpp(unsigned long long v) {
+  return wave_reduce_u64(v, ~0ull, [](unsigned long long a, unsigned long long b) { return b < a ? b : a; });
+}
+__device__ __forceinline__ unsigned long long wave_max_u64_dpp(unsigned long long v) {
+  return wave_reduce_u64(v, 0ull, [](unsigned long long a, unsigned long long b) { return b > a ? b : a; });
+}
+__device__ __forceinline__ unsigned wave_sum_u32_dpp(unsigned v) {
+  return static_cast<unsigned>(
+      wave_reduce_u64(v, 0ull, [](unsigned long long a, unsigned long long b) { return a + b; }));
+}
+
 // Internal hooks of dal_dw_step into dal_forest_score's kernel (forest.hip):
 //   status_reset (nullable) is zeroed by the first thread, before any later
 //                kernel of the step can raise a flag (a replayed step starts clean);

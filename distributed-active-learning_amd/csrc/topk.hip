@@ -972,6 +972,11 @@ constexpr int64_t kSelMin = 1024;    // below this the full bitonic is cheap
 #define DAL_RANK_MAX 512
 #endif
 constexpr int64_t kRankMax = DAL_RANK_MAX;  // at most this many: rank selection, no sorting network
+// wave min / max / count reductions of the selection's critical path by DPP
+// (common.hpp) instead of ds_bpermute shuffles
+#ifndef DAL_K3_DPP
+#define DAL_K3_DPP 1
+#endif
 
 constexpr int64_t kSelMaxK = 1536;   // k + kSelSmall must fit the sort arrays
 constexpr int kSelSmall = 512;
@@ -1014,11 +1019,16 @@ __device__ bool select_compact(const uint64_t* __restrict__ keys, const int64_t*
       mx = key[j] > mx ? key[j] : mx;
     }
   }
+#if DAL_K3_DPP
+  mn = wave_min_u64_dpp(mn);
+  mx = wave_max_u64_dpp(mx);
+#else
   for (int o = 32; o > 0; o >>= 1) {
     const unsigned long long a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
     mn = a < mn ? a : mn;
     mx = b > mx ? b : mx;
   }
+#endif
   if (lane == 0) {
     s_mn[tid >> 6] = mn;
     s_mx[tid >> 6] = mx;
@@ -1178,10 +1188,14 @@ __device__ void sort_tail_body(const uint64_t* __restrict__ keys, const int64_t*
       const bool miss = __ballot(over) != 0 || x > 0xFFFFFFFFull;
       const bool all_sorted = smax > 0 && __ballot(unsorted) == 0;
       unsigned long long cm = c0 > c1 ? c0 : c1;  // the longest region
+#if DAL_K3_DPP
+      cm = wave_max_u64_dpp(cm);
+#else
       for (int o = 32; o > 0; o >>= 1) {
         const unsigned long long y = __shfl_xor(cm, o);
         cm = y > cm ? y : cm;
       }
+#endif
       if (tid == 63) {
         s_run_max = static_cast<int>(cm);
         s_pre[tail.n_reg] = miss ? 0xFFFFFFFFu : static_cast<unsigned>(x);
@@ -1589,12 +1603,18 @@ __device__ unsigned long long group_threshold(const GroupSummary& S, int64_t k, 
       ++nv;
     }
   }
+#if DAL_K3_DPP
+  mn = wave_min_u64_dpp(mn);
+  mx = wave_max_u64_dpp(mx);
+  nv = wave_sum_u32_dpp(nv);
+#else
   for (int o = 32; o > 0; o >>= 1) {
     const unsigned long long a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
     mn = a < mn ? a : mn;
     mx = b > mx ? b : mx;
     nv += __shfl_xor(nv, o);
   }
+#endif
   if (lane == 0) {
     s_mn[w] = mn;
     s_mx[w] = mx;
