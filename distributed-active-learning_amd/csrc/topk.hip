@@ -1746,11 +1746,16 @@ __global__ __launch_bounds__(256) void group_min_kernel(const uint64_t* __restri
       hi = cj < hi ? cj : hi;
     }
   }
+#if DAL_K3_DPP
+  lo = wave_min_u64_dpp(lo);
+  hi = wave_min_u64_dpp(hi);
+#else
   for (int o = 32; o > 0; o >>= 1) {
     const unsigned long long a = __shfl_xor(lo, o), c = __shfl_xor(hi, o);
     lo = a < lo ? a : lo;
     hi = c < hi ? c : hi;
   }
+#endif
   if (lane == 0) {
     ginv[g] = ~lo;
     ginv[ng + g] = ~hi;
